@@ -1,0 +1,345 @@
+#!/usr/bin/env python3
+"""bench.py -- device-resident AES-GCM seal+open throughput of the MI355X engine (BASELINE.json metric).
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c4|c5]
+
+One step = seal of the whole per-GPU batch followed by open of the sealed batch (the BASELINE metric is
+"seal+open"), inputs already resident in HBM.  Default workload = BASELINE.json configs[1]
+("c2": 1M x 16 KiB TLS records, AES-128-GCM, one key) on every GPU: records are sharded by range,
+each rank owns its own 1M records (weak scaling), no collective touches the data path; ranks only
+meet at the barriers and the max-over-ranks of the timed region.
+
+Rank 0 prints ONE JSON line.  value = whole-job GiB/s = sum over ranks of 2 * sum(L) per step / time.
+Extra fields: roofline (seal kernel vs the 8 TB/s HBM peak), cpu_baseline (lib/fusion.c on this host's
+cores, oracle/_ref), parity (sampled records vs the golden digests of lib/fusion.c + full open check).
+"""
+import argparse
+import hashlib
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "hsig-picotls_amd"))
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+GIB = float(1 << 30)
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E, /opt/skills/guides/MI355X_MICROARCH.md chip table
+
+SEED_DATA = 0x70746C7300000001
+SEED_KEY = 0x6B65790000000000
+SEED_AAD = 0x6161640000000000
+SEED_LEN = 0x00000000006C656E
+GAMMA = np.uint64(0x9E3779B97F4A7C15)
+
+CONFIGS = {  # SURVEY.md §8(d); n = records per GPU
+    "c2": dict(n=1 << 20, L=16384, key_len=16, keys=1, aad="tls",
+               desc="AES-128-GCM, 1M x 16 KiB TLS records, single key, per GPU (BASELINE configs[1])"),
+    "c3": dict(n=4 << 20, L=1350, key_len=16, keys=1, aad="quic",
+               desc="AES-128-GCM, 4M x 1350 B QUIC records, 13 B AAD, single key (configs[2])"),
+    "c4": dict(n=4 << 20, L=None, key_len=32, keys=1 << 16, aad="tls",
+               desc="AES-256-GCM, 4M mixed 64 B-16 KiB records, 64K keys (configs[3])"),
+    "c5": dict(n=4 << 20, L=1350, key_len=16, keys=1, aad="quic",
+               desc="AES-128-GCM, 32M x 1350 B records sharded 4M per GPU over 8 GPUs (configs[4])"),
+}
+
+
+def splitmix_at(seed, k):
+    """k-th output of the splitmix64 stream seeded with `seed` (vectorised over seed and/or k)"""
+    with np.errstate(over="ignore"):
+        z = np.asarray(seed, dtype=np.uint64) + (np.asarray(k, dtype=np.uint64) + np.uint64(1)) * GAMMA
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        return z ^ (z >> np.uint64(31))
+
+
+def stream_bytes(seeds, nbytes):
+    """[len(seeds), nbytes] uint8: the first nbytes of each seed's stream"""
+    seeds = np.asarray(seeds, dtype=np.uint64)
+    words = (nbytes + 7) // 8
+    w = splitmix_at(seeds[:, None], np.arange(words, dtype=np.uint64)[None, :])
+    return w.astype("<u8").view(np.uint8).reshape(len(seeds), words * 8)[:, :nbytes]
+
+
+def make_workload(cfg, rank):
+    """per-rank record descriptors, in key-major order (records of one key adjacent)"""
+    import ptls_hip
+    n = cfg["n"]
+    base = rank * n
+    if cfg["keys"] == 1:
+        idx = np.arange(base, base + n, dtype=np.uint64)
+        keyslot = np.zeros(n, dtype=np.uint32)
+        seq = idx.copy()
+    else:  # record i uses key i % K, per-key seq i // K; order records by key
+        K = cfg["keys"]
+        per = n // K
+        kk = np.repeat(np.arange(K, dtype=np.uint64), per)
+        ss = np.tile(np.arange(per, dtype=np.uint64), K)
+        idx = np.uint64(base) + ss * np.uint64(K) + kk
+        keyslot = kk.astype(np.uint32)
+        seq = (idx // np.uint64(K)).astype(np.uint64)
+    if cfg["L"] is None:
+        lens = (np.uint64(64) + splitmix_at(np.uint64(SEED_LEN) ^ idx, 0) % np.uint64(16321)).astype(np.uint64)
+    else:
+        lens = np.full(n, cfg["L"], dtype=np.uint64)
+    aad_len = 5 if cfg["aad"] == "tls" else 13
+    recs, in_total, out_total, _ = ptls_hip.layout_records(lens, np.full(n, aad_len), keyslot, seq, align=16)
+    recs["aad_off"] = np.arange(n, dtype=np.uint64) * np.uint64(16)
+    return idx, recs, in_total, out_total, lens
+
+
+def build_aad(cfg, idx, lens):
+    n = len(idx)
+    aad = np.zeros((n, 16), dtype=np.uint8)
+    if cfg["aad"] == "tls":  # 17 03 03 len16(L + 16): build_aad, lib/picotls.c:696-703
+        reclen = lens + np.uint64(16)
+        aad[:, 0], aad[:, 1], aad[:, 2] = 0x17, 0x03, 0x03
+        aad[:, 3] = (reclen >> np.uint64(8)).astype(np.uint8)
+        aad[:, 4] = (reclen & np.uint64(0xFF)).astype(np.uint8)
+    else:
+        for s in range(0, n, 1 << 20):
+            aad[s:s + (1 << 20), :13] = stream_bytes(np.uint64(SEED_AAD) ^ idx[s:s + (1 << 20)], 13)
+    return aad.reshape(-1)
+
+
+def make_keys(cfg):
+    K, kl = cfg["keys"], cfg["key_len"]
+    s = stream_bytes(np.uint64(SEED_KEY) ^ np.arange(K, dtype=np.uint64), kl + 12)
+    return s[:, :kl].tobytes(), s[:, kl:kl + 12].tobytes()
+
+
+def cpu_baseline(cfg_name, cfg, budget_s=4.0):
+    """lib/fusion.c (oracle/_ref, built unmodified from the reference) on this host's cores, over a bounded
+    sample of the same workload shape: distinct record buffers, same AAD form, one context per thread."""
+    import ctypes
+    from oracle_lib import REF_SO, Ref, ORACLE_SO
+    L = cfg["L"] or 8224
+    nrec = max(64, min(4096, (64 << 20) // max(L, 1)))
+    stride = (L + 16 + 63) // 64 * 64
+    idx = np.arange(nrec, dtype=np.uint64)
+    data = np.zeros((nrec, stride), dtype=np.uint8)
+    data[:, :L] = stream_bytes(np.uint64(SEED_DATA) ^ idx, L)
+    aad_len = 5 if cfg["aad"] == "tls" else 13
+    aad = build_aad(cfg, idx, np.full(nrec, L, dtype=np.uint64)).reshape(nrec, 16)[:, :aad_len].copy()
+    key, iv = (b"\x11" * cfg["key_len"]), b"\x22" * 12
+    try:
+        ncpu = len(os.sched_getaffinity(0))
+    except AttributeError:
+        ncpu = os.cpu_count() or 1
+    threads = max(1, min(16, ncpu))
+    if not Ref.available:
+        o = ctypes.CDLL(ORACLE_SO)
+        o.oracle_bench_seal.restype = ctypes.c_double
+        o.oracle_bench_seal.argtypes = [ctypes.c_size_t, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_int]
+        n = 64
+        t = o.oracle_bench_seal(cfg["key_len"], n, L, 1)
+        return dict(value=n * L / t / GIB, unit="GiB/s (seal only)", cores=1, kind="port",
+                    sample=f"{n} x {L} B records, oracle C port, single thread")
+    ref = Ref()
+    ct = np.zeros_like(data)
+    pt = np.zeros_like(data)
+    cpus = sorted(os.sched_getaffinity(0))[:threads] if hasattr(os, "sched_getaffinity") else None
+
+    def run(do_open, src, dst, nthreads):
+        arr = (ctypes.c_int * nthreads)(*cpus[:nthreads]) if cpus else None
+        return ref.lib.ref_bench(cfg["key_len"] * 8, do_open, key, iv, src.ctypes.data, dst.ctypes.data, nrec, L, stride,
+                                 aad.ctypes.data, aad_len, nthreads, arr)
+
+    out = {}
+    for nthreads in sorted({1, threads}):
+        run(0, data, ct, nthreads)  # warm-up (+ produces valid ciphertext for open)
+        reps, ts, to = 0, 0.0, 0.0
+        t_start = time.time()
+        while time.time() - t_start < budget_s / 2 or reps < 3:
+            ts += run(0, data, ct, nthreads)
+            to += run(1, ct, pt, nthreads)
+            reps += 1
+        assert np.array_equal(pt[:, :L], data[:, :L]), "reference round trip failed"
+        out[nthreads] = dict(seal=reps * nrec * L / ts / GIB, open=reps * nrec * L / to / GIB,
+                             both=2 * reps * nrec * L / (ts + to) / GIB, reps=reps)
+    cpu_model = ""
+    try:
+        with open("/proc/cpuinfo") as f:
+            cpu_model = next((ln.split(":", 1)[1].strip() for ln in f if ln.startswith("model name")), "")
+    except OSError:
+        pass
+    best = out[threads]
+    return dict(value=round(best["both"], 3), unit="GiB/s seal+open", cores=threads, kind="reference",
+                single_core=round(out[1]["both"], 3), seal_gibps=round(best["seal"], 3), open_gibps=round(best["open"], 3),
+                fusion_can_aesni256=bool(ref.lib.ref_fusion_can_aesni256()), cpu=cpu_model,
+                sample=f"{nrec} x {L} B distinct records ({cfg_name} shape, {aad_len} B AAD), lib/fusion.c via "
+                       f"ptls_aead_encrypt/decrypt, {best['reps']} passes, {threads} pinned threads")
+
+
+def golden_check(cfg_name, idx, recs, d_ct):
+    """compare sampled sealed records with the digests lib/fusion.c produced (tests/golden/configs.json)"""
+    name = {"c2": "c2_tls16k_aes128", "c3": "c3_quic1350_aes128", "c4": "c4_mixed_aes256_64k",
+            "c5": "c5_quic1350_aes128_8gpu"}[cfg_name]
+    with open(os.path.join(ROOT, "tests", "golden", "configs.json")) as f:
+        golden = {r["i"]: r["sha256"] for r in json.load(f)["configs"][name]["records"]}
+    pos = {int(i): p for p, i in enumerate(idx) if int(i) in golden}
+    checked = 0
+    for i, p in pos.items():
+        off, L = int(recs["out_off"][p]), int(recs["len"][p])
+        blob = d_ct[off:off + L + 16].cpu().numpy().tobytes()
+        if hashlib.sha256(blob).hexdigest() != golden[i]:
+            raise AssertionError(f"record {i}: sealed bytes differ from lib/fusion.c")
+        checked += 1
+    return checked
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--config", default="c2", choices=list(CONFIGS))
+    ap.add_argument("--lanes", type=int, default=0)
+    ap.add_argument("--records", type=int, default=0, help="override records per GPU (smaller runs)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+    import ptls_hip
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    cfg = dict(CONFIGS[args.config])
+    if args.records:
+        cfg["n"] = args.records
+    eng = ptls_hip.Engine(local)
+    idx, recs, in_total, out_total, lens = make_workload(cfg, rank)
+    n = len(recs)
+    sum_L = int(lens.sum())
+    aad = build_aad(cfg, idx, lens)
+    aad_len = 5 if cfg["aad"] == "tls" else 13
+
+    keys, ivs = make_keys(cfg)
+    ks = ptls_hip.KeySet(eng, cfg["key_len"], cfg["keys"])
+    t0 = time.time()
+    ks.set(0, keys, ivs)
+    setup_s = time.time() - t0
+
+    seal_b = ptls_hip.Batch(eng, recs)
+    if args.lanes:
+        seal_b.set_lanes(args.lanes)
+    recs_o = recs.copy()
+    recs_o["in_off"], recs_o["out_off"] = recs["out_off"], recs["in_off"]
+    open_b = ptls_hip.Batch(eng, recs_o)
+    open_b.set_lanes(seal_b.lanes)
+
+    d_pt = torch.empty(in_total + 64, dtype=torch.uint8, device="cuda")
+    d_ct = torch.empty(out_total + 64, dtype=torch.uint8, device="cuda")
+    d_out = torch.empty(in_total + 64, dtype=torch.uint8, device="cuda")
+    d_aad = torch.from_numpy(aad).cuda()
+    d_res = torch.zeros(n, dtype=torch.int64, device="cuda")
+    # payload of record i = splitmix64 stream of SEED_DATA ^ i (same bytes the CPU side generates)
+    d_idx = torch.from_numpy(idx.astype(np.int64)).cuda()
+    seal_b.fill(d_pt, SEED_DATA, index=d_idx)
+    torch.cuda.synchronize()
+    del d_idx
+
+    stream = torch.cuda.current_stream()
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+
+    def step(times=None):
+        ev[0].record(stream)
+        seal_b.seal(ks, d_pt, d_aad, d_ct, stream)
+        ev[1].record(stream)
+        open_b.open(ks, d_ct, d_aad, d_out, d_res, stream)
+        ev[2].record(stream)
+        if times is not None:
+            torch.cuda.synchronize()
+            times.append((ev[0].elapsed_time(ev[1]), ev[1].elapsed_time(ev[2])))
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    # per-kernel timing (HIP events on the launch stream), outside the timed region
+    ktimes = []
+    for _ in range(max(2, min(args.steps, 5))):
+        step(ktimes)
+    seal_ms = float(np.median([a for a, _ in ktimes]))
+    open_ms = float(np.median([b for _, b in ktimes]))
+
+    # parity: every record opens to its length and original bytes; sampled records == lib/fusion.c
+    ok_open = bool((d_res == torch.tensor(lens.astype(np.int64), device="cuda")).all())
+    ok_pt = bool(torch.equal(d_out[:in_total], d_pt[:in_total]))
+    golden_n = golden_check(args.config, idx, recs, d_ct) if rank == 0 else 0
+    if not (ok_open and ok_pt):
+        raise AssertionError(f"rank {rank}: open round trip failed (status ok={ok_open}, bytes ok={ok_pt})")
+
+    alg_bytes = int(2 * sum_L + n * (aad_len + 16))  # 2L + A + 16 per record, per launch
+    achieved = alg_bytes / (seal_ms * 1e-3) / 1e9
+    value = world * 2 * sum_L * args.steps / elapsed / GIB
+
+    result = {
+        "metric": "GiB/s AES-128-GCM seal+open, device-resident, 16KiB records, 1/2/4/8 GPU"
+        if args.config == "c2" else f"GiB/s AES-GCM seal+open, device-resident ({args.config})",
+        "value": round(value, 2),
+        "unit": "GiB/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic (splitmix64 records, SURVEY.md §8(d)), generated in HBM",
+        "config": {"workload": cfg["desc"], "records_per_gpu": n, "record_bytes": cfg["L"] or "mixed 64-16384",
+                   "aad_bytes": aad_len, "keys": cfg["keys"], "key_bits": cfg["key_len"] * 8,
+                   "lanes_per_record": seal_b.lanes, "parallelism": f"records sharded by range over {world} GPU(s), no collective"},
+        "seal_gibps": round(world * sum_L / (seal_ms * 1e-3) / GIB, 2),
+        "open_gibps": round(world * sum_L / (open_ms * 1e-3) / GIB, 2),
+        "seal_ms": round(seal_ms, 3),
+        "open_ms": round(open_ms, 3),
+        "key_setup_s": round(setup_s, 4),
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                     "kernel": "aesgcm_batch_kernel (seal)", "algorithmic_bytes_per_launch": alg_bytes},
+        "parity": {"open_all_ok": ok_open, "roundtrip_bytes_equal": ok_pt, "golden_records_checked": golden_n},
+    }
+    tfile = os.path.join(ROOT, "profiles", f"traffic_{args.config}.json")
+    if os.path.exists(tfile):
+        with open(tfile) as f:
+            tr = json.load(f)
+        result["roofline"]["traffic"] = tr.get("hbm_bytes_per_seal_launch")
+        result["roofline"]["traffic_source"] = os.path.relpath(tfile, ROOT)
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        result["cpu_baseline"] = cpu_baseline(args.config, cfg)
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    for o in (seal_b, open_b, ks, eng):
+        o.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

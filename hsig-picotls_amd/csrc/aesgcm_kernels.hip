@@ -1,0 +1,683 @@
+/*
+ * aesgcm_kernels.hip -- gfx950 (MI355X) kernels of the AES-GCM record engine.
+ *
+ * What is computed (bit-exact with picotls lib/fusion.c):
+ *   seal  ptls_fusion_aesgcm_encrypt  lib/fusion.c:400-658
+ *   open  ptls_fusion_aesgcm_decrypt  lib/fusion.c:660-844
+ *   nonce calc_counter                lib/fusion.c:1126-1133 (== ptls_aead__build_iv lib/picotls.c:6492)
+ *   setup new_aesgcm + setup_one_ghash_entry  lib/fusion.c:984-1010, :939-966
+ * How: no AES / carry-less instructions exist on CDNA4 and north_star rules out MFMA,
+ * so both halves of GCM are table work in LDS:
+ *   AES   : T-table rounds.  One 256-entry table T0 (and T2 = rotl16(T0)) replicated 32x so that
+ *           lane l always hits bank l%32 -> ds_read_b32 is conflict-free for any data.  The LDS
+ *           address (byte << 8 | lane slot) is produced by ONE v_perm_b32 per lookup.
+ *   GHASH : multiplication by a fixed power P of H is GF(2)-linear, so X*P = XOR over the 16 bytes
+ *           of X of T8[p][X_p] with T8[p][v] = (v at byte p) * P.  The table is laid out row v, slot
+ *           p; lane l looks up byte p = (k + l) % 16 at step k, so the 16 lanes of every ds_read_b128
+ *           lane group touch 16 distinct slots -> conflict-free; X is pre-rotated per lane so the
+ *           byte for step k sits at a fixed position and the address is again one v_perm_b32.
+ *   Record parallelism: G lanes share one record (Horner with stride G inside a lane, then a
+ *           log2(G)-level shuffle tree with nibble tables for H, H^2, H^4), 64/G records per wave,
+ *           8 waves per workgroup, workgroups persist over key-homogeneous chunks of records.
+ */
+#include <hip/hip_runtime.h>
+#include "internal.h"
+
+namespace ptls_hip {
+
+/* ---------------- LDS map (bytes) ---------------- */
+constexpr uint32_t LDS_AES = 0;              /* 64 KiB: row v = [T0 x32 lane slots | T2 x32 lane slots]  */
+constexpr uint32_t LDS_GMAIN = 65536;        /* 64 KiB: row v (256 B) = 16 positions x 16 B, P = H^G       */
+constexpr uint32_t LDS_GTREE = 131072;       /* 3 x 8 KiB nibble tables for H^1, H^2, H^4: [p(32)][v(16)] */
+constexpr uint32_t LDS_TREE_STRIDE = 8192;
+constexpr uint32_t LDS_BYTES = LDS_GTREE + 3 * LDS_TREE_STRIDE; /* 152 KiB of the CU's 160 KiB */
+
+struct V4 {
+    uint32_t w0, w1, w2, w3;
+};
+
+__device__ __forceinline__ V4 v4xor(V4 a, V4 b)
+{
+    return V4{a.w0 ^ b.w0, a.w1 ^ b.w1, a.w2 ^ b.w2, a.w3 ^ b.w3};
+}
+
+__device__ __forceinline__ uint32_t bswap32(uint32_t x)
+{
+    return __builtin_bswap32(x);
+}
+
+__device__ __forceinline__ uint32_t lds32(const uint8_t *lds, uint32_t addr)
+{
+    return *reinterpret_cast<const uint32_t *>(lds + addr);
+}
+
+__device__ __forceinline__ V4 lds128(const uint8_t *lds, uint32_t addr)
+{
+    const uint4 v = *reinterpret_cast<const uint4 *>(lds + addr);
+    return V4{v.x, v.y, v.z, v.w};
+}
+
+__device__ __forceinline__ void lds128_store(uint8_t *lds, uint32_t addr, V4 v)
+{
+    *reinterpret_cast<uint4 *>(lds + addr) = make_uint4(v.w0, v.w1, v.w2, v.w3);
+}
+
+/* ======================================================================================= *
+ *  AES (FIPS-197) with replicated T-tables in LDS                                          *
+ * ======================================================================================= */
+
+/* LDS byte address of T0[byte k of x] for this lane: (x.byte[k] << 8) | lane_slot.
+ * v_perm_b32: result byte0 <- lb.byte0 (selector 0), byte1 <- x.byte[k] (selector 4+k), rest 0. */
+template <int K>
+__device__ __forceinline__ uint32_t aes_addr(uint32_t x, uint32_t lb)
+{
+    return __builtin_amdgcn_perm(x, lb, 0x0c0c0000u | ((4u + K) << 8));
+}
+
+__device__ __forceinline__ uint32_t rotl8(uint32_t x)
+{
+    return __builtin_amdgcn_alignbit(x, x, 24);
+}
+
+/* one output column of a full round:
+ * T0[x0.b0] ^ T1[x1.b1] ^ T2[x2.b2] ^ T3[x3.b3] ^ k  with T1 = rotl8(T0), T3 = rotl8(T2) */
+__device__ __forceinline__ uint32_t aes_col(const uint8_t *lds, uint32_t lb, uint32_t x0, uint32_t x1, uint32_t x2, uint32_t x3,
+                                            uint32_t k)
+{
+    const uint32_t a0 = lds32(lds, LDS_AES + aes_addr<0>(x0, lb));
+    const uint32_t a1 = lds32(lds, LDS_AES + aes_addr<1>(x1, lb));
+    const uint32_t a2 = lds32(lds, LDS_AES + 128 + aes_addr<2>(x2, lb));
+    const uint32_t a3 = lds32(lds, LDS_AES + 128 + aes_addr<3>(x3, lb));
+    return a0 ^ a2 ^ k ^ rotl8(a1 ^ a3);
+}
+
+/* final round column: S-box bytes picked out of T2[.].b0, T0[.].b1, T0[.].b2, T2[.].b3 */
+__device__ __forceinline__ uint32_t aes_col_last(const uint8_t *lds, uint32_t lb, uint32_t x0, uint32_t x1, uint32_t x2,
+                                                 uint32_t x3, uint32_t k)
+{
+    const uint32_t u0 = lds32(lds, LDS_AES + 128 + aes_addr<0>(x0, lb));
+    const uint32_t u1 = lds32(lds, LDS_AES + aes_addr<1>(x1, lb));
+    const uint32_t u2 = lds32(lds, LDS_AES + aes_addr<2>(x2, lb));
+    const uint32_t u3 = lds32(lds, LDS_AES + 128 + aes_addr<3>(x3, lb));
+    const uint32_t lo = __builtin_amdgcn_perm(u1, u0, 0x0c0c0500u); /* u0.b0 -> b0, u1.b1 -> b1 */
+    const uint32_t hi = __builtin_amdgcn_perm(u3, u2, 0x07020c0cu); /* u2.b2 -> b2, u3.b3 -> b3 */
+    return (lo | hi) ^ k;
+}
+
+template <int ROUNDS>
+__device__ __forceinline__ V4 aes_encrypt(const uint8_t *lds, uint32_t lb, const uint32_t *__restrict__ rk, V4 s)
+{
+    s.w0 ^= rk[0];
+    s.w1 ^= rk[1];
+    s.w2 ^= rk[2];
+    s.w3 ^= rk[3];
+#pragma unroll
+    for (int r = 1; r < ROUNDS; ++r) {
+        const uint32_t t0 = aes_col(lds, lb, s.w0, s.w1, s.w2, s.w3, rk[4 * r + 0]);
+        const uint32_t t1 = aes_col(lds, lb, s.w1, s.w2, s.w3, s.w0, rk[4 * r + 1]);
+        const uint32_t t2 = aes_col(lds, lb, s.w2, s.w3, s.w0, s.w1, rk[4 * r + 2]);
+        const uint32_t t3 = aes_col(lds, lb, s.w3, s.w0, s.w1, s.w2, rk[4 * r + 3]);
+        s = V4{t0, t1, t2, t3};
+    }
+    const uint32_t t0 = aes_col_last(lds, lb, s.w0, s.w1, s.w2, s.w3, rk[4 * ROUNDS + 0]);
+    const uint32_t t1 = aes_col_last(lds, lb, s.w1, s.w2, s.w3, s.w0, rk[4 * ROUNDS + 1]);
+    const uint32_t t2 = aes_col_last(lds, lb, s.w2, s.w3, s.w0, s.w1, rk[4 * ROUNDS + 2]);
+    const uint32_t t3 = aes_col_last(lds, lb, s.w3, s.w0, s.w1, s.w2, rk[4 * ROUNDS + 3]);
+    return V4{t0, t1, t2, t3};
+}
+
+/* ======================================================================================= *
+ *  GHASH multiply by table                                                                 *
+ * ======================================================================================= */
+
+struct GhLane {
+    uint32_t lb0, lb1, lb2, lb3; /* byte m of lbI = ((4I + m + lane) & 15) * 16 : slot of step 4I+m */
+    uint32_t shift;              /* 8 * (lane & 3) */
+    bool rot1, rot2;             /* word rotation by (lane >> 2) & 3 */
+};
+
+__device__ __forceinline__ GhLane gh_lane_init(int lane)
+{
+    GhLane g;
+    uint32_t lb[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        uint32_t v = 0;
+#pragma unroll
+        for (int m = 0; m < 4; ++m)
+            v |= (uint32_t)(((4 * i + m + lane) & 15) * 16) << (8 * m);
+        lb[i] = v;
+    }
+    g.lb0 = lb[0];
+    g.lb1 = lb[1];
+    g.lb2 = lb[2];
+    g.lb3 = lb[3];
+    g.shift = 8u * (lane & 3);
+    g.rot1 = ((lane >> 2) & 1) != 0;
+    g.rot2 = ((lane >> 3) & 1) != 0;
+    return g;
+}
+
+template <int K>
+__device__ __forceinline__ V4 gh_term(const uint8_t *lds, uint32_t xw, uint32_t lbw)
+{
+    /* address = (xrot.byte[K] << 8) | slot(K):  byte0 <- lbw.byte[K%4], byte1 <- xw.byte[K%4] */
+    const uint32_t addr = __builtin_amdgcn_perm(xw, lbw, 0x0c0c0000u | ((4u + (K & 3)) << 8) | (K & 3));
+    return lds128(lds, LDS_GMAIN + addr);
+}
+
+/* returns y * P ^ x, P = the power held in the main table */
+__device__ __forceinline__ V4 gh_mul_main(const uint8_t *lds, const GhLane &g, V4 y, V4 x)
+{
+    /* rotate y right by (lane & 15) bytes: xr.byte[k] = y.byte[(k + lane) & 15] */
+    const uint32_t s0 = g.rot1 ? y.w1 : y.w0, s1 = g.rot1 ? y.w2 : y.w1, s2 = g.rot1 ? y.w3 : y.w2, s3 = g.rot1 ? y.w0 : y.w3;
+    const uint32_t r0 = g.rot2 ? s2 : s0, r1 = g.rot2 ? s3 : s1, r2 = g.rot2 ? s0 : s2, r3 = g.rot2 ? s1 : s3;
+    const uint32_t x0 = __builtin_amdgcn_alignbit(r1, r0, g.shift);
+    const uint32_t x1 = __builtin_amdgcn_alignbit(r2, r1, g.shift);
+    const uint32_t x2 = __builtin_amdgcn_alignbit(r3, r2, g.shift);
+    const uint32_t x3 = __builtin_amdgcn_alignbit(r0, r3, g.shift);
+    V4 acc = x;
+    acc = v4xor(acc, gh_term<0>(lds, x0, g.lb0));
+    acc = v4xor(acc, gh_term<1>(lds, x0, g.lb0));
+    acc = v4xor(acc, gh_term<2>(lds, x0, g.lb0));
+    acc = v4xor(acc, gh_term<3>(lds, x0, g.lb0));
+    acc = v4xor(acc, gh_term<4>(lds, x1, g.lb1));
+    acc = v4xor(acc, gh_term<5>(lds, x1, g.lb1));
+    acc = v4xor(acc, gh_term<6>(lds, x1, g.lb1));
+    acc = v4xor(acc, gh_term<7>(lds, x1, g.lb1));
+    acc = v4xor(acc, gh_term<8>(lds, x2, g.lb2));
+    acc = v4xor(acc, gh_term<9>(lds, x2, g.lb2));
+    acc = v4xor(acc, gh_term<10>(lds, x2, g.lb2));
+    acc = v4xor(acc, gh_term<11>(lds, x2, g.lb2));
+    acc = v4xor(acc, gh_term<12>(lds, x3, g.lb3));
+    acc = v4xor(acc, gh_term<13>(lds, x3, g.lb3));
+    acc = v4xor(acc, gh_term<14>(lds, x3, g.lb3));
+    acc = v4xor(acc, gh_term<15>(lds, x3, g.lb3));
+    return acc;
+}
+
+/* y * P with a nibble table [p = 8w + j][v] (used only in the per-record reduction tree) */
+__device__ __forceinline__ V4 gh_mul_nibble(const uint8_t *lds, uint32_t table, V4 y)
+{
+    V4 acc = V4{0, 0, 0, 0};
+    const uint32_t w[4] = {y.w0, y.w1, y.w2, y.w3};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const uint32_t v = (w[i] >> (4 * j)) & 15u;
+            acc = v4xor(acc, lds128(lds, table + (uint32_t)(8 * i + j) * 256u + v * 16u));
+        }
+    }
+    return acc;
+}
+
+/* ---------------- table construction in LDS ---------------- */
+
+__device__ __forceinline__ V4 ld_basis(const uint32_t *b, int e)
+{
+    const uint4 v = reinterpret_cast<const uint4 *>(b)[e];
+    return V4{v.x, v.y, v.z, v.w};
+}
+
+/* AES tables: row v = [T0[v] x 32 | rotl16(T0[v]) x 32] */
+__device__ void build_aes_tables(uint8_t *lds, const uint32_t *__restrict__ t0)
+{
+    for (int e = threadIdx.x; e < 256 * 32; e += WG_THREADS) {
+        const int v = e >> 5, s = e & 31;
+        const uint32_t t = t0[v];
+        *reinterpret_cast<uint32_t *>(lds + LDS_AES + v * 256 + s * 4) = t;
+        *reinterpret_cast<uint32_t *>(lds + LDS_AES + v * 256 + 128 + s * 4) = (t << 16) | (t >> 16);
+    }
+}
+
+/* GHASH tables of one key slot.  basis = uint4[NPOW][128], basis[t][e] = H^(2^t) * x^e (GCM bit
+ * index e: byte e/8, bit 7 - e%8).  Raw byte p, bit t  <->  e = 8p + 7 - t. */
+__device__ void build_ghash_tables(uint8_t *lds, const uint32_t *__restrict__ basis, int log2g)
+{
+    const uint32_t *bm = basis + log2g * 128 * 4;
+    for (int e = threadIdx.x; e < 16 * 256; e += WG_THREADS) {
+        const int p = e >> 8, v = e & 255;
+        V4 acc = V4{0, 0, 0, 0};
+#pragma unroll
+        for (int t = 0; t < 8; ++t)
+            if ((v >> t) & 1)
+                acc = v4xor(acc, ld_basis(bm, 8 * p + 7 - t));
+        lds128_store(lds, LDS_GMAIN + v * 256 + p * 16, acc);
+    }
+    for (int e = threadIdx.x; e < 3 * 512; e += WG_THREADS) {
+        const int d = e >> 9, p = (e >> 4) & 31, v = e & 15;
+        const int w = p >> 3, j = p & 7;
+        const uint32_t *bt = basis + d * 128 * 4;
+        V4 acc = V4{0, 0, 0, 0};
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            if ((v >> t) & 1) {
+                const int u = 4 * j + t; /* bit u of little-endian word w = raw byte 4w + u/8, bit u%8 */
+                acc = v4xor(acc, ld_basis(bt, 8 * (4 * w + (u >> 3)) + 7 - (u & 7)));
+            }
+        }
+        lds128_store(lds, LDS_GTREE + d * LDS_TREE_STRIDE + p * 256 + v * 16, acc);
+    }
+}
+
+/* ---------------- global-memory block access ---------------- */
+
+__device__ __forceinline__ V4 load_block(const uint8_t *p, int n, bool fast)
+{
+    if (fast && n == 16) {
+        const uint4 v = *reinterpret_cast<const uint4 *>(p);
+        return V4{v.x, v.y, v.z, v.w};
+    }
+    uint32_t w[4] = {0, 0, 0, 0};
+#pragma unroll
+    for (int k = 0; k < 16; ++k)
+        if (k < n)
+            w[k >> 2] |= (uint32_t)p[k] << (8 * (k & 3));
+    return V4{w[0], w[1], w[2], w[3]};
+}
+
+__device__ __forceinline__ void store_block(uint8_t *p, int n, bool fast, V4 v)
+{
+    if (fast && n == 16) {
+        *reinterpret_cast<uint4 *>(p) = make_uint4(v.w0, v.w1, v.w2, v.w3);
+        return;
+    }
+    const uint32_t w[4] = {v.w0, v.w1, v.w2, v.w3};
+#pragma unroll
+    for (int k = 0; k < 16; ++k)
+        if (k < n)
+            p[k] = (uint8_t)(w[k >> 2] >> (8 * (k & 3)));
+}
+
+__device__ __forceinline__ V4 mask_block(V4 v, int n)
+{
+    /* keep the first n (0..16) bytes */
+    const uint32_t w[4] = {v.w0, v.w1, v.w2, v.w3};
+    uint32_t o[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int keep = n - 4 * i;
+        o[i] = keep >= 4 ? w[i] : (keep <= 0 ? 0u : (w[i] & ((1u << (8 * keep)) - 1u)));
+    }
+    return V4{o[0], o[1], o[2], o[3]};
+}
+
+__device__ __forceinline__ int wave_max(int v)
+{
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1)
+        v = max(v, __shfl_xor(v, o, 64));
+    return v;
+}
+
+/* ======================================================================================= *
+ *  batch seal / open                                                                       *
+ * ======================================================================================= */
+
+template <int G, int ROUNDS, bool OPEN>
+__global__ void __launch_bounds__(WG_THREADS) aesgcm_batch_kernel(KernelArgs a, uint32_t base_aligned)
+{
+    __shared__ __attribute__((aligned(16))) uint8_t lds[LDS_BYTES];
+    constexpr int LOG2G = G == 1 ? 0 : G == 2 ? 1 : G == 4 ? 2 : 3;
+    constexpr int R = 64 / G; /* records per wave task */
+
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    const uint32_t lb_aes = (uint32_t)(lane & 31) * 4u;
+    const GhLane gl = gh_lane_init(lane);
+    const int r = lane & (G - 1);
+    const int grp = lane >> LOG2G;
+
+    build_aes_tables(lds, a.t0);
+    uint32_t cur_key = 0xffffffffu;
+
+    for (uint32_t ci = blockIdx.x; ci < a.nchunks; ci += gridDim.x) {
+        const Chunk ch = a.chunks[ci];
+        if (ch.key != cur_key) {
+            __syncthreads();
+            build_ghash_tables(lds, a.basis + (size_t)ch.key * (NPOW * 128 * 4), LOG2G);
+            __syncthreads();
+            cur_key = ch.key;
+        }
+        const KeySlot *__restrict__ slot = a.slots + ch.key;
+        const uint32_t *__restrict__ rk = slot->rk;
+        const bool fast = (ch.flags & 1u) && base_aligned;
+        const int ntasks = (int)((ch.count + R - 1) / R);
+
+        for (int t = wave; t < ntasks; t += WAVES_PER_WG) {
+            const uint32_t ridx = (uint32_t)t * R + grp;
+            const bool valid = ridx < ch.count;
+            const uint32_t rec_i = ch.first + (valid ? ridx : 0);
+            const ptls_hip_record_t rec = a.recs[rec_i];
+            const int L = valid ? (int)rec.len : 0;
+            const int A = valid ? (int)rec.aad_len : 0;
+            const int na = (A + 15) >> 4, nc = (L + 15) >> 4;
+            const int N = valid ? na + nc + 1 : 0;
+            const int i0 = (r + na) & (G - 1);
+            const int my_iters = i0 < N ? ((N - 1 - i0) >> LOG2G) + 1 : 0;
+            const int iters = wave_max(my_iters);
+
+            const uint8_t *in_p = a.in + rec.in_off;
+            uint8_t *out_p = a.out + rec.out_off;
+            const uint8_t *aad_p = a.aad + rec.aad_off;
+            const uint32_t n0 = slot->iv[0], n1 = slot->iv[1] ^ bswap32((uint32_t)(rec.seq >> 32)),
+                           n2 = slot->iv[2] ^ bswap32((uint32_t)rec.seq);
+            const uint64_t abits = (uint64_t)A * 8, cbits = (uint64_t)L * 8;
+            const V4 lenblk = V4{bswap32((uint32_t)(abits >> 32)), bswap32((uint32_t)abits), bswap32((uint32_t)(cbits >> 32)),
+                                 bswap32((uint32_t)cbits)};
+
+            V4 y = V4{0, 0, 0, 0}, ek0 = V4{0, 0, 0, 0};
+            for (int m = 0; m < iters; ++m) {
+                const int i = i0 + m * G;
+                const bool active = i < N;
+                const bool is_aad = i < na;
+                const bool is_c = !is_aad && i < na + nc;
+                const bool is_len = active && i == N - 1;
+                const int c = i - na;
+                const int nbytes = is_c ? min(16, L - 16 * c) : 0;
+
+                V4 in_blk = V4{0, 0, 0, 0};
+                if (is_c)
+                    in_blk = load_block(in_p + 16 * (size_t)c, nbytes, fast);
+                /* keystream for data block c (counter inc32(J0) + c), or E_K(J0) for the lane holding the length block */
+                const V4 ctr = V4{n0, n1, n2, is_c ? bswap32((uint32_t)c + 2u) : 0x01000000u};
+                const V4 ks = aes_encrypt<ROUNDS>(lds, lb_aes, rk, ctr);
+
+                V4 x = V4{0, 0, 0, 0};
+                if (is_aad) {
+                    x = load_block(aad_p + 16 * i, min(16, A - 16 * i), fast);
+                } else if (is_c) {
+                    const V4 o = v4xor(in_blk, ks);
+                    if (OPEN) {
+                        store_block(out_p + 16 * (size_t)c, nbytes, fast, o);
+                        x = in_blk;
+                    } else {
+                        x = mask_block(o, nbytes);
+                        store_block(out_p + 16 * (size_t)c, nbytes, fast, x);
+                    }
+                } else if (is_len) {
+                    x = lenblk;
+                    ek0 = ks;
+                }
+                if (m == 0)
+                    y = x;
+                else if (active)
+                    y = gh_mul_main(lds, gl, y, x);
+            }
+
+            /* combine the G partial sums of each record: position q = distance of a lane's last element
+             * from the end of the GHASH input; sum_q y_q * H^(q+1) by a shuffle tree */
+            const int q = (nc - r) & (G - 1);
+#pragma unroll
+            for (int lvl = 0; lvl < LOG2G; ++lvl) {
+                const int d = 1 << lvl;
+                const int src = (lane & ~(G - 1)) | ((r - d) & (G - 1));
+                V4 v;
+                v.w0 = __shfl(y.w0, src, 64);
+                v.w1 = __shfl(y.w1, src, 64);
+                v.w2 = __shfl(y.w2, src, 64);
+                v.w3 = __shfl(y.w3, src, 64);
+                const V4 w = gh_mul_nibble(lds, LDS_GTREE + lvl * LDS_TREE_STRIDE, v);
+                if ((q & (2 * d - 1)) == 0)
+                    y = v4xor(y, w);
+            }
+            if (valid && q == 0) {
+                const V4 s = gh_mul_nibble(lds, LDS_GTREE, y); /* * H */
+                const V4 tag = v4xor(s, ek0);
+                const bool tag_fast = fast && (L & 15) == 0;
+                if (OPEN) {
+                    const V4 rt = load_block(in_p + L, 16, tag_fast);
+                    const bool ok = rt.w0 == tag.w0 && rt.w1 == tag.w1 && rt.w2 == tag.w2 && rt.w3 == tag.w3;
+                    a.result[rec_i] = ok ? (uint64_t)L : ~(uint64_t)0;
+                } else {
+                    store_block(out_p + L, 16, tag_fast, tag);
+                }
+            }
+        }
+    }
+}
+
+#define INST(G, R, O) template __global__ void aesgcm_batch_kernel<G, R, O>(KernelArgs, uint32_t);
+#define INST_G(G) INST(G, 10, false) INST(G, 10, true) INST(G, 14, false) INST(G, 14, true)
+INST_G(1)
+INST_G(2)
+INST_G(4)
+INST_G(8)
+#undef INST_G
+#undef INST
+
+/* ======================================================================================= *
+ *  key setup: one thread per key slot (setup_crypto, lib/fusion.c:1184-1206, :984-1010)    *
+ * ======================================================================================= */
+
+struct U128 {
+    uint64_t hi, lo; /* big-endian view: hi holds raw bytes 0..7 (byte 0 most significant) */
+};
+
+__device__ __forceinline__ U128 u128_from_raw(V4 v)
+{
+    return U128{__builtin_bswap64((uint64_t)v.w0 | ((uint64_t)v.w1 << 32)), __builtin_bswap64((uint64_t)v.w2 | ((uint64_t)v.w3 << 32))};
+}
+
+__device__ __forceinline__ V4 u128_to_raw(U128 u)
+{
+    const uint64_t a = __builtin_bswap64(u.hi), b = __builtin_bswap64(u.lo);
+    return V4{(uint32_t)a, (uint32_t)(a >> 32), (uint32_t)b, (uint32_t)(b >> 32)};
+}
+
+/* multiply by x in GCM's reflected bit order (SP 800-38D: V >> 1, xor R if the dropped bit was set) */
+__device__ __forceinline__ U128 gf_mulx(U128 v)
+{
+    const uint64_t carry = v.lo & 1;
+    U128 o{v.hi >> 1, (v.lo >> 1) | (v.hi << 63)};
+    if (carry)
+        o.hi ^= 0xe100000000000000ull;
+    return o;
+}
+
+__device__ U128 gf_mul_slow(U128 x, U128 y)
+{
+    U128 z{0, 0}, v = y;
+    for (int i = 0; i < 128; ++i) {
+        const uint64_t bit = i < 64 ? (x.hi >> (63 - i)) & 1 : (x.lo >> (127 - i)) & 1;
+        if (bit) {
+            z.hi ^= v.hi;
+            z.lo ^= v.lo;
+        }
+        v = gf_mulx(v);
+    }
+    return z;
+}
+
+__device__ __forceinline__ uint8_t sbox_of(const uint32_t *t0, uint8_t x)
+{
+    return (uint8_t)(t0[x] >> 8);
+}
+
+__device__ __forceinline__ uint8_t xtime8(uint8_t a)
+{
+    return (uint8_t)((a << 1) ^ ((a & 0x80) ? 0x1b : 0));
+}
+
+__global__ void keysetup_kernel(KeySlot *slots, uint32_t *basis, const uint8_t *keys, const uint8_t *ivs, uint32_t first,
+                                uint32_t count, int key_size, const uint32_t *t0)
+{
+    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= count)
+        return;
+    KeySlot *slot = slots + first + k;
+    const uint8_t *key = keys + (size_t)k * key_size;
+    const int nk = key_size / 4, rounds = nk + 6, total = 4 * (rounds + 1);
+
+    /* key expansion (FIPS-197 §5.2), words kept as raw little-endian uint32 */
+    uint32_t w[60];
+    for (int i = 0; i < nk; ++i)
+        w[i] = (uint32_t)key[4 * i] | ((uint32_t)key[4 * i + 1] << 8) | ((uint32_t)key[4 * i + 2] << 16) |
+               ((uint32_t)key[4 * i + 3] << 24);
+    uint8_t rcon = 1;
+    for (int i = nk; i < total; ++i) {
+        uint32_t t = w[i - 1];
+        if (i % nk == 0) {
+            t = (t >> 8) | (t << 24); /* RotWord on raw bytes */
+            t = (uint32_t)sbox_of(t0, t & 0xff) | ((uint32_t)sbox_of(t0, (t >> 8) & 0xff) << 8) |
+                ((uint32_t)sbox_of(t0, (t >> 16) & 0xff) << 16) | ((uint32_t)sbox_of(t0, t >> 24) << 24);
+            t ^= rcon;
+            rcon = xtime8(rcon);
+        } else if (nk > 6 && i % nk == 4) {
+            t = (uint32_t)sbox_of(t0, t & 0xff) | ((uint32_t)sbox_of(t0, (t >> 8) & 0xff) << 8) |
+                ((uint32_t)sbox_of(t0, (t >> 16) & 0xff) << 16) | ((uint32_t)sbox_of(t0, t >> 24) << 24);
+        }
+        w[i] = w[i - nk] ^ t;
+    }
+    for (int i = 0; i < 60; ++i)
+        slot->rk[i] = i < total ? w[i] : 0;
+    slot->rounds = (uint32_t)rounds;
+    for (int i = 0; i < 3; ++i)
+        slot->iv[i] = (uint32_t)ivs[12 * k + 4 * i] | ((uint32_t)ivs[12 * k + 4 * i + 1] << 8) |
+                      ((uint32_t)ivs[12 * k + 4 * i + 2] << 16) | ((uint32_t)ivs[12 * k + 4 * i + 3] << 24);
+
+    /* H = E_K(0^128), byte-oriented AES (setup only) */
+    uint8_t s[16], tmp[16];
+    for (int i = 0; i < 16; ++i)
+        s[i] = (uint8_t)(w[i >> 2] >> (8 * (i & 3)));
+    for (int rr = 1; rr <= rounds; ++rr) {
+        for (int c = 0; c < 4; ++c)
+            for (int row = 0; row < 4; ++row)
+                tmp[4 * c + row] = sbox_of(t0, s[4 * ((c + row) & 3) + row]);
+        if (rr != rounds) {
+            for (int c = 0; c < 4; ++c) {
+                const uint8_t a0 = tmp[4 * c], a1 = tmp[4 * c + 1], a2 = tmp[4 * c + 2], a3 = tmp[4 * c + 3];
+                const uint8_t all = a0 ^ a1 ^ a2 ^ a3;
+                s[4 * c + 0] = a0 ^ all ^ xtime8(a0 ^ a1);
+                s[4 * c + 1] = a1 ^ all ^ xtime8(a1 ^ a2);
+                s[4 * c + 2] = a2 ^ all ^ xtime8(a2 ^ a3);
+                s[4 * c + 3] = a3 ^ all ^ xtime8(a3 ^ a0);
+            }
+        } else {
+            for (int i = 0; i < 16; ++i)
+                s[i] = tmp[i];
+        }
+        for (int i = 0; i < 16; ++i)
+            s[i] ^= (uint8_t)(w[4 * rr + (i >> 2)] >> (8 * (i & 3)));
+    }
+    V4 h;
+    h.w0 = (uint32_t)s[0] | ((uint32_t)s[1] << 8) | ((uint32_t)s[2] << 16) | ((uint32_t)s[3] << 24);
+    h.w1 = (uint32_t)s[4] | ((uint32_t)s[5] << 8) | ((uint32_t)s[6] << 16) | ((uint32_t)s[7] << 24);
+    h.w2 = (uint32_t)s[8] | ((uint32_t)s[9] << 8) | ((uint32_t)s[10] << 16) | ((uint32_t)s[11] << 24);
+    h.w3 = (uint32_t)s[12] | ((uint32_t)s[13] << 8) | ((uint32_t)s[14] << 16) | ((uint32_t)s[15] << 24);
+
+    U128 p = u128_from_raw(h);
+    uint4 *bs = reinterpret_cast<uint4 *>(basis) + (size_t)(first + k) * NPOW * 128;
+    for (int t = 0; t < NPOW; ++t) {
+        if (t != 0)
+            p = gf_mul_slow(p, p);
+        const V4 pr = u128_to_raw(p);
+        slot->hpow[t][0] = pr.w0;
+        slot->hpow[t][1] = pr.w1;
+        slot->hpow[t][2] = pr.w2;
+        slot->hpow[t][3] = pr.w3;
+        U128 b = p;
+        for (int e = 0; e < 128; ++e) {
+            const V4 br = u128_to_raw(b);
+            bs[t * 128 + e] = make_uint4(br.w0, br.w1, br.w2, br.w3);
+            b = gf_mulx(b);
+        }
+    }
+}
+
+/* ======================================================================================= *
+ *  synthetic records: record i = splitmix64 stream seeded with seed ^ i   *
+ * ======================================================================================= */
+
+__device__ __forceinline__ uint64_t splitmix_mix(uint64_t z)
+{
+    z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+    z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+    return z ^ (z >> 31);
+}
+
+__global__ void fill_records_kernel(const ptls_hip_record_t *recs, uint32_t n, uint8_t *buf, uint64_t seed, uint64_t index_base,
+                                    const uint64_t *index)
+{
+    /* one wave per record, 16 bytes per lane per step */
+    const uint32_t lane = threadIdx.x & 63;
+    for (uint32_t i = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6); i < n; i += gridDim.x * (blockDim.x / 64)) {
+        const ptls_hip_record_t rec = recs[i];
+        const uint64_t sd = seed ^ (index != nullptr ? index[i] : index_base + i);
+        uint8_t *p = buf + rec.in_off;
+        const bool al = ((reinterpret_cast<uintptr_t>(p)) & 15) == 0;
+        for (uint32_t off = lane * 16; off < rec.len; off += 64 * 16) {
+            const uint64_t wi = off / 8;
+            const uint64_t v0 = splitmix_mix(sd + (wi + 1) * 0x9e3779b97f4a7c15ull);
+            const uint64_t v1 = splitmix_mix(sd + (wi + 2) * 0x9e3779b97f4a7c15ull);
+            const int nb = (int)min(16u, rec.len - off);
+            store_block(p + off, nb, al, V4{(uint32_t)v0, (uint32_t)(v0 >> 32), (uint32_t)v1, (uint32_t)(v1 >> 32)});
+        }
+    }
+}
+
+} // namespace ptls_hip
+
+/* ======================================================================================= *
+ *  host-side launchers                                                                     *
+ * ======================================================================================= */
+namespace ptls_hip {
+
+template <int G, int R, bool O>
+static hipError_t launch_one(unsigned grid, hipStream_t s, const KernelArgs &a, uint32_t al)
+{
+    hipLaunchKernelGGL((aesgcm_batch_kernel<G, R, O>), dim3(grid), dim3(WG_THREADS), 0, s, a, al);
+    return hipGetLastError();
+}
+
+template <int G>
+static hipError_t launch_g(int rounds, bool open, unsigned grid, hipStream_t s, const KernelArgs &a, uint32_t al)
+{
+    if (rounds == 10)
+        return open ? launch_one<G, 10, true>(grid, s, a, al) : launch_one<G, 10, false>(grid, s, a, al);
+    return open ? launch_one<G, 14, true>(grid, s, a, al) : launch_one<G, 14, false>(grid, s, a, al);
+}
+
+int launch_batch(int lanes, int rounds, bool open, unsigned grid, void *stream, const KernelArgs &a, bool base_aligned)
+{
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    const uint32_t al = base_aligned ? 1u : 0u;
+    hipError_t e;
+    switch (lanes) {
+    case 1:
+        e = launch_g<1>(rounds, open, grid, s, a, al);
+        break;
+    case 2:
+        e = launch_g<2>(rounds, open, grid, s, a, al);
+        break;
+    case 4:
+        e = launch_g<4>(rounds, open, grid, s, a, al);
+        break;
+    case 8:
+        e = launch_g<8>(rounds, open, grid, s, a, al);
+        break;
+    default:
+        return (int)hipErrorInvalidValue;
+    }
+    return (int)e;
+}
+
+int launch_keysetup(KeySlot *slots, uint32_t *basis, const uint8_t *keys, const uint8_t *ivs, uint32_t first, uint32_t count,
+                    int key_size, const uint32_t *t0, void *stream)
+{
+    const unsigned threads = 64, grid = (count + threads - 1) / threads;
+    hipLaunchKernelGGL(keysetup_kernel, dim3(grid), dim3(threads), 0, static_cast<hipStream_t>(stream), slots, basis, keys, ivs,
+                       first, count, key_size, t0);
+    return (int)hipGetLastError();
+}
+
+int launch_fill(const ptls_hip_record_t *recs, uint32_t n, uint8_t *buf, uint64_t seed, uint64_t index_base,
+                const uint64_t *index, unsigned grid, void *stream)
+{
+    hipLaunchKernelGGL(fill_records_kernel, dim3(grid), dim3(256), 0, static_cast<hipStream_t>(stream), recs, n, buf, seed,
+                       index_base, index);
+    return (int)hipGetLastError();
+}
+
+} // namespace ptls_hip

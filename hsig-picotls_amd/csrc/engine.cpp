@@ -1,0 +1,807 @@
+/*
+ * engine.cpp -- host side of the MI355X AES-GCM engine: the C ABI of include/ptls_hip.h.
+ *
+ *   engines   one per device; owns the AES T0 table in HBM and the launch geometry
+ *   keysets   device-resident AEAD contexts (KeySlot + GHASH basis), expanded on the GPU
+ *   batches   uploaded record descriptors + the launch plan (key-homogeneous chunks, lanes/record)
+ *   plugin    ptls_hip_aes{128,256}gcm: picotls ptls_aead_algorithm_t objects whose callbacks run one
+ *             record through the same kernels (setup_crypto / do_encrypt / do_encrypt_v / do_decrypt /
+ *             do_get_iv / do_set_iv / dispose_crypto, mirroring lib/fusion.c:1102-1256)
+ *
+ * There is no CPU crypto fallback: without a usable gfx950 device the constructors fail
+ * (setup_crypto returns -1 so ptls_aead_new returns NULL), and a device failure inside a
+ * void callback (do_encrypt has no error channel) aborts the process with a message.
+ */
+#include <hip/hip_runtime_api.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "internal.h"
+
+using namespace ptls_hip;
+
+/* ---------------------------------------------------------------------------------------------- */
+/* errors                                                                                          */
+/* ---------------------------------------------------------------------------------------------- */
+
+static thread_local std::string g_err;
+
+static int fail(int code, const char *fmt, ...)
+{
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return code;
+}
+
+#define HIP_TRY(expr, code)                                                                                                        \
+    do {                                                                                                                           \
+        hipError_t e_ = (expr);                                                                                                    \
+        if (e_ != hipSuccess)                                                                                                      \
+            return fail((code), "%s failed: %s", #expr, hipGetErrorString(e_));                                                  \
+    } while (0)
+
+extern "C" const char *ptls_hip_last_error(void)
+{
+    return g_err.c_str();
+}
+
+/* ---------------------------------------------------------------------------------------------- */
+/* AES T-table: T0[x] = (2s, s, s, 3s) little-endian, s = S-box(x) (FIPS-197 §5.1.1, §5.1.3)        */
+/* ---------------------------------------------------------------------------------------------- */
+
+static uint8_t gf8_mul(uint8_t a, uint8_t b)
+{
+    uint8_t r = 0;
+    for (; b; b >>= 1) {
+        if (b & 1)
+            r ^= a;
+        a = (uint8_t)((a << 1) ^ ((a & 0x80) ? 0x1b : 0));
+    }
+    return r;
+}
+
+static void make_t0(uint32_t t0[256])
+{
+    /* multiplicative inverse by x^254, then the affine map */
+    for (int x = 0; x < 256; ++x) {
+        uint8_t inv = 1, base = (uint8_t)x;
+        for (int e = 254; e; e >>= 1) {
+            if (e & 1)
+                inv = gf8_mul(inv, base);
+            base = gf8_mul(base, base);
+        }
+        if (x == 0)
+            inv = 0;
+        uint8_t s = inv;
+        for (int r = 1; r < 5; ++r)
+            s ^= (uint8_t)((inv << r) | (inv >> (8 - r)));
+        s ^= 0x63;
+        const uint8_t s2 = gf8_mul(s, 2), s3 = gf8_mul(s, 3);
+        t0[x] = (uint32_t)s2 | ((uint32_t)s << 8) | ((uint32_t)s << 16) | ((uint32_t)s3 << 24);
+    }
+}
+
+/* ---------------------------------------------------------------------------------------------- */
+/* objects                                                                                         */
+/* ---------------------------------------------------------------------------------------------- */
+
+struct st_ptls_hip_engine_t {
+    int device;
+    int ncu;
+    uint32_t *d_t0;
+};
+
+struct st_ptls_hip_keyset_t {
+    ptls_hip_engine_t *eng;
+    size_t key_size, nslots;
+    KeySlot *d_slots;
+    uint32_t *d_basis;
+    std::vector<uint8_t> ivs; /* host mirror of every slot's static IV (do_get_iv) */
+};
+
+struct st_ptls_hip_batch_t {
+    ptls_hip_engine_t *eng;
+    size_t n;
+    ptls_hip_record_t *d_recs;
+    std::vector<ptls_hip_record_t> h_recs;
+    Chunk *d_chunks;
+    uint32_t nchunks;
+    int lanes;      /* in use */
+    int auto_lanes; /* chosen from the record lengths */
+    bool forced;
+};
+
+class DeviceGuard {
+  public:
+    explicit DeviceGuard(int dev)
+    {
+        (void)hipGetDevice(&prev_);
+        if (prev_ != dev)
+            (void)hipSetDevice(dev);
+        dev_ = dev;
+    }
+    ~DeviceGuard()
+    {
+        if (prev_ != dev_)
+            (void)hipSetDevice(prev_);
+    }
+
+  private:
+    int prev_ = 0, dev_ = 0;
+};
+
+extern "C" ptls_hip_engine_t *ptls_hip_engine_new(int device)
+{
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) {
+        fail(PTLS_HIP_ENODEV, "no HIP device available");
+        return nullptr;
+    }
+    if (device < 0 || device >= ndev) {
+        fail(PTLS_HIP_EINVAL, "device %d out of range (%d devices)", device, ndev);
+        return nullptr;
+    }
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) != hipSuccess) {
+        fail(PTLS_HIP_ENODEV, "hipGetDeviceProperties failed");
+        return nullptr;
+    }
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) {
+        fail(PTLS_HIP_ENODEV, "device %d is %s, this engine is built for gfx950 only", device, prop.gcnArchName);
+        return nullptr;
+    }
+    DeviceGuard g(device);
+    auto *e = new st_ptls_hip_engine_t();
+    e->device = device;
+    e->ncu = prop.multiProcessorCount;
+    uint32_t t0[256];
+    make_t0(t0);
+    if (hipMalloc(&e->d_t0, sizeof(t0)) != hipSuccess || hipMemcpy(e->d_t0, t0, sizeof(t0), hipMemcpyHostToDevice) != hipSuccess) {
+        fail(PTLS_HIP_ENOMEM, "cannot allocate the AES table on device %d", device);
+        delete e;
+        return nullptr;
+    }
+    return e;
+}
+
+extern "C" void ptls_hip_engine_free(ptls_hip_engine_t *e)
+{
+    if (e == nullptr)
+        return;
+    DeviceGuard g(e->device);
+    (void)hipFree(e->d_t0);
+    delete e;
+}
+
+extern "C" int ptls_hip_engine_device(ptls_hip_engine_t *e)
+{
+    return e->device;
+}
+
+extern "C" int ptls_hip_engine_cu_count(ptls_hip_engine_t *e)
+{
+    return e->ncu;
+}
+
+/* ---------------------------------------------------------------------------------------------- */
+/* keysets                                                                                         */
+/* ---------------------------------------------------------------------------------------------- */
+
+static const size_t BASIS_WORDS_PER_SLOT = (size_t)NPOW * 128 * 4;
+
+extern "C" ptls_hip_keyset_t *ptls_hip_keyset_new(ptls_hip_engine_t *eng, size_t key_size, size_t nslots)
+{
+    if (eng == nullptr || (key_size != 16 && key_size != 32) || nslots == 0 || nslots > 0xffffffffu) {
+        fail(PTLS_HIP_EINVAL, "keyset_new: bad arguments (key_size %zu, nslots %zu)", key_size, nslots);
+        return nullptr;
+    }
+    DeviceGuard g(eng->device);
+    auto *ks = new st_ptls_hip_keyset_t();
+    ks->eng = eng;
+    ks->key_size = key_size;
+    ks->nslots = nslots;
+    ks->ivs.assign(nslots * 12, 0);
+    if (hipMalloc(&ks->d_slots, nslots * sizeof(KeySlot)) != hipSuccess ||
+        hipMalloc(&ks->d_basis, nslots * BASIS_WORDS_PER_SLOT * 4) != hipSuccess) {
+        fail(PTLS_HIP_ENOMEM, "keyset_new: cannot allocate %zu key slots", nslots);
+        (void)hipFree(ks->d_slots);
+        delete ks;
+        return nullptr;
+    }
+    (void)hipMemset(ks->d_slots, 0, nslots * sizeof(KeySlot));
+    return ks;
+}
+
+extern "C" void ptls_hip_keyset_free(ptls_hip_keyset_t *ks)
+{
+    if (ks == nullptr)
+        return;
+    DeviceGuard g(ks->eng->device);
+    /* zeroize key material before release (ptls_clear_memory in aesgcm_dispose_crypto, lib/fusion.c:1102-1107, :1042-1048) */
+    (void)hipMemset(ks->d_slots, 0, ks->nslots * sizeof(KeySlot));
+    (void)hipMemset(ks->d_basis, 0, ks->nslots * BASIS_WORDS_PER_SLOT * 4);
+    (void)hipDeviceSynchronize();
+    (void)hipFree(ks->d_slots);
+    (void)hipFree(ks->d_basis);
+    std::fill(ks->ivs.begin(), ks->ivs.end(), 0);
+    delete ks;
+}
+
+extern "C" size_t ptls_hip_keyset_size(ptls_hip_keyset_t *ks)
+{
+    return ks->nslots;
+}
+
+extern "C" int ptls_hip_keyset_set(ptls_hip_keyset_t *ks, size_t first, size_t count, const void *keys, const void *ivs,
+                                   void *stream)
+{
+    if (ks == nullptr || keys == nullptr || ivs == nullptr || first + count > ks->nslots)
+        return fail(PTLS_HIP_EINVAL, "keyset_set: bad arguments");
+    if (count == 0)
+        return 0;
+    DeviceGuard g(ks->eng->device);
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    uint8_t *d_tmp = nullptr;
+    const size_t kbytes = count * ks->key_size, ibytes = count * 12;
+    HIP_TRY(hipMalloc(&d_tmp, kbytes + ibytes), PTLS_HIP_ENOMEM);
+    int rc = 0;
+    if (hipMemcpyAsync(d_tmp, keys, kbytes, hipMemcpyHostToDevice, s) != hipSuccess ||
+        hipMemcpyAsync(d_tmp + kbytes, ivs, ibytes, hipMemcpyHostToDevice, s) != hipSuccess) {
+        rc = fail(PTLS_HIP_ENODEV, "keyset_set: upload failed");
+    } else {
+        int e = launch_keysetup(ks->d_slots, ks->d_basis, d_tmp, d_tmp + kbytes, (uint32_t)first, (uint32_t)count,
+                                (int)ks->key_size, ks->eng->d_t0, stream);
+        if (e != 0)
+            rc = fail(PTLS_HIP_ELAUNCH, "keyset_set: key setup launch failed: %s", hipGetErrorString((hipError_t)e));
+        else if (hipStreamSynchronize(s) != hipSuccess)
+            rc = fail(PTLS_HIP_ENODEV, "keyset_set: key setup failed");
+    }
+    /* raw keys do not stay in device memory outside the expanded slots */
+    (void)hipMemset(d_tmp, 0, kbytes + ibytes);
+    (void)hipStreamSynchronize(s);
+    (void)hipFree(d_tmp);
+    if (rc == 0)
+        std::memcpy(&ks->ivs[first * 12], ivs, ibytes);
+    return rc;
+}
+
+extern "C" int ptls_hip_keyset_get_iv(ptls_hip_keyset_t *ks, size_t slot, void *iv)
+{
+    if (ks == nullptr || slot >= ks->nslots)
+        return fail(PTLS_HIP_EINVAL, "keyset_get_iv: bad slot");
+    std::memcpy(iv, &ks->ivs[slot * 12], 12);
+    return 0;
+}
+
+extern "C" int ptls_hip_keyset_set_iv(ptls_hip_keyset_t *ks, size_t slot, const void *iv, void *stream)
+{
+    if (ks == nullptr || slot >= ks->nslots)
+        return fail(PTLS_HIP_EINVAL, "keyset_set_iv: bad slot");
+    DeviceGuard g(ks->eng->device);
+    std::memcpy(&ks->ivs[slot * 12], iv, 12);
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    HIP_TRY(hipMemcpyAsync(&ks->d_slots[slot].iv, &ks->ivs[slot * 12], 12, hipMemcpyHostToDevice, s), PTLS_HIP_ENODEV);
+    HIP_TRY(hipStreamSynchronize(s), PTLS_HIP_ENODEV);
+    return 0;
+}
+
+extern "C" int ptls_hip_keyset_xor_iv(ptls_hip_keyset_t *ks, size_t slot, const void *bytes, size_t len, void *stream)
+{
+    if (ks == nullptr || slot >= ks->nslots || len > 12)
+        return fail(PTLS_HIP_EINVAL, "keyset_xor_iv: bad arguments");
+    uint8_t iv[12];
+    std::memcpy(iv, &ks->ivs[slot * 12], 12);
+    for (size_t i = 0; i < len; ++i)
+        iv[i] ^= static_cast<const uint8_t *>(bytes)[i];
+    return ptls_hip_keyset_set_iv(ks, slot, iv, stream);
+}
+
+/* ---------------------------------------------------------------------------------------------- */
+/* batches                                                                                         */
+/* ---------------------------------------------------------------------------------------------- */
+
+/* lanes per record from the mean GHASH length N = ceil(A/16) + ceil(L/16) + 1: keep >= ~16 Horner
+ * steps per lane so the log2(G) reduction tree stays a small fraction of the work */
+static int choose_lanes(const std::vector<ptls_hip_record_t> &recs)
+{
+    if (recs.empty())
+        return 1;
+    double sum = 0;
+    for (const auto &r : recs)
+        sum += (double)((r.aad_len + 15) / 16 + (r.len + 15) / 16 + 1);
+    const double mean = sum / (double)recs.size();
+    return mean >= 128 ? 8 : mean >= 48 ? 4 : mean >= 16 ? 2 : 1;
+}
+
+static int plan_chunks(ptls_hip_batch_t *b)
+{
+    /* chunk = run of records with one key slot, sized to keep all 8 waves busy for a few tasks */
+    const uint32_t per_task = 64u / (uint32_t)b->lanes;
+    const uint32_t max_chunk = per_task * WAVES_PER_WG * 2;
+    std::vector<Chunk> ch;
+    size_t i = 0;
+    while (i < b->n) {
+        Chunk c;
+        c.first = (uint32_t)i;
+        c.key = b->h_recs[i].key;
+        c.count = 0;
+        c.flags = 1;
+        while (i < b->n && b->h_recs[i].key == c.key && c.count < max_chunk) {
+            const auto &r = b->h_recs[i];
+            if (((r.in_off | r.out_off | r.aad_off) & 15) != 0)
+                c.flags = 0;
+            ++c.count;
+            ++i;
+        }
+        ch.push_back(c);
+    }
+    if (b->d_chunks != nullptr)
+        (void)hipFree(b->d_chunks);
+    b->d_chunks = nullptr;
+    b->nchunks = (uint32_t)ch.size();
+    if (ch.empty())
+        return 0;
+    HIP_TRY(hipMalloc(&b->d_chunks, ch.size() * sizeof(Chunk)), PTLS_HIP_ENOMEM);
+    HIP_TRY(hipMemcpy(b->d_chunks, ch.data(), ch.size() * sizeof(Chunk), hipMemcpyHostToDevice), PTLS_HIP_ENODEV);
+    return 0;
+}
+
+extern "C" ptls_hip_batch_t *ptls_hip_batch_new(ptls_hip_engine_t *eng, const ptls_hip_record_t *recs, size_t n, void *stream)
+{
+    (void)stream;
+    if (eng == nullptr || (recs == nullptr && n != 0) || n > 0xffffffffu) {
+        fail(PTLS_HIP_EINVAL, "batch_new: bad arguments");
+        return nullptr;
+    }
+    DeviceGuard g(eng->device);
+    auto *b = new st_ptls_hip_batch_t();
+    b->eng = eng;
+    b->n = n;
+    b->h_recs.assign(recs, recs + n);
+    b->auto_lanes = b->lanes = choose_lanes(b->h_recs);
+    if (n != 0) {
+        if (hipMalloc(&b->d_recs, n * sizeof(ptls_hip_record_t)) != hipSuccess ||
+            hipMemcpy(b->d_recs, recs, n * sizeof(ptls_hip_record_t), hipMemcpyHostToDevice) != hipSuccess) {
+            fail(PTLS_HIP_ENOMEM, "batch_new: cannot upload %zu descriptors", n);
+            (void)hipFree(b->d_recs);
+            delete b;
+            return nullptr;
+        }
+    }
+    if (plan_chunks(b) != 0) {
+        (void)hipFree(b->d_recs);
+        delete b;
+        return nullptr;
+    }
+    return b;
+}
+
+extern "C" void ptls_hip_batch_free(ptls_hip_batch_t *b)
+{
+    if (b == nullptr)
+        return;
+    DeviceGuard g(b->eng->device);
+    (void)hipFree(b->d_recs);
+    (void)hipFree(b->d_chunks);
+    delete b;
+}
+
+extern "C" size_t ptls_hip_batch_count(ptls_hip_batch_t *b)
+{
+    return b->n;
+}
+
+extern "C" int ptls_hip_batch_set_lanes(ptls_hip_batch_t *b, int lanes)
+{
+    if (b == nullptr || !(lanes == 0 || lanes == 1 || lanes == 2 || lanes == 4 || lanes == 8))
+        return fail(PTLS_HIP_EINVAL, "batch_set_lanes: lanes must be 0, 1, 2, 4 or 8");
+    DeviceGuard g(b->eng->device);
+    const int want = lanes == 0 ? b->auto_lanes : lanes;
+    if (want == b->lanes)
+        return 0;
+    b->lanes = want;
+    return plan_chunks(b);
+}
+
+extern "C" int ptls_hip_batch_lanes(ptls_hip_batch_t *b)
+{
+    return b->lanes;
+}
+
+static int run_batch(ptls_hip_batch_t *b, ptls_hip_keyset_t *ks, const void *in, const void *aad, void *out, uint64_t *result,
+                     void *stream, bool open)
+{
+    if (b == nullptr || ks == nullptr || ks->eng != b->eng)
+        return fail(PTLS_HIP_EINVAL, "seal/open: batch and keyset must belong to the same engine");
+    if (b->n == 0)
+        return 0;
+    if (in == nullptr || out == nullptr || (open && result == nullptr))
+        return fail(PTLS_HIP_EINVAL, "seal/open: null buffer");
+    DeviceGuard g(b->eng->device);
+    KernelArgs a{};
+    a.recs = b->d_recs;
+    a.chunks = b->d_chunks;
+    a.nchunks = b->nchunks;
+    a.in = static_cast<const uint8_t *>(in);
+    a.aad = static_cast<const uint8_t *>(aad != nullptr ? aad : in);
+    a.out = static_cast<uint8_t *>(out);
+    a.result = result;
+    a.slots = ks->d_slots;
+    a.basis = ks->d_basis;
+    a.t0 = b->eng->d_t0;
+    const bool base_aligned = ((reinterpret_cast<uintptr_t>(in) | reinterpret_cast<uintptr_t>(a.aad) |
+                                reinterpret_cast<uintptr_t>(out)) & 15) == 0;
+    const unsigned grid = std::min<unsigned>(b->nchunks, (unsigned)b->eng->ncu);
+    const int rounds = ks->key_size == 16 ? 10 : 14;
+    int e = launch_batch(b->lanes, rounds, open, grid, stream, a, base_aligned);
+    if (e != 0)
+        return fail(PTLS_HIP_ELAUNCH, "kernel launch failed: %s", hipGetErrorString((hipError_t)e));
+    return 0;
+}
+
+extern "C" int ptls_hip_aesgcm_seal_batch(ptls_hip_batch_t *b, ptls_hip_keyset_t *ks, const void *in, const void *aad, void *out,
+                                          void *stream)
+{
+    return run_batch(b, ks, in, aad, out, nullptr, stream, false);
+}
+
+extern "C" int ptls_hip_aesgcm_open_batch(ptls_hip_batch_t *b, ptls_hip_keyset_t *ks, const void *in, const void *aad, void *out,
+                                          uint64_t *result, void *stream)
+{
+    return run_batch(b, ks, in, aad, out, result, stream, true);
+}
+
+extern "C" int ptls_hip_fill_records(ptls_hip_batch_t *b, void *buf, uint64_t seed, uint64_t index_base, const uint64_t *index,
+                                     void *stream)
+{
+    if (b == nullptr || buf == nullptr)
+        return fail(PTLS_HIP_EINVAL, "fill_records: bad arguments");
+    if (b->n == 0)
+        return 0;
+    DeviceGuard g(b->eng->device);
+    const unsigned grid = (unsigned)std::min<size_t>((b->n + 3) / 4, (size_t)b->eng->ncu * 16);
+    int e = launch_fill(b->d_recs, (uint32_t)b->n, static_cast<uint8_t *>(buf), seed, index_base, index, grid, stream);
+    if (e != 0)
+        return fail(PTLS_HIP_ELAUNCH, "fill launch failed: %s", hipGetErrorString((hipError_t)e));
+    return 0;
+}
+
+/* ---------------------------------------------------------------------------------------------- */
+/* picotls plugin: ptls_hip_aes128gcm / ptls_hip_aes256gcm                                         */
+/* ---------------------------------------------------------------------------------------------- */
+
+static std::mutex g_plugin_mu;
+static ptls_hip_engine_t *g_plugin_engine = nullptr;
+static int g_plugin_device = -1;
+
+extern "C" int ptls_hip_set_default_device(int device)
+{
+    std::lock_guard<std::mutex> lk(g_plugin_mu);
+    if (g_plugin_engine != nullptr)
+        return fail(PTLS_HIP_EINVAL, "set_default_device: contexts already created on device %d", g_plugin_engine->device);
+    g_plugin_device = device;
+    return 0;
+}
+
+static ptls_hip_engine_t *plugin_engine(void)
+{
+    std::lock_guard<std::mutex> lk(g_plugin_mu);
+    if (g_plugin_engine == nullptr) {
+        int dev = g_plugin_device;
+        if (dev < 0) {
+            const char *env = getenv("PTLS_HIP_DEVICE");
+            dev = env != nullptr ? atoi(env) : 0;
+        }
+        g_plugin_engine = ptls_hip_engine_new(dev);
+    }
+    return g_plugin_engine;
+}
+
+/* per-context state: one key slot plus device staging for one record */
+struct hip_aead_state {
+    ptls_hip_engine_t *eng;
+    ptls_hip_keyset_t *ks;
+    hipStream_t stream;
+    uint8_t *d_buf; /* [in: cap][out: cap + 16][aad: aad_cap] */
+    size_t cap, aad_cap;
+    ptls_hip_record_t *d_rec;
+    Chunk *d_chunk;
+    uint64_t *d_result;
+    uint8_t *h_stage; /* pinned: record + chunk + result */
+    uint8_t iv[12];
+    bool iv_dirty;
+};
+
+struct hip_aead_context {
+    ptls_aead_context_t super;
+    hip_aead_state *st;
+};
+
+[[noreturn]] static void plugin_die(const char *what)
+{
+    fprintf(stderr, "ptls_hip: fatal device error in %s: %s\n", what, g_err.c_str());
+    abort();
+}
+
+static void plugin_check(hipError_t e, const char *what)
+{
+    if (e != hipSuccess) {
+        g_err = hipGetErrorString(e);
+        plugin_die(what);
+    }
+}
+
+static void state_reserve(hip_aead_state *st, size_t len, size_t aadlen)
+{
+    if (len <= st->cap && aadlen <= st->aad_cap)
+        return;
+    size_t cap = std::max(st->cap, (size_t)2048), aad_cap = std::max(st->aad_cap, (size_t)256);
+    while (cap < len)
+        cap *= 2;
+    while (aad_cap < aadlen)
+        aad_cap *= 2;
+    cap = (cap + 15) & ~(size_t)15;
+    aad_cap = (aad_cap + 15) & ~(size_t)15;
+    if (st->d_buf != nullptr)
+        plugin_check(hipFree(st->d_buf), "hipFree");
+    plugin_check(hipMalloc(&st->d_buf, cap + (cap + 16) + aad_cap), "hipMalloc(staging)");
+    st->cap = cap;
+    st->aad_cap = aad_cap;
+}
+
+/* run one record through the batch kernel: in/out/aad are host buffers */
+static uint64_t plugin_run(hip_aead_state *st, bool open, void *output, const void *input, size_t len, uint64_t seq,
+                           const void *aad, size_t aadlen)
+{
+    DeviceGuard g(st->eng->device);
+    const size_t in_len = open ? len + 16 : len;
+    state_reserve(st, in_len, aadlen);
+    if (st->iv_dirty) {
+        if (ptls_hip_keyset_set_iv(st->ks, 0, st->iv, st->stream) != 0)
+            plugin_die("set_iv");
+        st->iv_dirty = false;
+    }
+    uint8_t *d_in = st->d_buf, *d_out = st->d_buf + st->cap, *d_aad = st->d_buf + st->cap + st->cap + 16;
+    ptls_hip_record_t rec{};
+    rec.in_off = 0;
+    rec.out_off = 0;
+    rec.aad_off = 0;
+    rec.seq = seq;
+    rec.len = (uint32_t)len;
+    rec.aad_len = (uint32_t)aadlen;
+    rec.key = 0;
+    Chunk ch{0, 1, 0, 1};
+    std::memcpy(st->h_stage, &rec, sizeof(rec));
+    std::memcpy(st->h_stage + 64, &ch, sizeof(ch));
+    plugin_check(hipMemcpyAsync(st->d_rec, st->h_stage, 64 + sizeof(ch), hipMemcpyHostToDevice, st->stream), "upload(rec)");
+    if (in_len != 0)
+        plugin_check(hipMemcpyAsync(d_in, input, in_len, hipMemcpyHostToDevice, st->stream), "upload(in)");
+    if (aadlen != 0)
+        plugin_check(hipMemcpyAsync(d_aad, aad, aadlen, hipMemcpyHostToDevice, st->stream), "upload(aad)");
+    KernelArgs a{};
+    a.recs = st->d_rec;
+    a.chunks = st->d_chunk;
+    a.nchunks = 1;
+    a.in = d_in;
+    a.aad = d_aad;
+    a.out = d_out;
+    a.result = st->d_result;
+    a.slots = st->ks->d_slots;
+    a.basis = st->ks->d_basis;
+    a.t0 = st->eng->d_t0;
+    const size_t n = (aadlen + 15) / 16 + (len + 15) / 16 + 1;
+    const int lanes = n >= 128 ? 8 : n >= 48 ? 4 : n >= 16 ? 2 : 1;
+    int e = launch_batch(lanes, st->ks->key_size == 16 ? 10 : 14, open, 1, st->stream, a, true);
+    if (e != 0) {
+        g_err = hipGetErrorString((hipError_t)e);
+        plugin_die("launch");
+    }
+    uint64_t result = len;
+    if (open) {
+        if (len != 0)
+            plugin_check(hipMemcpyAsync(output, d_out, len, hipMemcpyDeviceToHost, st->stream), "download(out)");
+        plugin_check(hipMemcpyAsync(st->h_stage + 128, st->d_result, 8, hipMemcpyDeviceToHost, st->stream), "download(result)");
+    } else {
+        plugin_check(hipMemcpyAsync(output, d_out, len + 16, hipMemcpyDeviceToHost, st->stream), "download(out)");
+    }
+    plugin_check(hipStreamSynchronize(st->stream), "hipStreamSynchronize");
+    if (open)
+        std::memcpy(&result, st->h_stage + 128, 8);
+    return result;
+}
+
+static void aead_dispose(ptls_aead_context_t *_ctx)
+{
+    auto *ctx = reinterpret_cast<hip_aead_context *>(_ctx);
+    hip_aead_state *st = ctx->st;
+    if (st == nullptr)
+        return;
+    {
+        DeviceGuard g(st->eng->device);
+        ptls_hip_keyset_free(st->ks);
+        if (st->d_buf != nullptr) {
+            (void)hipMemset(st->d_buf, 0, st->cap + st->cap + 16 + st->aad_cap);
+            (void)hipStreamSynchronize(st->stream);
+            (void)hipFree(st->d_buf);
+        }
+        (void)hipFree(st->d_rec);
+        (void)hipHostFree(st->h_stage);
+        (void)hipStreamDestroy(st->stream);
+    }
+    std::memset(st->iv, 0, sizeof(st->iv));
+    delete st;
+    ctx->st = nullptr;
+}
+
+static void aead_get_iv(ptls_aead_context_t *_ctx, void *iv)
+{
+    std::memcpy(iv, reinterpret_cast<hip_aead_context *>(_ctx)->st->iv, 12);
+}
+
+static void aead_set_iv(ptls_aead_context_t *_ctx, const void *iv)
+{
+    hip_aead_state *st = reinterpret_cast<hip_aead_context *>(_ctx)->st;
+    std::memcpy(st->iv, iv, 12);
+    st->iv_dirty = true;
+}
+
+static void aead_encrypt_init(ptls_aead_context_t *, uint64_t, const void *, size_t)
+{
+    fprintf(stderr, "ptls_hip: do_encrypt_init is deprecated and not supported\n");
+    abort();
+}
+
+static size_t aead_encrypt_update(ptls_aead_context_t *, void *, const void *, size_t)
+{
+    fprintf(stderr, "ptls_hip: do_encrypt_update is deprecated and not supported\n");
+    abort();
+}
+
+static size_t aead_encrypt_final(ptls_aead_context_t *, void *)
+{
+    fprintf(stderr, "ptls_hip: do_encrypt_final is deprecated and not supported\n");
+    abort();
+}
+
+static void aead_encrypt(ptls_aead_context_t *_ctx, void *output, const void *input, size_t inlen, uint64_t seq, const void *aad,
+                         size_t aadlen, ptls_aead_supplementary_encryption_t *supp)
+{
+    hip_aead_state *st = reinterpret_cast<hip_aead_context *>(_ctx)->st;
+    plugin_run(st, false, output, input, inlen, seq, aad, aadlen);
+    if (supp != nullptr) {
+        /* header-protection mask from the caller's cipher context, computed after the AEAD output exists
+         * (ptls_aead__do_encrypt, include/picotls.h:2027-2038; fusion fuses it, lib/fusion.c:636-650) */
+        supp->ctx->do_init(supp->ctx, supp->input);
+        std::memset(supp->output, 0, sizeof(supp->output));
+        supp->ctx->do_transform(supp->ctx, supp->output, supp->output, sizeof(supp->output));
+    }
+}
+
+static void aead_encrypt_v(ptls_aead_context_t *_ctx, void *output, ptls_iovec_t *input, size_t incnt, uint64_t seq,
+                           const void *aad, size_t aadlen)
+{
+    size_t total = 0;
+    for (size_t i = 0; i < incnt; ++i)
+        total += input[i].len;
+    std::vector<uint8_t> flat(total);
+    size_t off = 0;
+    for (size_t i = 0; i < incnt; ++i) {
+        if (input[i].len != 0)
+            std::memcpy(flat.data() + off, input[i].base, input[i].len);
+        off += input[i].len;
+    }
+    plugin_run(reinterpret_cast<hip_aead_context *>(_ctx)->st, false, output, flat.data(), total, seq, aad, aadlen);
+}
+
+static size_t aead_decrypt(ptls_aead_context_t *_ctx, void *output, const void *input, size_t inlen, uint64_t seq, const void *aad,
+                           size_t aadlen)
+{
+    if (inlen < 16)
+        return SIZE_MAX;
+    const uint64_t r = plugin_run(reinterpret_cast<hip_aead_context *>(_ctx)->st, true, output, input, inlen - 16, seq, aad, aadlen);
+    return r == ~(uint64_t)0 ? SIZE_MAX : (size_t)r;
+}
+
+static int aesgcm_setup(ptls_aead_context_t *_ctx, int is_enc, const void *key, const void *iv, size_t key_size)
+{
+    (void)is_enc; /* one context seals and opens, as fusion's (lib/fusion.c:1184-1206) */
+    auto *ctx = reinterpret_cast<hip_aead_context *>(_ctx);
+    if (key == nullptr) { /* IV-only re-setup (lib/fusion.c:1190-1191) */
+        if (ctx->st == nullptr)
+            return -1;
+        aead_set_iv(_ctx, iv);
+        return 0;
+    }
+    ctx->st = nullptr;
+    ptls_hip_engine_t *eng = plugin_engine();
+    if (eng == nullptr)
+        return -1;
+    DeviceGuard g(eng->device);
+    auto *st = new hip_aead_state();
+    st->eng = eng;
+    if (hipStreamCreateWithFlags(&st->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete st;
+        return -1;
+    }
+    st->ks = ptls_hip_keyset_new(eng, key_size, 1);
+    bool ok = st->ks != nullptr && hipMalloc(&st->d_rec, 256) == hipSuccess &&
+              hipHostMalloc(&st->h_stage, 256, hipHostMallocDefault) == hipSuccess &&
+              ptls_hip_keyset_set(st->ks, 0, 1, key, iv, st->stream) == 0;
+    if (!ok) {
+        if (st->ks != nullptr)
+            ptls_hip_keyset_free(st->ks);
+        (void)hipFree(st->d_rec);
+        (void)hipHostFree(st->h_stage);
+        (void)hipStreamDestroy(st->stream);
+        delete st;
+        return -1;
+    }
+    st->d_chunk = reinterpret_cast<Chunk *>(reinterpret_cast<uint8_t *>(st->d_rec) + 64);
+    st->d_result = reinterpret_cast<uint64_t *>(reinterpret_cast<uint8_t *>(st->d_rec) + 128);
+    std::memcpy(st->iv, iv, 12);
+    st->iv_dirty = false;
+    ctx->st = st;
+    ctx->super.dispose_crypto = aead_dispose;
+    ctx->super.do_get_iv = aead_get_iv;
+    ctx->super.do_set_iv = aead_set_iv;
+    ctx->super.do_encrypt_init = aead_encrypt_init;
+    ctx->super.do_encrypt_update = aead_encrypt_update;
+    ctx->super.do_encrypt_final = aead_encrypt_final;
+    ctx->super.do_encrypt = aead_encrypt;
+    ctx->super.do_encrypt_v = aead_encrypt_v;
+    ctx->super.do_decrypt = aead_decrypt;
+    return 0;
+}
+
+static int aes128gcm_setup(ptls_aead_context_t *ctx, int is_enc, const void *key, const void *iv)
+{
+    return aesgcm_setup(ctx, is_enc, key, iv, PTLS_AES128_KEY_SIZE);
+}
+
+static int aes256gcm_setup(ptls_aead_context_t *ctx, int is_enc, const void *key, const void *iv)
+{
+    return aesgcm_setup(ctx, is_enc, key, iv, PTLS_AES256_KEY_SIZE);
+}
+
+/* Field-for-field the values of ptls_fusion_aes{128,256}gcm (lib/fusion.c:1231-1256), except that no
+ * CTR cipher object is advertised yet (QUIC header protection fused into the batch kernel is a
+ * "next" row). */
+extern "C" {
+ptls_aead_algorithm_t ptls_hip_aes128gcm = {"AES128-GCM",
+                                            PTLS_AESGCM_CONFIDENTIALITY_LIMIT,
+                                            PTLS_AESGCM_INTEGRITY_LIMIT,
+                                            nullptr,
+                                            nullptr,
+                                            PTLS_AES128_KEY_SIZE,
+                                            PTLS_AESGCM_IV_SIZE,
+                                            PTLS_AESGCM_TAG_SIZE,
+                                            {0, 0},
+                                            0,
+                                            0,
+                                            sizeof(hip_aead_context),
+                                            aes128gcm_setup};
+ptls_aead_algorithm_t ptls_hip_aes256gcm = {"AES256-GCM",
+                                            PTLS_AESGCM_CONFIDENTIALITY_LIMIT,
+                                            PTLS_AESGCM_INTEGRITY_LIMIT,
+                                            nullptr,
+                                            nullptr,
+                                            PTLS_AES256_KEY_SIZE,
+                                            PTLS_AESGCM_IV_SIZE,
+                                            PTLS_AESGCM_TAG_SIZE,
+                                            {0, 0},
+                                            0,
+                                            0,
+                                            sizeof(hip_aead_context),
+                                            aes256gcm_setup};
+}

@@ -1,0 +1,63 @@
+/*
+ * internal.h -- layouts shared by the host engine (engine.cpp) and the gfx950 kernels (aesgcm_kernels.hip).
+ *
+ * HBM layout:
+ *   key slots    KeySlot[nslots]             512 B each: round keys, static IV, H powers
+ *   GHASH basis  uint4[nslots][NPOW][128]    8 KiB per slot: P * x^e for P in {H, H^2, H^4, H^8}
+ *   records      ptls_hip_record_t[n]        48 B descriptors (caller's order)
+ *   chunks       Chunk[nchunks]              runs of <= CHUNK_RECS records sharing one key slot
+ *   payloads     caller's buffers, untouched layout (in / aad / out)
+ */
+#ifndef PTLS_HIP_INTERNAL_H
+#define PTLS_HIP_INTERNAL_H
+
+#include <stdint.h>
+#include "ptls_hip.h"
+
+namespace ptls_hip {
+
+constexpr int NPOW = 4;          /* H^1, H^2, H^4, H^8 */
+constexpr int MAX_LANES = 8;     /* lanes per record (G) supported: 1, 2, 4, 8 */
+constexpr int WG_THREADS = 512;  /* 8 waves: one workgroup per CU (LDS-limited) */
+constexpr int WAVES_PER_WG = WG_THREADS / 64;
+
+struct KeySlot {
+    uint32_t rk[60];      /* AES round keys, raw byte order as little-endian words (11 or 15 used) */
+    uint32_t rounds;      /* 10 or 14 */
+    uint32_t iv[3];       /* static IV (12 bytes, raw) */
+    uint32_t hpow[NPOW][4]; /* H^(2^t), raw GCM byte order */
+    uint32_t pad[(512 - 240 - 4 - 12 - 16 * NPOW) / 4];
+};
+static_assert(sizeof(KeySlot) == 512, "KeySlot must stay 512 bytes");
+
+struct Chunk {
+    uint32_t first; /* index of first record */
+    uint32_t count; /* records in the chunk, all with the same key slot */
+    uint32_t key;   /* key slot */
+    uint32_t flags; /* bit0: every record of the chunk is 16-byte aligned (in/out/aad offsets) */
+};
+
+struct KernelArgs {
+    const ptls_hip_record_t *recs;
+    const Chunk *chunks;
+    uint32_t nchunks;
+    uint32_t pad0;
+    const uint8_t *in;
+    const uint8_t *aad;
+    uint8_t *out;
+    uint64_t *result;       /* open only */
+    const KeySlot *slots;
+    const uint32_t *basis;  /* uint4 [slot][NPOW][128] */
+    const uint32_t *t0;     /* AES T0 table, 256 words */
+};
+
+/* host-side launchers, defined next to the kernels (aesgcm_kernels.hip) */
+int launch_batch(int lanes, int rounds, bool open, unsigned grid, void *stream, const KernelArgs &a, bool base_aligned);
+int launch_keysetup(KeySlot *slots, uint32_t *basis, const uint8_t *keys, const uint8_t *ivs, uint32_t first, uint32_t count,
+                    int key_size, const uint32_t *t0, void *stream);
+int launch_fill(const ptls_hip_record_t *recs, uint32_t n, uint8_t *buf, uint64_t seed, uint64_t index_base,
+                const uint64_t *index, unsigned grid, void *stream);
+
+} // namespace ptls_hip
+
+#endif

@@ -1,0 +1,210 @@
+"""ctypes binding of libptls_hip.so (include/ptls_hip.h) for tests and bench.py.
+
+Device memory and streams come from PyTorch (plumbing only); every byte of crypto runs in the HIP
+kernels of libptls_hip.so.  There is no Python or CPU fallback: if the library or a gfx950 device
+is missing, the constructors raise.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libptls_hip.so")
+UINT64_MAX = (1 << 64) - 1
+
+RECORD_DTYPE = np.dtype([("in_off", "<u8"), ("out_off", "<u8"), ("aad_off", "<u8"), ("seq", "<u8"),
+                         ("len", "<u4"), ("aad_len", "<u4"), ("key", "<u4"), ("flags", "<u4")])
+assert RECORD_DTYPE.itemsize == 48
+
+# every function declared in include/ptls_hip.h: (restype, argtypes)
+_vp, _sz, _i, _u64 = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_uint64
+SIGNATURES = {
+    "ptls_hip_last_error": (ctypes.c_char_p, []),
+    "ptls_hip_set_default_device": (_i, [_i]),
+    "ptls_hip_engine_new": (_vp, [_i]),
+    "ptls_hip_engine_free": (None, [_vp]),
+    "ptls_hip_engine_device": (_i, [_vp]),
+    "ptls_hip_engine_cu_count": (_i, [_vp]),
+    "ptls_hip_keyset_new": (_vp, [_vp, _sz, _sz]),
+    "ptls_hip_keyset_free": (None, [_vp]),
+    "ptls_hip_keyset_size": (_sz, [_vp]),
+    "ptls_hip_keyset_set": (_i, [_vp, _sz, _sz, _vp, _vp, _vp]),
+    "ptls_hip_keyset_get_iv": (_i, [_vp, _sz, _vp]),
+    "ptls_hip_keyset_set_iv": (_i, [_vp, _sz, _vp, _vp]),
+    "ptls_hip_keyset_xor_iv": (_i, [_vp, _sz, _vp, _sz, _vp]),
+    "ptls_hip_batch_new": (_vp, [_vp, _vp, _sz, _vp]),
+    "ptls_hip_batch_free": (None, [_vp]),
+    "ptls_hip_batch_count": (_sz, [_vp]),
+    "ptls_hip_batch_set_lanes": (_i, [_vp, _i]),
+    "ptls_hip_batch_lanes": (_i, [_vp]),
+    "ptls_hip_aesgcm_seal_batch": (_i, [_vp, _vp, _vp, _vp, _vp, _vp]),
+    "ptls_hip_aesgcm_open_batch": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "ptls_hip_fill_records": (_i, [_vp, _vp, _u64, _u64, _vp, _vp]),
+}
+DATA_SYMBOLS = ("ptls_hip_aes128gcm", "ptls_hip_aes256gcm")
+
+_lib = None
+
+
+class HipError(RuntimeError):
+    pass
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise HipError(f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'`")
+        L = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = L
+    return _lib
+
+
+def last_error():
+    return lib().ptls_hip_last_error().decode()
+
+
+def _check(rc, what):
+    if rc != 0:
+        raise HipError(f"{what}: {last_error()} (rc={rc})")
+
+
+def _ptr(x):
+    """device/host pointer of a torch tensor, numpy array, int or None"""
+    if x is None:
+        return None
+    if isinstance(x, int):
+        return x
+    if hasattr(x, "data_ptr"):
+        return x.data_ptr()
+    if isinstance(x, np.ndarray):
+        return x.ctypes.data
+    raise TypeError(type(x))
+
+
+def _stream(stream):
+    if stream is None:
+        try:
+            import torch
+            return torch.cuda.current_stream().cuda_stream
+        except Exception:  # noqa: BLE001
+            return None
+    return stream if isinstance(stream, int) else getattr(stream, "cuda_stream", stream)
+
+
+class Engine:
+    def __init__(self, device=0):
+        self.ptr = lib().ptls_hip_engine_new(device)
+        if not self.ptr:
+            raise HipError(f"ptls_hip_engine_new({device}): {last_error()}")
+        self.device = device
+
+    @property
+    def cu_count(self):
+        return lib().ptls_hip_engine_cu_count(self.ptr)
+
+    def close(self):
+        if self.ptr:
+            lib().ptls_hip_engine_free(self.ptr)
+            self.ptr = None
+
+
+class KeySet:
+    def __init__(self, engine, key_size, nslots):
+        self.engine, self.key_size, self.nslots = engine, key_size, nslots
+        self.ptr = lib().ptls_hip_keyset_new(engine.ptr, key_size, nslots)
+        if not self.ptr:
+            raise HipError(f"ptls_hip_keyset_new: {last_error()}")
+
+    def set(self, first, keys, ivs, stream=None):
+        keys, ivs = bytes(keys), bytes(ivs)
+        count = len(keys) // self.key_size
+        assert len(keys) == count * self.key_size and len(ivs) == count * 12
+        _check(lib().ptls_hip_keyset_set(self.ptr, first, count, keys, ivs, _stream(stream)), "keyset_set")
+
+    def get_iv(self, slot):
+        buf = ctypes.create_string_buffer(12)
+        _check(lib().ptls_hip_keyset_get_iv(self.ptr, slot, buf), "keyset_get_iv")
+        return buf.raw
+
+    def set_iv(self, slot, iv, stream=None):
+        _check(lib().ptls_hip_keyset_set_iv(self.ptr, slot, bytes(iv), _stream(stream)), "keyset_set_iv")
+
+    def xor_iv(self, slot, data, stream=None):
+        _check(lib().ptls_hip_keyset_xor_iv(self.ptr, slot, bytes(data), len(data), _stream(stream)), "keyset_xor_iv")
+
+    def close(self):
+        if self.ptr:
+            lib().ptls_hip_keyset_free(self.ptr)
+            self.ptr = None
+
+
+class Batch:
+    def __init__(self, engine, recs, stream=None):
+        recs = np.ascontiguousarray(recs, dtype=RECORD_DTYPE)
+        self.engine, self.recs = engine, recs
+        self.ptr = lib().ptls_hip_batch_new(engine.ptr, recs.ctypes.data, len(recs), _stream(stream))
+        if not self.ptr:
+            raise HipError(f"ptls_hip_batch_new: {last_error()}")
+
+    def __len__(self):
+        return len(self.recs)
+
+    @property
+    def lanes(self):
+        return lib().ptls_hip_batch_lanes(self.ptr)
+
+    def set_lanes(self, lanes):
+        _check(lib().ptls_hip_batch_set_lanes(self.ptr, lanes), "batch_set_lanes")
+
+    def seal(self, keyset, inp, aad, out, stream=None):
+        _check(lib().ptls_hip_aesgcm_seal_batch(self.ptr, keyset.ptr, _ptr(inp), _ptr(aad), _ptr(out), _stream(stream)),
+               "seal_batch")
+
+    def open(self, keyset, inp, aad, out, result, stream=None):
+        _check(lib().ptls_hip_aesgcm_open_batch(self.ptr, keyset.ptr, _ptr(inp), _ptr(aad), _ptr(out), _ptr(result),
+                                                _stream(stream)), "open_batch")
+
+    def fill(self, buf, seed, index_base=0, index=None, stream=None):
+        """index: optional device tensor (int64/uint64) of per-descriptor generator indices"""
+        _check(lib().ptls_hip_fill_records(self.ptr, _ptr(buf), seed, index_base, _ptr(index), _stream(stream)),
+               "fill_records")
+
+    def close(self):
+        if self.ptr:
+            lib().ptls_hip_batch_free(self.ptr)
+            self.ptr = None
+
+
+def layout_records(lens, aad_lens, keys, seqs, align=16, tag_in_input=False):
+    """Pack records into in / out / aad buffers with `align`-byte aligned offsets.
+
+    Returns (recs, in_bytes, out_bytes, aad_bytes).  in holds L (+16 if tag_in_input) per record,
+    out holds L + 16 (seal output: ct || tag)."""
+    lens = np.asarray(lens, dtype=np.uint64)
+    aad_lens = np.asarray(aad_lens, dtype=np.uint64)
+    n = len(lens)
+    a = np.uint64(align)
+
+    def offsets(sizes):
+        padded = (sizes + a - np.uint64(1)) // a * a
+        off = np.zeros(n, dtype=np.uint64)
+        if n > 1:
+            np.cumsum(padded[:-1], out=off[1:])
+        total = int(off[-1] + padded[-1]) if n else 0
+        return off, total
+
+    recs = np.zeros(n, dtype=RECORD_DTYPE)
+    recs["in_off"], in_total = offsets(lens + (np.uint64(16) if tag_in_input else np.uint64(0)))
+    recs["out_off"], out_total = offsets(lens + np.uint64(16))
+    recs["aad_off"], aad_total = offsets(aad_lens)
+    recs["len"] = lens
+    recs["aad_len"] = aad_lens
+    recs["key"] = keys
+    recs["seq"] = seqs
+    return recs, in_total, out_total, max(aad_total, 16)

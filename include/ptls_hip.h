@@ -1,0 +1,133 @@
+/*
+ * ptls_hip.h -- MI355X (gfx950) AES-GCM record-protection engine for picotls.
+ *
+ * Two faces, one library (libptls_hip.so):
+ *
+ * 1. The picotls plugin surface.  `ptls_hip_aes128gcm` / `ptls_hip_aes256gcm` are ordinary
+ *    `ptls_aead_algorithm_t` objects, interchangeable with `ptls_fusion_aes128gcm` /
+ *    `ptls_fusion_aes256gcm` (reference: lib/fusion.c:1231-1256, include/picotls/fusion.h:104).
+ *    Create contexts with picotls's own `ptls_aead_new` / `ptls_aead_new_direct`
+ *    (lib/picotls.c:6452-6473) and use `ptls_aead_encrypt*` / `ptls_aead_decrypt`
+ *    (include/picotls.h:1993-2055).  Each call is synchronous and runs one record on the GPU.
+ *
+ * 2. The batch extension (picotls has no batch API).  Many independent records, each with its own
+ *    key slot, sequence number, AAD, input and output, are sealed or opened by one asynchronous
+ *    kernel launch on a HIP stream.  Inputs and outputs are device pointers.  This is the
+ *    throughput path measured by bench.py.
+ *
+ * Plain C ABI: pointers, sizes, integers.  `stream` is a hipStream_t passed as void* (NULL = the
+ * null stream).  Functions returning int give 0 on success and a negative PTLS_HIP_E* code on
+ * failure; `ptls_hip_last_error()` describes the most recent failure on the calling thread.
+ */
+#ifndef PTLS_HIP_H
+#define PTLS_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+#include "picotls_plugin_abi.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PTLS_HIP_EINVAL (-1)   /* bad argument */
+#define PTLS_HIP_ENODEV (-2)   /* no usable gfx950 device / HIP runtime failure */
+#define PTLS_HIP_ENOMEM (-3)   /* device or host allocation failed */
+#define PTLS_HIP_ELAUNCH (-4)  /* kernel launch failed */
+
+const char *ptls_hip_last_error(void);
+
+/* ------------------------------------------------------------------------------------------ *
+ * 1. picotls plugin objects                                                                   *
+ * ------------------------------------------------------------------------------------------ */
+
+/* Replace ptls_fusion_aes128gcm / ptls_fusion_aes256gcm (lib/fusion.c:1231-1256).
+ * setup_crypto returns non-zero (=> ptls_aead_new returns NULL) when no gfx950 device is usable;
+ * key == NULL re-sets the static IV only (as fusion's aesgcm_setup, lib/fusion.c:1188-1191).
+ * do_encrypt / do_encrypt_v / do_decrypt match lib/fusion.c:1135-1166 byte for byte, and in
+ * addition implement do_encrypt_v (fusion asserts "FIXME" there, lib/fusion.c:1145-1149). */
+extern ptls_aead_algorithm_t ptls_hip_aes128gcm, ptls_hip_aes256gcm;
+
+/* Device ordinal used by contexts created through the plugin objects (default 0; also read from
+ * the environment variable PTLS_HIP_DEVICE).  Must be called before the first context is made. */
+int ptls_hip_set_default_device(int device);
+
+/* ------------------------------------------------------------------------------------------ *
+ * 2. batch extension                                                                          *
+ * ------------------------------------------------------------------------------------------ */
+
+typedef struct st_ptls_hip_engine_t ptls_hip_engine_t;
+typedef struct st_ptls_hip_keyset_t ptls_hip_keyset_t;
+typedef struct st_ptls_hip_batch_t ptls_hip_batch_t;
+
+/* One engine per device: owns the device's AES tables and the launch configuration. */
+ptls_hip_engine_t *ptls_hip_engine_new(int device);
+void ptls_hip_engine_free(ptls_hip_engine_t *engine);
+int ptls_hip_engine_device(ptls_hip_engine_t *engine);
+int ptls_hip_engine_cu_count(ptls_hip_engine_t *engine);
+
+/* A keyset is an array of device-resident AEAD contexts ("key slots"), all AES-128 (key_size 16)
+ * or all AES-256 (key_size 32).  Slot i corresponds to one ptls_aead_context_t of the plugin
+ * surface: key schedule, GHASH key powers and the 12-byte static IV. */
+ptls_hip_keyset_t *ptls_hip_keyset_new(ptls_hip_engine_t *engine, size_t key_size, size_t nslots);
+void ptls_hip_keyset_free(ptls_hip_keyset_t *ks); /* zeroizes device key material */
+size_t ptls_hip_keyset_size(ptls_hip_keyset_t *ks);
+/* Load `count` keys (count * key_size bytes) and static IVs (count * 12 bytes) from host memory into
+ * slots [first, first + count) and expand them on the device (key schedule, H = E_K(0), powers of H).
+ * Equivalent to setup_crypto(ctx, is_enc, key, iv) for each slot (lib/fusion.c:1184-1206). */
+int ptls_hip_keyset_set(ptls_hip_keyset_t *ks, size_t first, size_t count, const void *keys, const void *ivs, void *stream);
+/* Static-IV get/set of one slot (do_get_iv / do_set_iv, lib/fusion.c:1168-1182); with
+ * ptls_hip_keyset_xor_iv this gives ptls_aead_xor_iv semantics (lib/picotls.c:6481-6490). */
+int ptls_hip_keyset_get_iv(ptls_hip_keyset_t *ks, size_t slot, void *iv);
+int ptls_hip_keyset_set_iv(ptls_hip_keyset_t *ks, size_t slot, const void *iv, void *stream);
+int ptls_hip_keyset_xor_iv(ptls_hip_keyset_t *ks, size_t slot, const void *bytes, size_t len, void *stream);
+
+/* Record descriptor (48 bytes).  Offsets are byte offsets into the buffers passed to seal/open.
+ *   seal: reads len bytes at in+in_off, writes len bytes of ciphertext and the 16-byte tag at
+ *         out+out_off (len + 16 bytes), like ptls_aead_encrypt (include/picotls.h:1993).
+ *   open: reads len bytes of ciphertext followed by the 16-byte tag at in+in_off, writes len bytes
+ *         of plaintext at out+out_off (always, like fusion's decrypt-then-verify), and sets
+ *         result[i] = len on success or UINT64_MAX on authentication failure (the SIZE_MAX of
+ *         ptls_aead_decrypt, lib/fusion.c:1151-1166).
+ * The nonce is slot.iv with bytes 4..11 XORed with big-endian seq (ptls_aead__build_iv,
+ * lib/picotls.c:6492-6506).  in == out (in place) is allowed.  For full speed keep in_off, out_off
+ * 16-byte aligned and put records of the same key next to each other. */
+typedef struct st_ptls_hip_record_t {
+    uint64_t in_off;
+    uint64_t out_off;
+    uint64_t aad_off;
+    uint64_t seq;
+    uint32_t len;
+    uint32_t aad_len;
+    uint32_t key;   /* key slot index */
+    uint32_t flags; /* reserved, must be 0 */
+} ptls_hip_record_t;
+
+/* Upload `n` host descriptors and plan the launch (runs of equal key slot, lane-group width from the
+ * record lengths).  A batch is reusable for any number of seal/open calls over same-shaped buffers. */
+ptls_hip_batch_t *ptls_hip_batch_new(ptls_hip_engine_t *engine, const ptls_hip_record_t *recs, size_t n, void *stream);
+void ptls_hip_batch_free(ptls_hip_batch_t *batch);
+size_t ptls_hip_batch_count(ptls_hip_batch_t *batch);
+/* lanes cooperating on one record (1, 2, 4 or 8); 0 = automatic (default).  For tuning and tests. */
+int ptls_hip_batch_set_lanes(ptls_hip_batch_t *batch, int lanes);
+int ptls_hip_batch_lanes(ptls_hip_batch_t *batch);
+
+/* Asynchronous on `stream`; all pointers are device (or device-accessible) memory. */
+int ptls_hip_aesgcm_seal_batch(ptls_hip_batch_t *batch, ptls_hip_keyset_t *ks, const void *in, const void *aad, void *out,
+                               void *stream);
+int ptls_hip_aesgcm_open_batch(ptls_hip_batch_t *batch, ptls_hip_keyset_t *ks, const void *in, const void *aad, void *out,
+                               uint64_t *result, void *stream);
+
+/* ------------------------------------------------------------------------------------------ *
+ * 3. synthetic workload (bench / tests): the payload of descriptor i is the splitmix64 stream     *
+ *    seeded with seed ^ g(i), written at buf + recs[i].in_off for recs[i].len     *
+ *    bytes, where g(i) = index[i] if `index` (device array of n uint64) is given, else base + i.     *
+ * ------------------------------------------------------------------------------------------ */
+int ptls_hip_fill_records(ptls_hip_batch_t *batch, void *buf, uint64_t seed, uint64_t index_base, const uint64_t *index,
+                          void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif

@@ -1,0 +1,162 @@
+"""ctypes bindings for the CPU checkers -- TEST INFRASTRUCTURE ONLY.
+
+* ``Oracle``  -> oracle/liboracle.so, the plain-C restatement (oracle/aesgcm_oracle.c).
+* ``Ref``     -> oracle/_ref/libptls_fusion_ref.so, the reference's own lib/fusion.c built unmodified
+                 by oracle/Makefile (absent on a box that never had /root/reference; tests that need it
+                 skip, the committed golden fixtures still pin parity).
+"""
+import ctypes
+import os
+import subprocess
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ORACLE_SO = os.path.join(ROOT, "oracle", "liboracle.so")
+REF_SO = os.path.join(ROOT, "oracle", "_ref", "libptls_fusion_ref.so")
+SIZE_MAX = (1 << 64) - 1
+
+_c = ctypes
+_u8p = _c.c_void_p
+
+
+def _buf(b):
+    return _c.create_string_buffer(bytes(b), max(len(b), 1))
+
+
+def build_oracle():
+    if not os.path.exists(ORACLE_SO):
+        subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "oracle")])
+
+
+class Oracle:
+    def __init__(self):
+        build_oracle()
+        L = self.lib = _c.CDLL(ORACLE_SO)
+        L.oracle_aes_expand.restype = _c.c_int
+        L.oracle_aes_expand.argtypes = [_u8p, _c.c_size_t, _u8p]
+        L.oracle_aes_ecb.argtypes = [_u8p, _c.c_size_t, _u8p, _u8p]
+        L.oracle_gf128_mul.argtypes = [_u8p, _u8p, _u8p]
+        L.oracle_ghash.argtypes = [_u8p, _u8p, _c.c_size_t, _u8p, _c.c_size_t, _u8p]
+        L.oracle_build_iv.argtypes = [_u8p, _c.c_uint64, _u8p]
+        for f in (L.oracle_aesgcm_seal, L.oracle_aesgcm_open):
+            f.restype = _c.c_size_t
+            f.argtypes = [_u8p, _c.c_size_t, _u8p, _c.c_uint64, _u8p, _c.c_size_t, _u8p, _c.c_size_t, _u8p]
+        L.oracle_fusion_domain_ghash.argtypes = [_u8p, _u8p, _c.c_size_t, _u8p]
+        L.oracle_splitmix64_at.restype = _c.c_uint64
+        L.oracle_splitmix64_at.argtypes = [_c.c_uint64, _c.c_uint64]
+        L.oracle_stream_bytes.argtypes = [_c.c_uint64, _u8p, _c.c_size_t]
+        L.oracle_gen_key.argtypes = [_c.c_uint64, _c.c_size_t, _u8p, _u8p]
+        L.oracle_gen_record.argtypes = [_c.c_uint64, _u8p, _c.c_size_t]
+        L.oracle_gen_quic_aad.argtypes = [_c.c_uint64, _u8p]
+        L.oracle_mixed_len.restype = _c.c_uint32
+        L.oracle_mixed_len.argtypes = [_c.c_uint64]
+        L.oracle_bench_seal.restype = _c.c_double
+        L.oracle_bench_seal.argtypes = [_c.c_size_t, _c.c_size_t, _c.c_size_t, _c.c_int]
+
+    def aes_ecb(self, key, block):
+        out = _c.create_string_buffer(16)
+        self.lib.oracle_aes_ecb(_buf(key), len(key), _buf(block), out)
+        return out.raw
+
+    def gf128_mul(self, x, y):
+        out = _c.create_string_buffer(16)
+        self.lib.oracle_gf128_mul(_buf(x), _buf(y), out)
+        return out.raw
+
+    def ghash(self, H, aad, ct):
+        out = _c.create_string_buffer(16)
+        self.lib.oracle_ghash(_buf(H), _buf(aad), len(aad), _buf(ct), len(ct), out)
+        return out.raw
+
+    def seal(self, key, iv, seq, aad, pt):
+        out = _c.create_string_buffer(len(pt) + 16)
+        n = self.lib.oracle_aesgcm_seal(_buf(key), len(key), _buf(iv), seq, _buf(aad), len(aad), _buf(pt), len(pt), out)
+        assert n == len(pt) + 16
+        return out.raw
+
+    def open(self, key, iv, seq, aad, ct):
+        out = _c.create_string_buffer(max(len(ct), 16))
+        n = self.lib.oracle_aesgcm_open(_buf(key), len(key), _buf(iv), seq, _buf(aad), len(aad), _buf(ct), len(ct), out)
+        return (None if n == SIZE_MAX else n), out.raw[: max(len(ct) - 16, 0)]
+
+    def fusion_domain_ghash(self, Hf, blocks):
+        out = _c.create_string_buffer(16)
+        self.lib.oracle_fusion_domain_ghash(_buf(Hf), _buf(blocks), len(blocks) // 16, out)
+        return out.raw
+
+    def stream(self, seed, n):
+        out = _c.create_string_buffer(max(n, 1))
+        self.lib.oracle_stream_bytes(seed, out, n)
+        return out.raw[:n]
+
+    def gen_key(self, j, key_len):
+        key = _c.create_string_buffer(32)
+        iv = _c.create_string_buffer(12)
+        self.lib.oracle_gen_key(j, key_len, key, iv)
+        return key.raw[:key_len], iv.raw
+
+    def gen_record(self, i, n):
+        out = _c.create_string_buffer(max(n, 1))
+        self.lib.oracle_gen_record(i, out, n)
+        return out.raw[:n]
+
+    def gen_quic_aad(self, i):
+        out = _c.create_string_buffer(13)
+        self.lib.oracle_gen_quic_aad(i, out)
+        return out.raw
+
+    def mixed_len(self, i):
+        return self.lib.oracle_mixed_len(i)
+
+
+def tls_aad(payload_len):
+    reclen = payload_len + 16
+    return bytes([0x17, 0x03, 0x03, (reclen >> 8) & 0xFF, reclen & 0xFF])
+
+
+class Ref:
+    """The reference engine (lib/fusion.c) reached through picotls's public AEAD API."""
+
+    available = os.path.exists(REF_SO)
+
+    def __init__(self):
+        L = self.lib = _c.CDLL(REF_SO)
+        for name in ("ref_seal", "ref_open"):
+            f = getattr(L, name)
+            f.restype = _c.c_size_t
+            f.argtypes = [_c.c_int, _u8p, _u8p, _c.c_uint64, _u8p, _c.c_size_t, _u8p, _c.c_size_t, _u8p]
+        L.ref_seal_supp.restype = _c.c_size_t
+        L.ref_seal_supp.argtypes = [_c.c_int, _u8p, _u8p, _c.c_uint64, _u8p, _c.c_size_t, _u8p, _c.c_size_t, _u8p,
+                                    _u8p, _c.c_size_t, _u8p]
+        L.ref_seal_iv96.restype = _c.c_size_t
+        L.ref_seal_iv96.argtypes = [_c.c_int, _u8p, _u8p, _u8p, _c.c_size_t, _c.c_uint64, _u8p, _c.c_size_t, _u8p,
+                                    _c.c_size_t, _u8p]
+        L.ref_bench.restype = _c.c_double
+        L.ref_bench.argtypes = [_c.c_int, _c.c_int, _u8p, _u8p, _u8p, _u8p, _c.c_size_t, _c.c_size_t, _c.c_size_t,
+                                _u8p, _c.c_size_t, _c.c_int, _c.c_void_p]
+        L.ref_fusion_supported.restype = _c.c_int
+        L.ref_fusion_can_aesni256.restype = _c.c_int
+        self.supported = bool(L.ref_fusion_supported())
+
+    def seal(self, key, iv, seq, aad, pt):
+        out = _c.create_string_buffer(len(pt) + 16)
+        n = self.lib.ref_seal(len(key) * 8, _buf(key), _buf(iv), seq, _buf(aad), len(aad), _buf(pt), len(pt), out)
+        assert n == len(pt) + 16
+        return out.raw
+
+    def seal_supp(self, key, iv, seq, aad, pt, hp_key, supp_off):
+        out = _c.create_string_buffer(len(pt) + 16)
+        supp = _c.create_string_buffer(16)
+        self.lib.ref_seal_supp(len(key) * 8, _buf(key), _buf(iv), seq, _buf(aad), len(aad), _buf(pt), len(pt), out,
+                               _buf(hp_key), supp_off, supp)
+        return out.raw, supp.raw
+
+    def seal_iv96(self, key, iv, xor_bytes, seq, aad, pt):
+        out = _c.create_string_buffer(len(pt) + 16)
+        self.lib.ref_seal_iv96(len(key) * 8, _buf(key), _buf(iv), _buf(xor_bytes), len(xor_bytes), seq, _buf(aad),
+                               len(aad), _buf(pt), len(pt), out)
+        return out.raw
+
+    def open(self, key, iv, seq, aad, ct):
+        out = _c.create_string_buffer(max(len(ct), 16))
+        n = self.lib.ref_open(len(key) * 8, _buf(key), _buf(iv), seq, _buf(aad), len(aad), _buf(ct), len(ct), out)
+        return (None if n == SIZE_MAX else n), out.raw[: max(len(ct) - 16, 0)]

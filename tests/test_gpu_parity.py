@@ -1,0 +1,283 @@
+"""Parity of the MI355X kernels (through the C ABI of libptls_hip.so) with the reference engine.
+
+Pins: tests/golden/*.json were produced by running lib/fusion.c itself (tests/golden/make_golden.py);
+the CPU oracle (oracle/) is used as a checker for data the fixtures do not cover.  Bar: bit-exact.
+Shapes follow the reference's own tests (t/fusion.c): KATs, length sweep incl. partial blocks and
+empty AAD/payload, iv96, tamper -> SIZE_MAX, differential runs, plus the batch-only cases (mixed
+keys / lengths in one launch, lanes-per-record variants, unaligned and in-place layouts).
+"""
+import hashlib
+import os
+import sys
+
+import numpy as np
+import pytest
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(HERE, "golden"))
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+import ptls_hip  # noqa: E402
+from hip_helpers import HostBatch  # noqa: E402
+from make_golden import CONFIGS, config_record, sweep_inputs  # noqa: E402
+from oracle_lib import tls_aad  # noqa: E402
+
+UINT64_MAX = (1 << 64) - 1
+LANES = (1, 2, 4, 8)
+
+
+def kat_records(golden):
+    k = golden["kats"]
+    recs, outs = [], []
+    for v in k["aead"]:
+        recs.append((bytes.fromhex(v["key"]), bytes.fromhex(v["iv"]), v["seq"], bytes.fromhex(v["aad"]),
+                     bytes.fromhex(v["pt"])))
+        outs.append(bytes.fromhex(v["out"]))
+    return recs, outs
+
+
+@pytest.mark.parametrize("lanes", LANES)
+def test_gcm_basic_and_capacity_kats(engine, golden, lanes):
+    """t/fusion.c gcm_basic (:235-274) and gcm_capacity (:276-287)"""
+    recs, outs = kat_records(golden)
+    hb = HostBatch(engine, recs)
+    assert hb.seal(lanes) == outs
+    res, pts = hb.open(outs, lanes)
+    assert res == [len(r[4]) for r in recs] and pts == [r[4] for r in recs]
+    hb.close()
+
+
+@pytest.mark.parametrize("lanes", LANES)
+def test_gcm_test_vectors(engine, golden, lanes):
+    """t/fusion.c gcm_test_vectors (:289-343): key 0, iv 0, all-zero AAD/payload, 19 (aadlen, ptlen)"""
+    tv = golden["kats"]["gcm_test_vectors"]
+    recs = [(bytes(16), bytes(12), 0, bytes(v["aadlen"]), bytes(v["ptlen"])) for v in tv]
+    hb = HostBatch(engine, recs)
+    outs = hb.seal(lanes)
+    for v, o in zip(tv, outs):
+        assert o[v["ptlen"]:].hex() == v["tag"], v
+    res, pts = hb.open(outs, lanes)
+    assert res == [v["ptlen"] for v in tv]
+    assert all(p == bytes(len(p)) for p in pts)
+    hb.close()
+
+
+def test_tamper_returns_size_max_and_writes_plaintext(engine, golden):
+    """aead_do_decrypt returns SIZE_MAX on a bad tag (lib/fusion.c:1162-1164) but the plaintext has
+    already been written (decrypt-then-verify, :822-840); t/picotls.c test_ciphersuite flips a bit."""
+    recs, outs = kat_records(golden)
+    hb = HostBatch(engine, recs)
+    bad = []
+    for o in outs:
+        b = bytearray(o)
+        b[len(b) // 2] ^= 0x01
+        bad.append(bytes(b))
+    res, pts = hb.open(bad)
+    assert res == [UINT64_MAX] * len(recs)
+    # every byte except the flipped one decrypts correctly (CTR), as fusion would leave it
+    for (key, iv, seq, aad, pt), p, o in zip(recs, pts, outs):
+        flip = len(o) // 2
+        exp = bytearray(pt)
+        if flip < len(pt):
+            exp[flip] ^= 0x01
+        assert p == bytes(exp)
+    hb.close()
+
+
+def test_iv96_xor_iv(engine, golden):
+    """t/fusion.c gcm_iv96 (:345-379) through the keyset's xor_iv (ptls_aead_xor_iv semantics)"""
+    k = golden["kats"]
+    v = k["gcm_iv96"]
+    basic2 = k["aead"][1]
+    key, iv = bytes.fromhex(v["key"]), bytes.fromhex(v["iv"])
+    pt, aad = bytes.fromhex(basic2["pt"]), bytes.fromhex(basic2["aad"])
+    hb = HostBatch(engine, [(key, iv, 0, aad, pt)])
+    hb.keyset.xor_iv(0, bytes.fromhex(v["xor"]))
+    assert hb.keyset.get_iv(0) == bytes.fromhex(basic2["iv"])
+    out = hb.seal()
+    assert out[0].hex() == basic2["out"]
+    hb.keyset.xor_iv(0, bytes.fromhex(v["xor"]))
+    hb.keyset.xor_iv(0, bytes.fromhex(v["bad_xor"]))
+    res, _ = hb.open(out)
+    assert res == [UINT64_MAX]
+    hb.keyset.xor_iv(0, bytes.fromhex(v["bad_xor"]))
+    hb.keyset.xor_iv(0, bytes.fromhex(v["xor"]))
+    res, pts = hb.open(out)
+    assert res == [len(pt)] and pts == [pt]
+    hb.close()
+
+
+@pytest.mark.parametrize("key_len", [16, 32])
+@pytest.mark.parametrize("lanes", (0,) + LANES)
+def test_length_sweep(engine, oracle, golden, key_len, lanes):
+    """L in {0..97, 1328..1339, 1350, 4095..4097, 16383, 16384} x AAD {0,5,13,20,32};
+    each record its own key slot, all in ONE launch; compared with lib/fusion.c output digests."""
+    vecs = [v for v in golden["sweep"]["vectors"] if v["key_len"] == key_len]
+    recs = [sweep_inputs(oracle, v["idx"], key_len, v["L"], v["A"]) for v in vecs]
+    hb = HostBatch(engine, recs)
+    outs = hb.seal(lanes)
+    bad = [v["idx"] for v, o in zip(vecs, outs) if hashlib.sha256(o).hexdigest() != v["sha256"]]
+    assert not bad, f"{len(bad)} mismatching vectors, first idx {bad[:8]}"
+    res, pts = hb.open(outs, lanes)
+    assert res == [v["L"] for v in vecs]
+    assert pts == [r[4] for r in recs]
+    hb.close()
+
+
+@pytest.mark.parametrize("name", list(CONFIGS))
+def test_baseline_config_samples(engine, oracle, golden, name):
+    """first/last 64 records (+ shard seams) of every BASELINE config"""
+    cfg = golden["configs"]["configs"][name]
+    recs = [config_record(oracle, CONFIGS[name], r["i"]) for r in cfg["records"]]
+    recs_sorted = sorted(range(len(recs)), key=lambda j: recs[j][0])  # group same-key records
+    hb = HostBatch(engine, [recs[j] for j in recs_sorted])
+    outs = hb.seal()
+    for j, o in zip(recs_sorted, outs):
+        assert hashlib.sha256(o).hexdigest() == cfg["records"][j]["sha256"], (name, cfg["records"][j]["i"])
+    hb.close()
+
+
+@pytest.mark.parametrize("align", [1, 4])
+def test_unaligned_layout(engine, oracle, align):
+    """records packed at 1- and 4-byte granularity take the byte-granular path; must stay exact"""
+    rng = np.random.default_rng(7)
+    recs = []
+    for i in range(300):
+        L = int(rng.integers(0, 1500))
+        A = int(rng.integers(0, 40))
+        key, iv = oracle.gen_key(i % 3, 16)
+        recs.append((key, iv, i, oracle.stream(1000 + i, A), oracle.stream(5000 + i, L)))
+    recs.sort(key=lambda r: r[0])
+    hb = HostBatch(engine, recs, align=align)
+    outs = hb.seal()
+    for r, o in zip(recs, outs):
+        assert o == oracle.seal(*r)
+    res, pts = hb.open(outs)
+    assert res == [len(r[4]) for r in recs] and pts == [r[4] for r in recs]
+    hb.close()
+
+
+def test_in_place_seal(engine, oracle):
+    """output == input is allowed (fusion, SURVEY.md §7 hard parts)"""
+    recs = []
+    for i in range(64):
+        key, iv = oracle.gen_key(0, 32)
+        recs.append((key, iv, i, tls_aad(100 + 37 * i), oracle.gen_record(i, 100 + 37 * i)))
+    hb = HostBatch(engine, recs)
+    outs = hb.seal(in_place=True)
+    for r, o in zip(recs, outs):
+        assert o == oracle.seal(*r)
+    hb.close()
+
+
+def test_differential_random(engine, oracle):
+    """t/fusion.c test_generated (:384-465) in batch form: random keys/ivs/seq/aad/text < 256 B,
+    both key sizes, compared with the CPU oracle; then opened back."""
+    rng = np.random.default_rng(12345)
+    for key_len in (16, 32):
+        recs = []
+        for i in range(2000):
+            key = rng.integers(0, 256, key_len, dtype=np.uint8).tobytes()
+            iv = rng.integers(0, 256, 12, dtype=np.uint8).tobytes()
+            seq = int(rng.integers(0, 2 ** 63))
+            aad = rng.integers(0, 256, int(rng.integers(0, 256)), dtype=np.uint8).tobytes()
+            pt = rng.integers(0, 256, int(rng.integers(0, 256)), dtype=np.uint8).tobytes()
+            recs.append((key, iv, seq, aad, pt))
+        hb = HostBatch(engine, recs)
+        outs = hb.seal()
+        for r, o in zip(recs, outs):
+            assert o == oracle.seal(*r)
+        res, pts = hb.open(outs)
+        assert res == [len(r[4]) for r in recs] and pts == [r[4] for r in recs]
+        hb.close()
+
+
+def test_full_size_roundtrip_16k(engine, oracle):
+    """64K x 16 KiB (1 GiB) synthetic records filled on the GPU: seal -> open must return every
+    record with its length and the original bytes (size-independent property), and sampled records
+    must equal the oracle's seal of the generator's bytes."""
+    n, L = 1 << 16, 16384
+    key, iv = oracle.gen_key(0, 16)
+    recs, in_total, out_total, _ = ptls_hip.layout_records([L] * n, [5] * n, [0] * n, np.arange(n))
+    aad = np.tile(np.frombuffer(tls_aad(L), np.uint8), (n, 1))
+    aad = np.concatenate([aad, np.zeros((n, 11), np.uint8)], axis=1).reshape(-1)  # 16-B aligned AAD slots
+    recs["aad_off"] = np.arange(n, dtype=np.uint64) * 16
+    ks = ptls_hip.KeySet(engine, 16, 1)
+    ks.set(0, key, iv)
+    b = ptls_hip.Batch(engine, recs)
+    d_in = torch.empty(in_total, dtype=torch.uint8, device="cuda")
+    d_aad = torch.from_numpy(aad).cuda()
+    d_ct = torch.empty(out_total, dtype=torch.uint8, device="cuda")
+    d_pt = torch.empty(in_total, dtype=torch.uint8, device="cuda")
+    d_res = torch.zeros(n, dtype=torch.int64, device="cuda")
+    b.fill(d_in, 0x70746C7300000001)
+    b.seal(ks, d_in, d_aad, d_ct)
+    # open reads ct||tag at in_off = out_off of the seal
+    recs_o = recs.copy()
+    recs_o["in_off"] = recs["out_off"]
+    recs_o["out_off"] = recs["in_off"]
+    bo = ptls_hip.Batch(engine, recs_o)
+    bo.open(ks, d_ct, d_aad, d_pt, d_res)
+    torch.cuda.synchronize()
+    assert bool((d_res == L).all())
+    assert torch.equal(d_pt, d_in)
+    ct = d_ct.cpu().numpy()
+    for i in (0, 1, 777, n // 2, n - 1):
+        pt = oracle.gen_record(i, L)
+        assert d_in[recs["in_off"][i]: recs["in_off"][i] + L].cpu().numpy().tobytes() == pt
+        exp = oracle.seal(key, iv, i, tls_aad(L), pt)
+        assert ct[recs["out_off"][i]: recs["out_off"][i] + L + 16].tobytes() == exp
+    for o in (b, bo, ks):
+        o.close()
+
+
+def test_plugin_through_reference_picotls(engine, oracle, golden):
+    """Drop-in: the reference's own ptls_aead_new_direct / ptls_aead_xor_iv (oracle/_ref, i.e.
+    lib/picotls.c) instantiate ptls_hip_aes128gcm / aes256gcm and drive them through the vtable,
+    as picotls applications do; outputs compared with lib/fusion.c in the same process."""
+    from oracle_lib import Ref
+    if not Ref.available:
+        pytest.skip("oracle/_ref not built")
+    import plugin_driver
+    drv = plugin_driver.PluginDriver()
+    k = golden["kats"]
+    basic2 = k["aead"][1]
+    key, iv = bytes.fromhex(basic2["key"]), bytes.fromhex(basic2["iv"])
+    pt, aad = bytes.fromhex(basic2["pt"]), bytes.fromhex(basic2["aad"])
+    ctx = drv.new(128, key, iv)
+    assert drv.encrypt(ctx, pt, 0, aad).hex() == basic2["out"]
+    assert drv.decrypt(ctx, bytes.fromhex(basic2["out"]), 0, aad) == pt
+    bad = bytearray.fromhex(basic2["out"])
+    bad[3] ^= 1
+    assert drv.decrypt(ctx, bytes(bad), 0, aad) is None
+    assert drv.decrypt(ctx, b"short", 0, aad) is None  # inlen < 16 -> SIZE_MAX
+    drv.free(ctx)
+    # gcm_iv96 through the reference's ptls_aead_xor_iv
+    v = k["gcm_iv96"]
+    ctx = drv.new(128, key, bytes.fromhex(v["iv"]))
+    drv.xor_iv(ctx, bytes.fromhex(v["xor"]))
+    assert drv.encrypt(ctx, pt, 0, aad).hex() == basic2["out"]
+    drv.free(ctx)
+    # encrypt_v with three iovecs (what ptls_send uses, lib/picotls.c:705-715)
+    ctx = drv.new(256, bytes(range(32)), bytes(12))
+    out_v = drv.encrypt_v(ctx, [pt[:10], pt[10:50], pt[50:]], 7, aad)
+    assert out_v == oracle.seal(bytes(range(32)), bytes(12), 7, aad, pt)
+    drv.free(ctx)
+    # test_generated-style differential vs lib/fusion.c, both directions
+    ref = Ref()
+    rng = np.random.default_rng(99)
+    for bits in (128, 256):
+        for i in range(40):
+            key = rng.integers(0, 256, bits // 8, dtype=np.uint8).tobytes()
+            iv = rng.integers(0, 256, 12, dtype=np.uint8).tobytes()
+            seq = int(rng.integers(0, 2 ** 62))
+            aad = rng.integers(0, 256, int(rng.integers(0, 64)), dtype=np.uint8).tobytes()
+            text = rng.integers(0, 256, int(rng.integers(0, 3000)), dtype=np.uint8).tobytes()
+            ctx = drv.new(bits, key, iv)
+            sealed = drv.encrypt(ctx, text, seq, aad)
+            assert sealed == ref.seal(key, iv, seq, aad, text)
+            assert ref.open(key, iv, seq, aad, sealed) == (len(text), text)
+            assert drv.decrypt(ctx, ref.seal(key, iv, seq + 1, aad, text), seq + 1, aad) == text
+            drv.free(ctx)
