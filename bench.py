@@ -174,6 +174,17 @@ def cpu_baseline(cfg_name, cfg, budget_s=4.0):
                        f"ptls_aead_encrypt/decrypt, {best['reps']} passes, {threads} pinned threads")
 
 
+def max_over_ranks(x, world, device):
+    """the slowest rank's time: the whole job is done only when every shard is"""
+    if world == 1:
+        return x
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor([x], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
 def golden_check(cfg_name, idx, recs, d_ct):
     """compare sampled sealed records with the digests lib/fusion.c produced (tests/golden/configs.json)"""
     name = {"c2": "c2_tls16k_aes128", "c3": "c3_quic1350_aes128", "c4": "c4_mixed_aes256_64k",
@@ -274,11 +285,7 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = max_over_ranks(time.perf_counter() - t0, world, "cuda")
 
     # per-kernel timing (HIP events on the launch stream), outside the timed region
     ktimes = []

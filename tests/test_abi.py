@@ -1,0 +1,108 @@
+"""CPU tests of the drop-in boundary: the C-ABI library loads, exports every symbol include/ptls_hip.h
+declares, its plugin structs are layout-identical to picotls's, and it fails loudly without a GPU."""
+import ctypes
+import os
+import re
+import shutil
+import subprocess
+
+import pytest
+
+import ptls_hip
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "ptls_hip.h")
+REF_INCLUDE = "/root/reference/include"
+
+
+def declared_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(ptls_hip_[a-z0-9_]+)\s*\(", src)))
+
+
+def declared_data():
+    src = open(HEADER).read()
+    m = re.findall(r"extern\s+ptls_aead_algorithm_t\s+([^;]+);", src)
+    return sorted(n.strip() for decl in m for n in decl.split(","))
+
+
+def test_library_exports_every_declared_symbol():
+    L = ptls_hip.lib()
+    funcs = declared_functions()
+    assert len(funcs) >= 20
+    for name in funcs:
+        assert hasattr(L, name), name
+    for name in declared_data():
+        assert ctypes.c_char.in_dll(L, name) is not None, name
+    # the Python binding covers exactly what the header declares
+    assert sorted(ptls_hip.SIGNATURES) == funcs
+    assert sorted(ptls_hip.DATA_SYMBOLS) == declared_data()
+
+
+def test_record_descriptor_layout():
+    assert ptls_hip.RECORD_DTYPE.itemsize == 48
+    assert [ptls_hip.RECORD_DTYPE.fields[f][1] for f in ("in_off", "out_off", "aad_off", "seq", "len", "aad_len", "key",
+                                                          "flags")] == [0, 8, 16, 24, 32, 36, 40, 44]
+
+
+def _layout(tmp_path, extra):
+    exe = tmp_path / ("abi" + str(len(extra)))
+    subprocess.check_call(["gcc", "-std=gnu99", "-w", "-include", "string.h", *extra, "-I", os.path.join(ROOT, "include"),
+                           os.path.join(ROOT, "tests", "abi_layout.c"), "-o", str(exe)])
+    return subprocess.check_output([str(exe)]).decode()
+
+
+@pytest.mark.skipif(shutil.which("gcc") is None, reason="gcc missing")
+def test_plugin_structs_match_picotls_abi(tmp_path):
+    ours = _layout(tmp_path, [])
+    assert "ptls_aead_context_t size 80" in ours and "ptls_hip_record_t size 48" in ours
+    if not os.path.exists(os.path.join(REF_INCLUDE, "picotls.h")):
+        pytest.skip("reference picotls.h not present (GPU box)")
+    theirs = _layout(tmp_path, ["-I", REF_INCLUDE, "-include", "picotls.h"])
+    assert ours == theirs
+
+
+def test_algorithm_objects_mirror_fusion():
+    """field values of ptls_hip_aes{128,256}gcm vs ptls_fusion_aes{128,256}gcm (lib/fusion.c:1231-1256)"""
+    L = ptls_hip.lib()
+
+    class Algo(ctypes.Structure):  # include/picotls.h:499-560 (layout checked above)
+        _fields_ = [("name", ctypes.c_char_p), ("conf", ctypes.c_uint64), ("integ", ctypes.c_uint64),
+                    ("ctr", ctypes.c_void_p), ("ecb", ctypes.c_void_p), ("key_size", ctypes.c_size_t),
+                    ("iv_size", ctypes.c_size_t), ("tag_size", ctypes.c_size_t), ("fixed_iv", ctypes.c_size_t),
+                    ("record_iv", ctypes.c_size_t), ("bits", ctypes.c_uint8), ("align_bits", ctypes.c_uint8),
+                    ("context_size", ctypes.c_size_t), ("setup", ctypes.c_void_p)]
+
+    for name, ks, label in (("ptls_hip_aes128gcm", 16, b"AES128-GCM"), ("ptls_hip_aes256gcm", 32, b"AES256-GCM")):
+        a = Algo.in_dll(L, name)
+        assert a.name == label and a.key_size == ks and a.iv_size == 12 and a.tag_size == 16
+        assert a.conf == 0x2000000 and a.integ == 0x40000000000000
+        assert (a.fixed_iv, a.record_iv, a.bits & 1, a.align_bits) == (0, 0, 0, 0)
+        assert a.context_size >= 80 and a.setup
+
+
+def _gpu_present():
+    try:
+        import torch
+        return torch.cuda.device_count() > 0
+    except Exception:  # noqa: BLE001
+        return False
+
+
+@pytest.mark.skipif(_gpu_present(), reason="this checks the no-device error path")
+def test_fails_loudly_without_device():
+    """no CPU fallback: engine construction errors out, and picotls's own ptls_aead_new_direct returns NULL
+    for our algorithm (setup_crypto != 0, lib/picotls.c:6467-6470)"""
+    L = ptls_hip.lib()
+    assert not L.ptls_hip_engine_new(0)
+    assert "device" in ptls_hip.last_error().lower()
+    with pytest.raises(ptls_hip.HipError):
+        ptls_hip.Engine(0)
+    from oracle_lib import REF_SO, Ref
+    if Ref.available:
+        ref = ctypes.CDLL(REF_SO)
+        ref.ptls_aead_new_direct.restype = ctypes.c_void_p
+        ref.ptls_aead_new_direct.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
+        algo = ctypes.addressof(ctypes.c_char.in_dll(L, "ptls_hip_aes128gcm"))
+        assert not ref.ptls_aead_new_direct(algo, 1, bytes(16), bytes(12))

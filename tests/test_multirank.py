@@ -1,0 +1,69 @@
+"""world_size-2 gloo test of bench.py's multi-GPU logic on CPU: record shards are disjoint and cover the
+job, keys/seq stay globally consistent, and the reported time is the max over ranks."""
+import os
+import socket
+import sys
+
+import numpy as np
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _worker(rank, world, port, cfg, q):
+    import torch
+    import torch.distributed as dist
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "hsig-picotls_amd"))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import bench
+    idx, recs, in_total, out_total, lens = bench.make_workload(cfg, rank)
+    t = bench.max_over_ranks(1.0 + rank, world, "cpu")
+    q.put((rank, idx.copy(), recs["key"].copy(), recs["seq"].copy(), lens.copy(), t))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _run(cfg, world=2):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, cfg, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = sorted(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    return out
+
+
+def test_single_key_shards():
+    cfg = dict(n=4096, L=1350, key_len=16, keys=1, aad="quic")
+    out = _run(cfg)
+    all_idx = np.concatenate([o[1] for o in out])
+    assert np.array_equal(np.sort(all_idx), np.arange(2 * 4096, dtype=np.uint64))  # disjoint, complete
+    for rank, idx, key, seq, lens, t in out:
+        assert np.array_equal(idx, np.arange(rank * 4096, (rank + 1) * 4096, dtype=np.uint64))
+        assert np.array_equal(seq, idx) and not key.any()
+        assert t == 2.0  # max over ranks (1.0, 2.0)
+
+
+def test_multi_key_shards_key_major():
+    K = 64
+    cfg = dict(n=K * 8, L=None, key_len=32, keys=K, aad="tls")
+    out = _run(cfg)
+    all_idx = np.concatenate([o[1] for o in out])
+    assert np.array_equal(np.sort(all_idx), np.arange(2 * K * 8, dtype=np.uint64))
+    for rank, idx, key, seq, lens, t in out:
+        assert np.array_equal(key, (idx % K).astype(np.uint32))  # record i uses key i mod K
+        assert np.array_equal(seq, idx // K)                       # per-key sequence number
+        assert np.all(np.diff(key.astype(np.int64)) >= 0)          # same-key records adjacent
+        assert lens.min() >= 64 and lens.max() <= 16384
