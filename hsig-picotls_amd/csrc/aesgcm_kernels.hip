@@ -26,8 +26,8 @@
 namespace ptls_hip {
 
 /* ---------------- LDS map (bytes) ---------------- */
-constexpr uint32_t LDS_AES = 0;              /* 64 KiB: row v = [T0 x32 lane slots | T2 x32 lane slots]  */
-constexpr uint32_t LDS_GMAIN = 65536;        /* 64 KiB: row v (256 B) = 16 positions x 16 B, P = H^G       */
+constexpr uint32_t LDS_GMAIN = 0;            /* 64 KiB: row v (256 B) = 16 positions x 16 B, P = H^G       */
+constexpr uint32_t LDS_AES = 65536;          /* 64 KiB: row v = [T0 x32 lane slots | T2 x32 lane slots]  */
 constexpr uint32_t LDS_GTREE = 131072;       /* 3 x 8 KiB nibble tables for H^1, H^2, H^4: [p(32)][v(16)] */
 constexpr uint32_t LDS_TREE_STRIDE = 8192;
 constexpr uint32_t LDS_BYTES = LDS_GTREE + 3 * LDS_TREE_STRIDE; /* 152 KiB of the CU's 160 KiB */
@@ -39,6 +39,16 @@ struct V4 {
 __device__ __forceinline__ V4 v4xor(V4 a, V4 b)
 {
     return V4{a.w0 ^ b.w0, a.w1 ^ b.w1, a.w2 ^ b.w2, a.w3 ^ b.w3};
+}
+
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c)
+{
+    return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96); /* v_bitop3_b32: a ^ b ^ c in one VALU op */
+}
+
+__device__ __forceinline__ V4 v4xor3(V4 a, V4 b, V4 c)
+{
+    return V4{xor3(a.w0, b.w0, c.w0), xor3(a.w1, b.w1, c.w1), xor3(a.w2, b.w2, c.w2), xor3(a.w3, b.w3, c.w3)};
 }
 
 __device__ __forceinline__ uint32_t bswap32(uint32_t x)
@@ -66,12 +76,14 @@ __device__ __forceinline__ void lds128_store(uint8_t *lds, uint32_t addr, V4 v)
  *  AES (FIPS-197) with replicated T-tables in LDS                                          *
  * ======================================================================================= */
 
-/* LDS byte address of T0[byte k of x] for this lane: (x.byte[k] << 8) | lane_slot.
- * v_perm_b32: result byte0 <- lb.byte0 (selector 0), byte1 <- x.byte[k] (selector 4+k), rest 0. */
+/* LDS byte address of T0[byte k of x] for this lane: LDS_AES | (x.byte[k] << 8) | lane_slot, from ONE
+ * v_perm_b32: byte0 <- lb.byte0 (selector 0), byte1 <- x.byte[k] (selector 4+k), byte2 <- lb.byte2 (= 1,
+ * i.e. the 64 KiB table base, selector 2), byte3 <- 0.  lb = (lane & 31) * 4 | LDS_AES. */
 template <int K>
 __device__ __forceinline__ uint32_t aes_addr(uint32_t x, uint32_t lb)
 {
-    return __builtin_amdgcn_perm(x, lb, 0x0c0c0000u | ((4u + K) << 8));
+    static_assert(LDS_AES == 65536, "the table base is injected as byte 2 of the address");
+    return __builtin_amdgcn_perm(x, lb, 0x0c020000u | ((4u + K) << 8));
 }
 
 __device__ __forceinline__ uint32_t rotl8(uint32_t x)
@@ -84,24 +96,24 @@ __device__ __forceinline__ uint32_t rotl8(uint32_t x)
 __device__ __forceinline__ uint32_t aes_col(const uint8_t *lds, uint32_t lb, uint32_t x0, uint32_t x1, uint32_t x2, uint32_t x3,
                                             uint32_t k)
 {
-    const uint32_t a0 = lds32(lds, LDS_AES + aes_addr<0>(x0, lb));
-    const uint32_t a1 = lds32(lds, LDS_AES + aes_addr<1>(x1, lb));
-    const uint32_t a2 = lds32(lds, LDS_AES + 128 + aes_addr<2>(x2, lb));
-    const uint32_t a3 = lds32(lds, LDS_AES + 128 + aes_addr<3>(x3, lb));
-    return a0 ^ a2 ^ k ^ rotl8(a1 ^ a3);
+    const uint32_t a0 = lds32(lds, aes_addr<0>(x0, lb));
+    const uint32_t a1 = lds32(lds, aes_addr<1>(x1, lb));
+    const uint32_t a2 = lds32(lds, 128 + aes_addr<2>(x2, lb));
+    const uint32_t a3 = lds32(lds, 128 + aes_addr<3>(x3, lb));
+    return xor3(a0, a2, rotl8(a1 ^ a3)) ^ k;
 }
 
 /* final round column: S-box bytes picked out of T2[.].b0, T0[.].b1, T0[.].b2, T2[.].b3 */
 __device__ __forceinline__ uint32_t aes_col_last(const uint8_t *lds, uint32_t lb, uint32_t x0, uint32_t x1, uint32_t x2,
                                                  uint32_t x3, uint32_t k)
 {
-    const uint32_t u0 = lds32(lds, LDS_AES + 128 + aes_addr<0>(x0, lb));
-    const uint32_t u1 = lds32(lds, LDS_AES + aes_addr<1>(x1, lb));
-    const uint32_t u2 = lds32(lds, LDS_AES + aes_addr<2>(x2, lb));
-    const uint32_t u3 = lds32(lds, LDS_AES + 128 + aes_addr<3>(x3, lb));
+    const uint32_t u0 = lds32(lds, 128 + aes_addr<0>(x0, lb));
+    const uint32_t u1 = lds32(lds, aes_addr<1>(x1, lb));
+    const uint32_t u2 = lds32(lds, aes_addr<2>(x2, lb));
+    const uint32_t u3 = lds32(lds, 128 + aes_addr<3>(x3, lb));
     const uint32_t lo = __builtin_amdgcn_perm(u1, u0, 0x0c0c0500u); /* u0.b0 -> b0, u1.b1 -> b1 */
     const uint32_t hi = __builtin_amdgcn_perm(u3, u2, 0x07020c0cu); /* u2.b2 -> b2, u3.b3 -> b3 */
-    return (lo | hi) ^ k;
+    return xor3(lo, hi, k); /* lo and hi occupy disjoint bytes: lo ^ hi == lo | hi */
 }
 
 template <int ROUNDS>
@@ -124,6 +136,45 @@ __device__ __forceinline__ V4 aes_encrypt(const uint8_t *lds, uint32_t lb, const
     const uint32_t t2 = aes_col_last(lds, lb, s.w2, s.w3, s.w0, s.w1, rk[4 * ROUNDS + 2]);
     const uint32_t t3 = aes_col_last(lds, lb, s.w3, s.w0, s.w1, s.w2, rk[4 * ROUNDS + 3]);
     return V4{t0, t1, t2, t3};
+}
+
+/* two independent blocks, round-interleaved: twice the LDS requests in flight per wave */
+template <int ROUNDS>
+__device__ __forceinline__ void aes_encrypt2(const uint8_t *lds, uint32_t lb, const uint32_t *__restrict__ rk, V4 &s, V4 &u)
+{
+    s.w0 ^= rk[0];
+    s.w1 ^= rk[1];
+    s.w2 ^= rk[2];
+    s.w3 ^= rk[3];
+    u.w0 ^= rk[0];
+    u.w1 ^= rk[1];
+    u.w2 ^= rk[2];
+    u.w3 ^= rk[3];
+#pragma unroll
+    for (int r = 1; r < ROUNDS; ++r) {
+        const uint32_t k0 = rk[4 * r + 0], k1 = rk[4 * r + 1], k2 = rk[4 * r + 2], k3 = rk[4 * r + 3];
+        const uint32_t t0 = aes_col(lds, lb, s.w0, s.w1, s.w2, s.w3, k0);
+        const uint32_t v0 = aes_col(lds, lb, u.w0, u.w1, u.w2, u.w3, k0);
+        const uint32_t t1 = aes_col(lds, lb, s.w1, s.w2, s.w3, s.w0, k1);
+        const uint32_t v1 = aes_col(lds, lb, u.w1, u.w2, u.w3, u.w0, k1);
+        const uint32_t t2 = aes_col(lds, lb, s.w2, s.w3, s.w0, s.w1, k2);
+        const uint32_t v2 = aes_col(lds, lb, u.w2, u.w3, u.w0, u.w1, k2);
+        const uint32_t t3 = aes_col(lds, lb, s.w3, s.w0, s.w1, s.w2, k3);
+        const uint32_t v3 = aes_col(lds, lb, u.w3, u.w0, u.w1, u.w2, k3);
+        s = V4{t0, t1, t2, t3};
+        u = V4{v0, v1, v2, v3};
+    }
+    const uint32_t k0 = rk[4 * ROUNDS + 0], k1 = rk[4 * ROUNDS + 1], k2 = rk[4 * ROUNDS + 2], k3 = rk[4 * ROUNDS + 3];
+    const uint32_t t0 = aes_col_last(lds, lb, s.w0, s.w1, s.w2, s.w3, k0);
+    const uint32_t v0 = aes_col_last(lds, lb, u.w0, u.w1, u.w2, u.w3, k0);
+    const uint32_t t1 = aes_col_last(lds, lb, s.w1, s.w2, s.w3, s.w0, k1);
+    const uint32_t v1 = aes_col_last(lds, lb, u.w1, u.w2, u.w3, u.w0, k1);
+    const uint32_t t2 = aes_col_last(lds, lb, s.w2, s.w3, s.w0, s.w1, k2);
+    const uint32_t v2 = aes_col_last(lds, lb, u.w2, u.w3, u.w0, u.w1, k2);
+    const uint32_t t3 = aes_col_last(lds, lb, s.w3, s.w0, s.w1, s.w2, k3);
+    const uint32_t v3 = aes_col_last(lds, lb, u.w3, u.w0, u.w1, u.w2, k3);
+    s = V4{t0, t1, t2, t3};
+    u = V4{v0, v1, v2, v3};
 }
 
 /* ======================================================================================= *
@@ -176,23 +227,14 @@ __device__ __forceinline__ V4 gh_mul_main(const uint8_t *lds, const GhLane &g, V
     const uint32_t x1 = __builtin_amdgcn_alignbit(r2, r1, g.shift);
     const uint32_t x2 = __builtin_amdgcn_alignbit(r3, r2, g.shift);
     const uint32_t x3 = __builtin_amdgcn_alignbit(r0, r3, g.shift);
-    V4 acc = x;
-    acc = v4xor(acc, gh_term<0>(lds, x0, g.lb0));
-    acc = v4xor(acc, gh_term<1>(lds, x0, g.lb0));
-    acc = v4xor(acc, gh_term<2>(lds, x0, g.lb0));
-    acc = v4xor(acc, gh_term<3>(lds, x0, g.lb0));
-    acc = v4xor(acc, gh_term<4>(lds, x1, g.lb1));
-    acc = v4xor(acc, gh_term<5>(lds, x1, g.lb1));
-    acc = v4xor(acc, gh_term<6>(lds, x1, g.lb1));
-    acc = v4xor(acc, gh_term<7>(lds, x1, g.lb1));
-    acc = v4xor(acc, gh_term<8>(lds, x2, g.lb2));
-    acc = v4xor(acc, gh_term<9>(lds, x2, g.lb2));
-    acc = v4xor(acc, gh_term<10>(lds, x2, g.lb2));
-    acc = v4xor(acc, gh_term<11>(lds, x2, g.lb2));
-    acc = v4xor(acc, gh_term<12>(lds, x3, g.lb3));
-    acc = v4xor(acc, gh_term<13>(lds, x3, g.lb3));
-    acc = v4xor(acc, gh_term<14>(lds, x3, g.lb3));
-    acc = v4xor(acc, gh_term<15>(lds, x3, g.lb3));
+    V4 acc = v4xor3(x, gh_term<0>(lds, x0, g.lb0), gh_term<1>(lds, x0, g.lb0));
+    acc = v4xor3(acc, gh_term<2>(lds, x0, g.lb0), gh_term<3>(lds, x0, g.lb0));
+    acc = v4xor3(acc, gh_term<4>(lds, x1, g.lb1), gh_term<5>(lds, x1, g.lb1));
+    acc = v4xor3(acc, gh_term<6>(lds, x1, g.lb1), gh_term<7>(lds, x1, g.lb1));
+    acc = v4xor3(acc, gh_term<8>(lds, x2, g.lb2), gh_term<9>(lds, x2, g.lb2));
+    acc = v4xor3(acc, gh_term<10>(lds, x2, g.lb2), gh_term<11>(lds, x2, g.lb2));
+    acc = v4xor3(acc, gh_term<12>(lds, x3, g.lb3), gh_term<13>(lds, x3, g.lb3));
+    acc = v4xor3(acc, gh_term<14>(lds, x3, g.lb3), gh_term<15>(lds, x3, g.lb3));
     return acc;
 }
 
@@ -224,7 +266,7 @@ __device__ __forceinline__ V4 ld_basis(const uint32_t *b, int e)
 __device__ void build_aes_tables(uint8_t *lds, const uint32_t *__restrict__ t0)
 {
     for (int e = threadIdx.x; e < 256 * 32; e += WG_THREADS) {
-        const int v = e >> 5, s = e & 31;
+        const int v = e >> 5, s = e & 31; /* row v, lane slot s */
         const uint32_t t = t0[v];
         *reinterpret_cast<uint32_t *>(lds + LDS_AES + v * 256 + s * 4) = t;
         *reinterpret_cast<uint32_t *>(lds + LDS_AES + v * 256 + 128 + s * 4) = (t << 16) | (t >> 16);
@@ -315,8 +357,57 @@ __device__ __forceinline__ int wave_max(int v)
  *  batch seal / open                                                                       *
  * ======================================================================================= */
 
+/* one GHASH element of a lane: which of AAD / ciphertext / length block it is */
+struct Elem {
+    bool active, is_aad, is_c, is_len;
+    int i, c, nbytes;
+};
+
+__device__ __forceinline__ Elem elem_of(int i, int N, int na, int nc, int L)
+{
+    Elem e;
+    e.i = i;
+    e.active = i < N;
+    e.is_aad = i < na;
+    e.is_c = !e.is_aad && i < na + nc;
+    e.is_len = e.active && i == N - 1;
+    e.c = i - na;
+    e.nbytes = e.is_c ? min(16, L - 16 * e.c) : 0;
+    return e;
+}
+
+template <bool OPEN>
+__device__ __forceinline__ V4 finish_elem(const Elem &e, V4 in_blk, V4 ks, const uint8_t *aad_p, int A, uint8_t *out_p, bool fast,
+                                          V4 lenblk, V4 &ek0)
+{
+    V4 x = V4{0, 0, 0, 0};
+    if (e.is_aad) {
+        x = load_block(aad_p + 16 * e.i, min(16, A - 16 * e.i), fast);
+    } else if (e.is_c) {
+        const V4 o = v4xor(in_blk, ks);
+        if (OPEN) {
+            store_block(out_p + 16 * (size_t)e.c, e.nbytes, fast, o);
+            x = in_blk;
+        } else {
+            x = mask_block(o, e.nbytes);
+            store_block(out_p + 16 * (size_t)e.c, e.nbytes, fast, x);
+        }
+    } else if (e.is_len) {
+        x = lenblk;
+        ek0 = ks;
+    }
+    return x;
+}
+
+/* Pointers are separate __restrict__ kernel parameters (not a struct) so the compiler can prove that
+ * the key slots, tables and descriptors are never written by the kernel and read them through the
+ * scalar unit (s_load into SGPRs) instead of per-lane vector loads.  in/out may alias (in place). */
 template <int G, int ROUNDS, bool OPEN>
-__global__ void __launch_bounds__(WG_THREADS) aesgcm_batch_kernel(KernelArgs a, uint32_t base_aligned)
+__global__ void __launch_bounds__(WG_THREADS)
+    aesgcm_batch_kernel(const ptls_hip_record_t *__restrict__ recs, const Chunk *__restrict__ chunks, uint32_t nchunks,
+                        const uint8_t *in, const uint8_t *__restrict__ aad, uint8_t *out, uint64_t *__restrict__ result,
+                        const KeySlot *__restrict__ slots, const uint32_t *__restrict__ basis, const uint32_t *__restrict__ t0,
+                        uint32_t base_aligned)
 {
     __shared__ __attribute__((aligned(16))) uint8_t lds[LDS_BYTES];
     constexpr int LOG2G = G == 1 ? 0 : G == 2 ? 1 : G == 4 ? 2 : 3;
@@ -324,23 +415,23 @@ __global__ void __launch_bounds__(WG_THREADS) aesgcm_batch_kernel(KernelArgs a, 
 
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
-    const uint32_t lb_aes = (uint32_t)(lane & 31) * 4u;
+    const uint32_t lb_aes = (uint32_t)(lane & 31) * 4u | LDS_AES;
     const GhLane gl = gh_lane_init(lane);
     const int r = lane & (G - 1);
     const int grp = lane >> LOG2G;
 
-    build_aes_tables(lds, a.t0);
+    build_aes_tables(lds, t0);
     uint32_t cur_key = 0xffffffffu;
 
-    for (uint32_t ci = blockIdx.x; ci < a.nchunks; ci += gridDim.x) {
-        const Chunk ch = a.chunks[ci];
+    for (uint32_t ci = blockIdx.x; ci < nchunks; ci += gridDim.x) {
+        const Chunk ch = chunks[ci];
         if (ch.key != cur_key) {
             __syncthreads();
-            build_ghash_tables(lds, a.basis + (size_t)ch.key * (NPOW * 128 * 4), LOG2G);
+            build_ghash_tables(lds, basis + (size_t)ch.key * (NPOW * 128 * 4), LOG2G);
             __syncthreads();
             cur_key = ch.key;
         }
-        const KeySlot *__restrict__ slot = a.slots + ch.key;
+        const KeySlot *__restrict__ slot = slots + ch.key;
         const uint32_t *__restrict__ rk = slot->rk;
         const bool fast = (ch.flags & 1u) && base_aligned;
         const int ntasks = (int)((ch.count + R - 1) / R);
@@ -349,7 +440,7 @@ __global__ void __launch_bounds__(WG_THREADS) aesgcm_batch_kernel(KernelArgs a, 
             const uint32_t ridx = (uint32_t)t * R + grp;
             const bool valid = ridx < ch.count;
             const uint32_t rec_i = ch.first + (valid ? ridx : 0);
-            const ptls_hip_record_t rec = a.recs[rec_i];
+            const ptls_hip_record_t rec = recs[rec_i];
             const int L = valid ? (int)rec.len : 0;
             const int A = valid ? (int)rec.aad_len : 0;
             const int na = (A + 15) >> 4, nc = (L + 15) >> 4;
@@ -358,9 +449,9 @@ __global__ void __launch_bounds__(WG_THREADS) aesgcm_batch_kernel(KernelArgs a, 
             const int my_iters = i0 < N ? ((N - 1 - i0) >> LOG2G) + 1 : 0;
             const int iters = wave_max(my_iters);
 
-            const uint8_t *in_p = a.in + rec.in_off;
-            uint8_t *out_p = a.out + rec.out_off;
-            const uint8_t *aad_p = a.aad + rec.aad_off;
+            const uint8_t *in_p = in + rec.in_off;
+            uint8_t *out_p = out + rec.out_off;
+            const uint8_t *aad_p = aad + rec.aad_off;
             const uint32_t n0 = slot->iv[0], n1 = slot->iv[1] ^ bswap32((uint32_t)(rec.seq >> 32)),
                            n2 = slot->iv[2] ^ bswap32((uint32_t)rec.seq);
             const uint64_t abits = (uint64_t)A * 8, cbits = (uint64_t)L * 8;
@@ -368,42 +459,27 @@ __global__ void __launch_bounds__(WG_THREADS) aesgcm_batch_kernel(KernelArgs a, 
                                  bswap32((uint32_t)cbits)};
 
             V4 y = V4{0, 0, 0, 0}, ek0 = V4{0, 0, 0, 0};
-            for (int m = 0; m < iters; ++m) {
-                const int i = i0 + m * G;
-                const bool active = i < N;
-                const bool is_aad = i < na;
-                const bool is_c = !is_aad && i < na + nc;
-                const bool is_len = active && i == N - 1;
-                const int c = i - na;
-                const int nbytes = is_c ? min(16, L - 16 * c) : 0;
-
-                V4 in_blk = V4{0, 0, 0, 0};
-                if (is_c)
-                    in_blk = load_block(in_p + 16 * (size_t)c, nbytes, fast);
-                /* keystream for data block c (counter inc32(J0) + c), or E_K(J0) for the lane holding the length block */
-                const V4 ctr = V4{n0, n1, n2, is_c ? bswap32((uint32_t)c + 2u) : 0x01000000u};
-                const V4 ks = aes_encrypt<ROUNDS>(lds, lb_aes, rk, ctr);
-
-                V4 x = V4{0, 0, 0, 0};
-                if (is_aad) {
-                    x = load_block(aad_p + 16 * i, min(16, A - 16 * i), fast);
-                } else if (is_c) {
-                    const V4 o = v4xor(in_blk, ks);
-                    if (OPEN) {
-                        store_block(out_p + 16 * (size_t)c, nbytes, fast, o);
-                        x = in_blk;
-                    } else {
-                        x = mask_block(o, nbytes);
-                        store_block(out_p + 16 * (size_t)c, nbytes, fast, x);
-                    }
-                } else if (is_len) {
-                    x = lenblk;
-                    ek0 = ks;
-                }
+            /* two Horner elements per iteration: their AES blocks are independent and run interleaved */
+            for (int m = 0; m < iters; m += 2) {
+                const Elem e0 = elem_of(i0 + m * G, N, na, nc, L);
+                const Elem e1 = elem_of(i0 + (m + 1) * G, N, na, nc, L);
+                V4 in0 = V4{0, 0, 0, 0}, in1 = V4{0, 0, 0, 0};
+                if (e0.is_c)
+                    in0 = load_block(in_p + 16 * (size_t)e0.c, e0.nbytes, fast);
+                if (e1.is_c)
+                    in1 = load_block(in_p + 16 * (size_t)e1.c, e1.nbytes, fast);
+                /* keystream for data block c (counter inc32(J0) + c), E_K(J0) for the length-block lane */
+                V4 ks0 = V4{n0, n1, n2, e0.is_c ? bswap32((uint32_t)e0.c + 2u) : 0x01000000u};
+                V4 ks1 = V4{n0, n1, n2, e1.is_c ? bswap32((uint32_t)e1.c + 2u) : 0x01000000u};
+                aes_encrypt2<ROUNDS>(lds, lb_aes, rk, ks0, ks1);
+                const V4 x0 = finish_elem<OPEN>(e0, in0, ks0, aad_p, A, out_p, fast, lenblk, ek0);
+                const V4 x1 = finish_elem<OPEN>(e1, in1, ks1, aad_p, A, out_p, fast, lenblk, ek0);
                 if (m == 0)
-                    y = x;
-                else if (active)
-                    y = gh_mul_main(lds, gl, y, x);
+                    y = x0;
+                else if (e0.active)
+                    y = gh_mul_main(lds, gl, y, x0);
+                if (e1.active)
+                    y = gh_mul_main(lds, gl, y, x1);
             }
 
             /* combine the G partial sums of each record: position q = distance of a lane's last element
@@ -429,7 +505,7 @@ __global__ void __launch_bounds__(WG_THREADS) aesgcm_batch_kernel(KernelArgs a, 
                 if (OPEN) {
                     const V4 rt = load_block(in_p + L, 16, tag_fast);
                     const bool ok = rt.w0 == tag.w0 && rt.w1 == tag.w1 && rt.w2 == tag.w2 && rt.w3 == tag.w3;
-                    a.result[rec_i] = ok ? (uint64_t)L : ~(uint64_t)0;
+                    result[rec_i] = ok ? (uint64_t)L : ~(uint64_t)0;
                 } else {
                     store_block(out_p + L, 16, tag_fast, tag);
                 }
@@ -438,7 +514,11 @@ __global__ void __launch_bounds__(WG_THREADS) aesgcm_batch_kernel(KernelArgs a, 
     }
 }
 
-#define INST(G, R, O) template __global__ void aesgcm_batch_kernel<G, R, O>(KernelArgs, uint32_t);
+#define INST(G, R, O)                                                                                                      \
+    template __global__ void aesgcm_batch_kernel<G, R, O>(const ptls_hip_record_t *__restrict__, const Chunk *__restrict__, \
+                                                          uint32_t, const uint8_t *, const uint8_t *__restrict__, uint8_t *,  \
+                                                          uint64_t *__restrict__, const KeySlot *__restrict__,                \
+                                                          const uint32_t *__restrict__, const uint32_t *__restrict__, uint32_t);
 #define INST_G(G) INST(G, 10, false) INST(G, 10, true) INST(G, 14, false) INST(G, 14, true)
 INST_G(1)
 INST_G(2)
@@ -627,7 +707,8 @@ namespace ptls_hip {
 template <int G, int R, bool O>
 static hipError_t launch_one(unsigned grid, hipStream_t s, const KernelArgs &a, uint32_t al)
 {
-    hipLaunchKernelGGL((aesgcm_batch_kernel<G, R, O>), dim3(grid), dim3(WG_THREADS), 0, s, a, al);
+    hipLaunchKernelGGL((aesgcm_batch_kernel<G, R, O>), dim3(grid), dim3(WG_THREADS), 0, s, a.recs, a.chunks, a.nchunks, a.in,
+                       a.aad, a.out, a.result, a.slots, a.basis, a.t0, al);
     return hipGetLastError();
 }
 
