@@ -238,18 +238,23 @@ __device__ __forceinline__ V4 gh_mul_main(const uint8_t *lds, const GhLane &g, V
     return acc;
 }
 
-/* y * P with a nibble table [p = 8w + j][v] (used only in the per-record reduction tree) */
+/* y * P with a nibble table [p = 8w + j][v] (used only in the per-record reduction tree).  One word
+ * (8 lookups) at a time: sched barriers keep the compiler from hoisting all 32 ds_read_b128 (128 VGPRs). */
 __device__ __forceinline__ V4 gh_mul_nibble(const uint8_t *lds, uint32_t table, V4 y)
 {
     V4 acc = V4{0, 0, 0, 0};
     const uint32_t w[4] = {y.w0, y.w1, y.w2, y.w3};
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
+        V4 t[8];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            const uint32_t v = (w[i] >> (4 * j)) & 15u;
-            acc = v4xor(acc, lds128(lds, table + (uint32_t)(8 * i + j) * 256u + v * 16u));
-        }
+        for (int j = 0; j < 8; ++j)
+            t[j] = lds128(lds, table + (uint32_t)(8 * i + j) * 256u + ((w[i] >> (4 * j)) & 15u) * 16u);
+        acc = v4xor3(acc, t[0], t[1]);
+        acc = v4xor3(acc, t[2], t[3]);
+        acc = v4xor3(acc, t[4], t[5]);
+        acc = v4xor3(acc, t[6], t[7]);
+        __builtin_amdgcn_sched_barrier(0);
     }
     return acc;
 }
@@ -305,31 +310,61 @@ __device__ void build_ghash_tables(uint8_t *lds, const uint32_t *__restrict__ ba
 
 /* ---------------- global-memory block access ---------------- */
 
-__device__ __forceinline__ V4 load_block(const uint8_t *p, int n, bool fast)
+/* 128-bit shifts by one byte (raw byte order: w0 holds bytes 0..3) */
+__device__ __forceinline__ V4 shr8(V4 v)
 {
-    if (fast && n == 16) {
-        const uint4 v = *reinterpret_cast<const uint4 *>(p);
-        return V4{v.x, v.y, v.z, v.w};
-    }
-    uint32_t w[4] = {0, 0, 0, 0};
-#pragma unroll
-    for (int k = 0; k < 16; ++k)
-        if (k < n)
-            w[k >> 2] |= (uint32_t)p[k] << (8 * (k & 3));
-    return V4{w[0], w[1], w[2], w[3]};
+    return V4{__builtin_amdgcn_alignbit(v.w1, v.w0, 8), __builtin_amdgcn_alignbit(v.w2, v.w1, 8),
+              __builtin_amdgcn_alignbit(v.w3, v.w2, 8), v.w3 >> 8};
 }
 
-__device__ __forceinline__ void store_block(uint8_t *p, int n, bool fast, V4 v)
+__device__ __forceinline__ V4 shl8_in(V4 v, uint8_t b)
 {
-    if (fast && n == 16) {
+    return V4{(v.w0 << 8) | b, __builtin_amdgcn_alignbit(v.w1, v.w0, 24), __builtin_amdgcn_alignbit(v.w2, v.w1, 24),
+              __builtin_amdgcn_alignbit(v.w3, v.w2, 24)};
+}
+
+/* exact byte-granular access (n in 0..16): compact loops, used for unaligned layouts and partial stores */
+__device__ __forceinline__ V4 load_bytes(const uint8_t *p, int n)
+{
+    V4 v = V4{0, 0, 0, 0};
+#pragma unroll 1
+    for (int k = n - 1; k >= 0; --k)
+        v = shl8_in(v, p[k]);
+    return v;
+}
+
+__device__ __forceinline__ void store_bytes(uint8_t *p, int n, V4 v)
+{
+#pragma unroll 1
+    for (int k = 0; k < n; ++k) {
+        p[k] = (uint8_t)v.w0;
+        v = shr8(v);
+    }
+}
+
+__device__ __forceinline__ V4 mask_block(V4 v, int n);
+
+/* ALIGNED: p is 16-byte aligned, so the 16-byte chunk holding a partial block never crosses a page;
+ * load it whole and keep the first n bytes.  Otherwise read exactly n bytes. */
+template <bool ALIGNED>
+__device__ __forceinline__ V4 load_block(const uint8_t *p, int n)
+{
+    if (ALIGNED) {
+        const uint4 v = *reinterpret_cast<const uint4 *>(p);
+        const V4 r = V4{v.x, v.y, v.z, v.w};
+        return n == 16 ? r : mask_block(r, n);
+    }
+    return load_bytes(p, n);
+}
+
+template <bool ALIGNED>
+__device__ __forceinline__ void store_block(uint8_t *p, int n, V4 v)
+{
+    if (ALIGNED && n == 16) {
         *reinterpret_cast<uint4 *>(p) = make_uint4(v.w0, v.w1, v.w2, v.w3);
         return;
     }
-    const uint32_t w[4] = {v.w0, v.w1, v.w2, v.w3};
-#pragma unroll
-    for (int k = 0; k < 16; ++k)
-        if (k < n)
-            p[k] = (uint8_t)(w[k >> 2] >> (8 * (k & 3)));
+    store_bytes(p, n, v);
 }
 
 __device__ __forceinline__ V4 mask_block(V4 v, int n)
@@ -376,21 +411,21 @@ __device__ __forceinline__ Elem elem_of(int i, int N, int na, int nc, int L)
     return e;
 }
 
-template <bool OPEN>
-__device__ __forceinline__ V4 finish_elem(const Elem &e, V4 in_blk, V4 ks, const uint8_t *aad_p, int A, uint8_t *out_p, bool fast,
+template <bool OPEN, bool ALIGNED>
+__device__ __forceinline__ V4 finish_elem(const Elem &e, V4 in_blk, V4 ks, const uint8_t *aad_p, int A, uint8_t *out_p,
                                           V4 lenblk, V4 &ek0)
 {
     V4 x = V4{0, 0, 0, 0};
     if (e.is_aad) {
-        x = load_block(aad_p + 16 * e.i, min(16, A - 16 * e.i), fast);
+        x = load_block<ALIGNED>(aad_p + 16 * e.i, min(16, A - 16 * e.i));
     } else if (e.is_c) {
         const V4 o = v4xor(in_blk, ks);
         if (OPEN) {
-            store_block(out_p + 16 * (size_t)e.c, e.nbytes, fast, o);
+            store_block<ALIGNED>(out_p + 16 * (size_t)e.c, e.nbytes, o);
             x = in_blk;
         } else {
             x = mask_block(o, e.nbytes);
-            store_block(out_p + 16 * (size_t)e.c, e.nbytes, fast, x);
+            store_block<ALIGNED>(out_p + 16 * (size_t)e.c, e.nbytes, x);
         }
     } else if (e.is_len) {
         x = lenblk;
@@ -402,12 +437,11 @@ __device__ __forceinline__ V4 finish_elem(const Elem &e, V4 in_blk, V4 ks, const
 /* Pointers are separate __restrict__ kernel parameters (not a struct) so the compiler can prove that
  * the key slots, tables and descriptors are never written by the kernel and read them through the
  * scalar unit (s_load into SGPRs) instead of per-lane vector loads.  in/out may alias (in place). */
-template <int G, int ROUNDS, bool OPEN>
+template <int G, int ROUNDS, bool OPEN, bool ALIGNED>
 __global__ void __launch_bounds__(WG_THREADS)
     aesgcm_batch_kernel(const ptls_hip_record_t *__restrict__ recs, const Chunk *__restrict__ chunks, uint32_t nchunks,
                         const uint8_t *in, const uint8_t *__restrict__ aad, uint8_t *out, uint64_t *__restrict__ result,
-                        const KeySlot *__restrict__ slots, const uint32_t *__restrict__ basis, const uint32_t *__restrict__ t0,
-                        uint32_t base_aligned)
+                        const KeySlot *__restrict__ slots, const uint32_t *__restrict__ basis, const uint32_t *__restrict__ t0)
 {
     __shared__ __attribute__((aligned(16))) uint8_t lds[LDS_BYTES];
     constexpr int LOG2G = G == 1 ? 0 : G == 2 ? 1 : G == 4 ? 2 : 3;
@@ -433,7 +467,6 @@ __global__ void __launch_bounds__(WG_THREADS)
         }
         const KeySlot *__restrict__ slot = slots + ch.key;
         const uint32_t *__restrict__ rk = slot->rk;
-        const bool fast = (ch.flags & 1u) && base_aligned;
         const int ntasks = (int)((ch.count + R - 1) / R);
 
         for (int t = wave; t < ntasks; t += WAVES_PER_WG) {
@@ -459,27 +492,83 @@ __global__ void __launch_bounds__(WG_THREADS)
                                  bswap32((uint32_t)cbits)};
 
             V4 y = V4{0, 0, 0, 0}, ek0 = V4{0, 0, 0, 0};
-            /* two Horner elements per iteration: their AES blocks are independent and run interleaved */
-            for (int m = 0; m < iters; m += 2) {
-                const Elem e0 = elem_of(i0 + m * G, N, na, nc, L);
-                const Elem e1 = elem_of(i0 + (m + 1) * G, N, na, nc, L);
+            /* Iterations handle two Horner elements (i and i + G) of a lane; their AES blocks are independent
+             * and run interleaved.  y = y * P ^ x is exact from y = 0 (0 * P = 0), so no first-element case. */
+            auto generic_iter = [&](int j) {
+                const Elem e0 = elem_of(i0 + 2 * j * G, N, na, nc, L);
+                const Elem e1 = elem_of(i0 + (2 * j + 1) * G, N, na, nc, L);
                 V4 in0 = V4{0, 0, 0, 0}, in1 = V4{0, 0, 0, 0};
                 if (e0.is_c)
-                    in0 = load_block(in_p + 16 * (size_t)e0.c, e0.nbytes, fast);
+                    in0 = load_block<ALIGNED>(in_p + 16 * (size_t)e0.c, e0.nbytes);
                 if (e1.is_c)
-                    in1 = load_block(in_p + 16 * (size_t)e1.c, e1.nbytes, fast);
+                    in1 = load_block<ALIGNED>(in_p + 16 * (size_t)e1.c, e1.nbytes);
                 /* keystream for data block c (counter inc32(J0) + c), E_K(J0) for the length-block lane */
                 V4 ks0 = V4{n0, n1, n2, e0.is_c ? bswap32((uint32_t)e0.c + 2u) : 0x01000000u};
                 V4 ks1 = V4{n0, n1, n2, e1.is_c ? bswap32((uint32_t)e1.c + 2u) : 0x01000000u};
                 aes_encrypt2<ROUNDS>(lds, lb_aes, rk, ks0, ks1);
-                const V4 x0 = finish_elem<OPEN>(e0, in0, ks0, aad_p, A, out_p, fast, lenblk, ek0);
-                const V4 x1 = finish_elem<OPEN>(e1, in1, ks1, aad_p, A, out_p, fast, lenblk, ek0);
-                if (m == 0)
-                    y = x0;
-                else if (e0.active)
+                const V4 x0 = finish_elem<OPEN, ALIGNED>(e0, in0, ks0, aad_p, A, out_p, lenblk, ek0);
+                const V4 x1 = finish_elem<OPEN, ALIGNED>(e1, in1, ks1, aad_p, A, out_p, lenblk, ek0);
+                if (e0.active)
                     y = gh_mul_main(lds, gl, y, x0);
                 if (e1.active)
                     y = gh_mul_main(lds, gl, y, x1);
+            };
+
+            /* "pure" iterations: both elements of every lane of the wave are full data blocks.  There the
+             * body is branch-free, so the GHASH lookups can be scheduled among the AES lookups. */
+            const int nf = L >> 4;
+            const int T = (na + nf - 1 - i0) >= 0 ? (na + nf - 1 - i0) >> LOG2G : -1;
+            const int my_jlo = na > i0 ? (na - i0 + 2 * G - 1) / (2 * G) : 0;
+            const int my_jhi = (ALIGNED && valid && T >= 1) ? (T + 1) >> 1 : 0;
+            const int jlo = wave_max(my_jlo), jhi = -wave_max(-my_jhi);
+            const int jt = (iters + 1) >> 1;
+            const bool has_pure = jhi > jlo;
+            const int pre_end = has_pure ? jlo : jt;
+
+            for (int j = 0; j < pre_end; ++j)
+                generic_iter(j);
+            if (has_pure) {
+                const uint8_t *src = in_p + 16 * (size_t)(i0 - na);
+                uint8_t *dst = out_p + 16 * (size_t)(i0 - na);
+                const uint32_t cbase = (uint32_t)(i0 - na) + 2u;
+                if (OPEN) {
+                    for (int j = jlo; j < jhi; ++j) {
+                        const size_t o = (size_t)(2 * j * G) * 16;
+                        const V4 c0 = load_block<true>(src + o, 16), c1 = load_block<true>(src + o + 16 * G, 16);
+                        V4 k0 = V4{n0, n1, n2, bswap32(cbase + 2 * j * G)}, k1 = V4{n0, n1, n2, bswap32(cbase + (2 * j + 1) * G)};
+                        aes_encrypt2<ROUNDS>(lds, lb_aes, rk, k0, k1);
+                        y = gh_mul_main(lds, gl, gh_mul_main(lds, gl, y, c0), c1);
+                        store_block<true>(dst + o, 16, v4xor(c0, k0));
+                        store_block<true>(dst + o + 16 * G, 16, v4xor(c1, k1));
+                    }
+                } else {
+                    /* software pipelined: the ciphertext of iteration j is hashed during iteration j + 1 */
+                    V4 p0, p1;
+                    {
+                        const size_t o = (size_t)(2 * jlo * G) * 16;
+                        const V4 a0 = load_block<true>(src + o, 16), a1 = load_block<true>(src + o + 16 * G, 16);
+                        V4 k0 = V4{n0, n1, n2, bswap32(cbase + 2 * jlo * G)}, k1 = V4{n0, n1, n2, bswap32(cbase + (2 * jlo + 1) * G)};
+                        aes_encrypt2<ROUNDS>(lds, lb_aes, rk, k0, k1);
+                        p0 = v4xor(a0, k0);
+                        p1 = v4xor(a1, k1);
+                        store_block<true>(dst + o, 16, p0);
+                        store_block<true>(dst + o + 16 * G, 16, p1);
+                    }
+                    for (int j = jlo + 1; j < jhi; ++j) {
+                        const size_t o = (size_t)(2 * j * G) * 16;
+                        const V4 a0 = load_block<true>(src + o, 16), a1 = load_block<true>(src + o + 16 * G, 16);
+                        V4 k0 = V4{n0, n1, n2, bswap32(cbase + 2 * j * G)}, k1 = V4{n0, n1, n2, bswap32(cbase + (2 * j + 1) * G)};
+                        aes_encrypt2<ROUNDS>(lds, lb_aes, rk, k0, k1);
+                        y = gh_mul_main(lds, gl, gh_mul_main(lds, gl, y, p0), p1);
+                        p0 = v4xor(a0, k0);
+                        p1 = v4xor(a1, k1);
+                        store_block<true>(dst + o, 16, p0);
+                        store_block<true>(dst + o + 16 * G, 16, p1);
+                    }
+                    y = gh_mul_main(lds, gl, gh_mul_main(lds, gl, y, p0), p1);
+                }
+                for (int j = jhi; j < jt; ++j)
+                    generic_iter(j);
             }
 
             /* combine the G partial sums of each record: position q = distance of a lane's last element
@@ -501,25 +590,30 @@ __global__ void __launch_bounds__(WG_THREADS)
             if (valid && q == 0) {
                 const V4 s = gh_mul_nibble(lds, LDS_GTREE, y); /* * H */
                 const V4 tag = v4xor(s, ek0);
-                const bool tag_fast = fast && (L & 15) == 0;
+                const bool tag_fast = ALIGNED && (L & 15) == 0;
                 if (OPEN) {
-                    const V4 rt = load_block(in_p + L, 16, tag_fast);
+                    const V4 rt = tag_fast ? load_block<true>(in_p + L, 16) : load_bytes(in_p + L, 16);
                     const bool ok = rt.w0 == tag.w0 && rt.w1 == tag.w1 && rt.w2 == tag.w2 && rt.w3 == tag.w3;
                     result[rec_i] = ok ? (uint64_t)L : ~(uint64_t)0;
                 } else {
-                    store_block(out_p + L, 16, tag_fast, tag);
+                    if (tag_fast)
+                        store_block<true>(out_p + L, 16, tag);
+                    else
+                        store_bytes(out_p + L, 16, tag);
                 }
             }
         }
     }
 }
 
-#define INST(G, R, O)                                                                                                      \
-    template __global__ void aesgcm_batch_kernel<G, R, O>(const ptls_hip_record_t *__restrict__, const Chunk *__restrict__, \
-                                                          uint32_t, const uint8_t *, const uint8_t *__restrict__, uint8_t *,  \
-                                                          uint64_t *__restrict__, const KeySlot *__restrict__,                \
-                                                          const uint32_t *__restrict__, const uint32_t *__restrict__, uint32_t);
-#define INST_G(G) INST(G, 10, false) INST(G, 10, true) INST(G, 14, false) INST(G, 14, true)
+#define INST(G, R, O, A)                                                                                                   \
+    template __global__ void aesgcm_batch_kernel<G, R, O, A>(const ptls_hip_record_t *__restrict__, const Chunk *__restrict__, \
+                                                             uint32_t, const uint8_t *, const uint8_t *__restrict__, uint8_t *,  \
+                                                             uint64_t *__restrict__, const KeySlot *__restrict__,                \
+                                                             const uint32_t *__restrict__, const uint32_t *__restrict__);
+#define INST_G(G)                                                                                                          \
+    INST(G, 10, false, true) INST(G, 10, true, true) INST(G, 14, false, true) INST(G, 14, true, true)                       \
+    INST(G, 10, false, false) INST(G, 10, true, false) INST(G, 14, false, false) INST(G, 14, true, false)
 INST_G(1)
 INST_G(2)
 INST_G(4)
@@ -692,7 +786,11 @@ __global__ void fill_records_kernel(const ptls_hip_record_t *recs, uint32_t n, u
             const uint64_t v0 = splitmix_mix(sd + (wi + 1) * 0x9e3779b97f4a7c15ull);
             const uint64_t v1 = splitmix_mix(sd + (wi + 2) * 0x9e3779b97f4a7c15ull);
             const int nb = (int)min(16u, rec.len - off);
-            store_block(p + off, nb, al, V4{(uint32_t)v0, (uint32_t)(v0 >> 32), (uint32_t)v1, (uint32_t)(v1 >> 32)});
+            const V4 v = V4{(uint32_t)v0, (uint32_t)(v0 >> 32), (uint32_t)v1, (uint32_t)(v1 >> 32)};
+            if (al)
+                store_block<true>(p + off, nb, v);
+            else
+                store_bytes(p + off, nb, v);
         }
     }
 }
@@ -705,38 +803,42 @@ __global__ void fill_records_kernel(const ptls_hip_record_t *recs, uint32_t n, u
 namespace ptls_hip {
 
 template <int G, int R, bool O>
-static hipError_t launch_one(unsigned grid, hipStream_t s, const KernelArgs &a, uint32_t al)
+static hipError_t launch_one(unsigned grid, hipStream_t s, const KernelArgs &a, bool aligned)
 {
-    hipLaunchKernelGGL((aesgcm_batch_kernel<G, R, O>), dim3(grid), dim3(WG_THREADS), 0, s, a.recs, a.chunks, a.nchunks, a.in,
-                       a.aad, a.out, a.result, a.slots, a.basis, a.t0, al);
+    if (aligned)
+        hipLaunchKernelGGL((aesgcm_batch_kernel<G, R, O, true>), dim3(grid), dim3(WG_THREADS), 0, s, a.recs, a.chunks, a.nchunks,
+                           a.in, a.aad, a.out, a.result, a.slots, a.basis, a.t0);
+    else
+        hipLaunchKernelGGL((aesgcm_batch_kernel<G, R, O, false>), dim3(grid), dim3(WG_THREADS), 0, s, a.recs, a.chunks,
+                           a.nchunks, a.in, a.aad, a.out, a.result, a.slots, a.basis, a.t0);
     return hipGetLastError();
 }
 
 template <int G>
-static hipError_t launch_g(int rounds, bool open, unsigned grid, hipStream_t s, const KernelArgs &a, uint32_t al)
+static hipError_t launch_g(int rounds, bool open, unsigned grid, hipStream_t s, const KernelArgs &a, bool al)
 {
     if (rounds == 10)
         return open ? launch_one<G, 10, true>(grid, s, a, al) : launch_one<G, 10, false>(grid, s, a, al);
     return open ? launch_one<G, 14, true>(grid, s, a, al) : launch_one<G, 14, false>(grid, s, a, al);
 }
 
-int launch_batch(int lanes, int rounds, bool open, unsigned grid, void *stream, const KernelArgs &a, bool base_aligned)
+/* `aligned`: every record's in/out/aad offset and the three base pointers are 16-byte aligned */
+int launch_batch(int lanes, int rounds, bool open, unsigned grid, void *stream, const KernelArgs &a, bool aligned)
 {
     hipStream_t s = static_cast<hipStream_t>(stream);
-    const uint32_t al = base_aligned ? 1u : 0u;
     hipError_t e;
     switch (lanes) {
     case 1:
-        e = launch_g<1>(rounds, open, grid, s, a, al);
+        e = launch_g<1>(rounds, open, grid, s, a, aligned);
         break;
     case 2:
-        e = launch_g<2>(rounds, open, grid, s, a, al);
+        e = launch_g<2>(rounds, open, grid, s, a, aligned);
         break;
     case 4:
-        e = launch_g<4>(rounds, open, grid, s, a, al);
+        e = launch_g<4>(rounds, open, grid, s, a, aligned);
         break;
     case 8:
-        e = launch_g<8>(rounds, open, grid, s, a, al);
+        e = launch_g<8>(rounds, open, grid, s, a, aligned);
         break;
     default:
         return (int)hipErrorInvalidValue;

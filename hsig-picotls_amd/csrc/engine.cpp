@@ -118,6 +118,7 @@ struct st_ptls_hip_batch_t {
     Chunk *d_chunks;
     uint32_t nchunks;
     int lanes;      /* in use */
+    bool all_aligned; /* every descriptor's in/out/aad offset is a multiple of 16 */
     int auto_lanes; /* chosen from the record lengths */
     bool forced;
 };
@@ -350,6 +351,9 @@ static int plan_chunks(ptls_hip_batch_t *b)
         (void)hipFree(b->d_chunks);
     b->d_chunks = nullptr;
     b->nchunks = (uint32_t)ch.size();
+    b->all_aligned = true;
+    for (const auto &c : ch)
+        b->all_aligned = b->all_aligned && (c.flags & 1u);
     if (ch.empty())
         return 0;
     HIP_TRY(hipMalloc(&b->d_chunks, ch.size() * sizeof(Chunk)), PTLS_HIP_ENOMEM);
@@ -442,9 +446,10 @@ static int run_batch(ptls_hip_batch_t *b, ptls_hip_keyset_t *ks, const void *in,
     a.t0 = b->eng->d_t0;
     const bool base_aligned = ((reinterpret_cast<uintptr_t>(in) | reinterpret_cast<uintptr_t>(a.aad) |
                                 reinterpret_cast<uintptr_t>(out)) & 15) == 0;
+    const bool aligned = base_aligned && b->all_aligned;
     const unsigned grid = std::min<unsigned>(b->nchunks, (unsigned)b->eng->ncu);
     const int rounds = ks->key_size == 16 ? 10 : 14;
-    int e = launch_batch(b->lanes, rounds, open, grid, stream, a, base_aligned);
+    int e = launch_batch(b->lanes, rounds, open, grid, stream, a, aligned);
     if (e != 0)
         return fail(PTLS_HIP_ELAUNCH, "kernel launch failed: %s", hipGetErrorString((hipError_t)e));
     return 0;

@@ -1,0 +1,25 @@
+#!/usr/bin/env python3
+"""Summarise tools/pmc_passes.sh output: per-dispatch counter values of the batch kernel (first dispatch
+of each bench step = seal), averaged."""
+import csv
+import glob
+import sys
+from collections import defaultdict
+
+out = sys.argv[1]
+vals = defaultdict(list)
+for f in sorted(glob.glob(f"{out}/pass*/run_counter_collection.csv")):
+    rows = [r for r in csv.DictReader(open(f)) if r["Kernel_Name"].startswith("aesgcm")]
+    ids = sorted({int(r["Dispatch_Id"]) for r in rows})
+    seal_ids = set(ids[0::2])  # seal, open, seal, open, ...
+    for r in rows:
+        if int(r["Dispatch_Id"]) in seal_ids:
+            vals[r["Counter_Name"]].append(float(r["Counter_Value"]))
+avg = {k: sum(v) / len(v) for k, v in vals.items()}
+for k in sorted(avg):
+    print(f"{k:28s} {avg[k]:18.1f}")
+if "SQ_WAVE_CYCLES" in avg and "SQ_BUSY_CYCLES" in avg:
+    wc = avg["SQ_WAVE_CYCLES"]
+    print("--- shares of wave-cycles: wait_any %.3f wait_inst_any %.3f active_any %.3f valu %.3f lds %.3f" % (
+        avg["SQ_WAIT_ANY"] / wc, avg["SQ_WAIT_INST_ANY"] / wc, avg["SQ_ACTIVE_INST_ANY"] / wc,
+        avg["SQ_ACTIVE_INST_VALU"] / wc, avg["SQ_ACTIVE_INST_LDS"] / wc))
