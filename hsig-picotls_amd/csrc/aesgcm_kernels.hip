@@ -32,6 +32,22 @@ constexpr uint32_t LDS_GTREE = 131072;       /* 3 x 8 KiB nibble tables for H^1,
 constexpr uint32_t LDS_TREE_STRIDE = 8192;
 constexpr uint32_t LDS_BYTES = LDS_GTREE + 3 * LDS_TREE_STRIDE; /* 152 KiB of the CU's 160 KiB */
 
+#ifndef PREFETCH_BARRIER
+#define PREFETCH_BARRIER 1
+#endif
+#ifndef ABLATE_AES
+#define ABLATE_AES 0
+#endif
+#ifndef ABLATE_GHASH
+#define ABLATE_GHASH 0
+#endif
+#ifndef GHASH_HALF_BARRIER
+#define GHASH_HALF_BARRIER 0
+#endif
+#ifndef PURE_BLOCKS
+#define PURE_BLOCKS 2 /* data blocks per lane per iteration of the branch-free loop */
+#endif
+
 struct V4 {
     uint32_t w0, w1, w2, w3;
 };
@@ -177,6 +193,46 @@ __device__ __forceinline__ void aes_encrypt2(const uint8_t *lds, uint32_t lb, co
     u = V4{v0, v1, v2, v3};
 }
 
+/* K independent blocks, round-interleaved */
+template <int ROUNDS, int K>
+__device__ __forceinline__ void aes_encrypt_n(const uint8_t *lds, uint32_t lb, const uint32_t *__restrict__ rk, V4 (&s)[K])
+{
+#pragma unroll
+    for (int b = 0; b < K; ++b) {
+        s[b].w0 ^= rk[0];
+        s[b].w1 ^= rk[1];
+        s[b].w2 ^= rk[2];
+        s[b].w3 ^= rk[3];
+    }
+#pragma unroll
+    for (int r = 1; r < ROUNDS; ++r) {
+        const uint32_t k0 = rk[4 * r + 0], k1 = rk[4 * r + 1], k2 = rk[4 * r + 2], k3 = rk[4 * r + 3];
+        V4 t[K];
+#pragma unroll
+        for (int b = 0; b < K; ++b) {
+            t[b].w0 = aes_col(lds, lb, s[b].w0, s[b].w1, s[b].w2, s[b].w3, k0);
+            t[b].w1 = aes_col(lds, lb, s[b].w1, s[b].w2, s[b].w3, s[b].w0, k1);
+            t[b].w2 = aes_col(lds, lb, s[b].w2, s[b].w3, s[b].w0, s[b].w1, k2);
+            t[b].w3 = aes_col(lds, lb, s[b].w3, s[b].w0, s[b].w1, s[b].w2, k3);
+        }
+#pragma unroll
+        for (int b = 0; b < K; ++b)
+            s[b] = t[b];
+    }
+    const uint32_t k0 = rk[4 * ROUNDS + 0], k1 = rk[4 * ROUNDS + 1], k2 = rk[4 * ROUNDS + 2], k3 = rk[4 * ROUNDS + 3];
+    V4 t[K];
+#pragma unroll
+    for (int b = 0; b < K; ++b) {
+        t[b].w0 = aes_col_last(lds, lb, s[b].w0, s[b].w1, s[b].w2, s[b].w3, k0);
+        t[b].w1 = aes_col_last(lds, lb, s[b].w1, s[b].w2, s[b].w3, s[b].w0, k1);
+        t[b].w2 = aes_col_last(lds, lb, s[b].w2, s[b].w3, s[b].w0, s[b].w1, k2);
+        t[b].w3 = aes_col_last(lds, lb, s[b].w3, s[b].w0, s[b].w1, s[b].w2, k3);
+    }
+#pragma unroll
+    for (int b = 0; b < K; ++b)
+        s[b] = t[b];
+}
+
 /* ======================================================================================= *
  *  GHASH multiply by table                                                                 *
  * ======================================================================================= */
@@ -231,6 +287,9 @@ __device__ __forceinline__ V4 gh_mul_main(const uint8_t *lds, const GhLane &g, V
     acc = v4xor3(acc, gh_term<2>(lds, x0, g.lb0), gh_term<3>(lds, x0, g.lb0));
     acc = v4xor3(acc, gh_term<4>(lds, x1, g.lb1), gh_term<5>(lds, x1, g.lb1));
     acc = v4xor3(acc, gh_term<6>(lds, x1, g.lb1), gh_term<7>(lds, x1, g.lb1));
+#if GHASH_HALF_BARRIER
+    __builtin_amdgcn_sched_barrier(0);
+#endif
     acc = v4xor3(acc, gh_term<8>(lds, x2, g.lb2), gh_term<9>(lds, x2, g.lb2));
     acc = v4xor3(acc, gh_term<10>(lds, x2, g.lb2), gh_term<11>(lds, x2, g.lb2));
     acc = v4xor3(acc, gh_term<12>(lds, x3, g.lb3), gh_term<13>(lds, x3, g.lb3));
@@ -412,8 +471,8 @@ __device__ __forceinline__ Elem elem_of(int i, int N, int na, int nc, int L)
 }
 
 template <bool OPEN, bool ALIGNED>
-__device__ __forceinline__ V4 finish_elem(const Elem &e, V4 in_blk, V4 ks, const uint8_t *aad_p, int A, uint8_t *out_p,
-                                          V4 lenblk, V4 &ek0)
+__device__ __forceinline__ V4 finish_elem(const Elem &e, V4 in_blk, V4 ks, const uint8_t *aad_p, int A, int L, uint8_t *out_p,
+                                          V4 &ek0)
 {
     V4 x = V4{0, 0, 0, 0};
     if (e.is_aad) {
@@ -427,8 +486,8 @@ __device__ __forceinline__ V4 finish_elem(const Elem &e, V4 in_blk, V4 ks, const
             x = mask_block(o, e.nbytes);
             store_block<ALIGNED>(out_p + 16 * (size_t)e.c, e.nbytes, x);
         }
-    } else if (e.is_len) {
-        x = lenblk;
+    } else if (e.is_len) { /* [len(A)]64 || [len(C)]64 in bits, big-endian (lib/fusion.c:468) */
+        x = V4{0, bswap32((uint32_t)A << 3), 0, bswap32((uint32_t)L << 3)};
         ek0 = ks;
     }
     return x;
@@ -487,88 +546,106 @@ __global__ void __launch_bounds__(WG_THREADS)
             const uint8_t *aad_p = aad + rec.aad_off;
             const uint32_t n0 = slot->iv[0], n1 = slot->iv[1] ^ bswap32((uint32_t)(rec.seq >> 32)),
                            n2 = slot->iv[2] ^ bswap32((uint32_t)rec.seq);
-            const uint64_t abits = (uint64_t)A * 8, cbits = (uint64_t)L * 8;
-            const V4 lenblk = V4{bswap32((uint32_t)(abits >> 32)), bswap32((uint32_t)abits), bswap32((uint32_t)(cbits >> 32)),
-                                 bswap32((uint32_t)cbits)};
 
             V4 y = V4{0, 0, 0, 0}, ek0 = V4{0, 0, 0, 0};
             /* Iterations handle two Horner elements (i and i + G) of a lane; their AES blocks are independent
              * and run interleaved.  y = y * P ^ x is exact from y = 0 (0 * P = 0), so no first-element case. */
-            auto generic_iter = [&](int j) {
-                const Elem e0 = elem_of(i0 + 2 * j * G, N, na, nc, L);
-                const Elem e1 = elem_of(i0 + (2 * j + 1) * G, N, na, nc, L);
-                V4 in0 = V4{0, 0, 0, 0}, in1 = V4{0, 0, 0, 0};
+            auto generic_iter_m = [&](int m) {
+                const Elem e0 = elem_of(i0 + m * G, N, na, nc, L);
+                V4 in0 = V4{0, 0, 0, 0};
                 if (e0.is_c)
                     in0 = load_block<ALIGNED>(in_p + 16 * (size_t)e0.c, e0.nbytes);
-                if (e1.is_c)
-                    in1 = load_block<ALIGNED>(in_p + 16 * (size_t)e1.c, e1.nbytes);
                 /* keystream for data block c (counter inc32(J0) + c), E_K(J0) for the length-block lane */
-                V4 ks0 = V4{n0, n1, n2, e0.is_c ? bswap32((uint32_t)e0.c + 2u) : 0x01000000u};
-                V4 ks1 = V4{n0, n1, n2, e1.is_c ? bswap32((uint32_t)e1.c + 2u) : 0x01000000u};
-                aes_encrypt2<ROUNDS>(lds, lb_aes, rk, ks0, ks1);
-                const V4 x0 = finish_elem<OPEN, ALIGNED>(e0, in0, ks0, aad_p, A, out_p, lenblk, ek0);
-                const V4 x1 = finish_elem<OPEN, ALIGNED>(e1, in1, ks1, aad_p, A, out_p, lenblk, ek0);
+                V4 ks0[1] = {V4{n0, n1, n2, e0.is_c ? bswap32((uint32_t)e0.c + 2u) : 0x01000000u}};
+                aes_encrypt_n<ROUNDS, 1>(lds, lb_aes, rk, ks0);
+                const V4 x0 = finish_elem<OPEN, ALIGNED>(e0, in0, ks0[0], aad_p, A, L, out_p, ek0);
                 if (e0.active)
                     y = gh_mul_main(lds, gl, y, x0);
-                if (e1.active)
-                    y = gh_mul_main(lds, gl, y, x1);
             };
 
-            /* "pure" iterations: both elements of every lane of the wave are full data blocks.  There the
-             * body is branch-free, so the GHASH lookups can be scheduled among the AES lookups. */
+            /* "pure" stretch: elements m in [pm0, pm1) of every lane of the wave are full, aligned data blocks.
+             * There the body is branch-free and handles KP blocks per iteration, so their AES lookups and the
+             * GHASH lookups of the previous iteration's ciphertext can all be in flight together. */
+            constexpr int KP = PURE_BLOCKS;
             const int nf = L >> 4;
-            const int T = (na + nf - 1 - i0) >= 0 ? (na + nf - 1 - i0) >> LOG2G : -1;
-            const int my_jlo = na > i0 ? (na - i0 + 2 * G - 1) / (2 * G) : 0;
-            const int my_jhi = (ALIGNED && valid && T >= 1) ? (T + 1) >> 1 : 0;
-            const int jlo = wave_max(my_jlo), jhi = -wave_max(-my_jhi);
-            const int jt = (iters + 1) >> 1;
-            const bool has_pure = jhi > jlo;
-            const int pre_end = has_pure ? jlo : jt;
+            const int my_mlo = na > i0 ? (na - i0 + G - 1) >> LOG2G : 0;
+            const int my_mhi = (ALIGNED && valid && na + nf - 1 - i0 >= 0) ? ((na + nf - 1 - i0) >> LOG2G) + 1 : 0;
+            const int pm0 = wave_max(my_mlo);
+            const int pm_hi = -wave_max(-my_mhi);
+            const int npure = pm_hi > pm0 ? (pm_hi - pm0) / KP : 0;
+            const int pm1 = pm0 + npure * KP;
 
-            for (int j = 0; j < pre_end; ++j)
-                generic_iter(j);
-            if (has_pure) {
-                const uint8_t *src = in_p + 16 * (size_t)(i0 - na);
-                uint8_t *dst = out_p + 16 * (size_t)(i0 - na);
-                const uint32_t cbase = (uint32_t)(i0 - na) + 2u;
-                if (OPEN) {
-                    for (int j = jlo; j < jhi; ++j) {
-                        const size_t o = (size_t)(2 * j * G) * 16;
-                        const V4 c0 = load_block<true>(src + o, 16), c1 = load_block<true>(src + o + 16 * G, 16);
-                        V4 k0 = V4{n0, n1, n2, bswap32(cbase + 2 * j * G)}, k1 = V4{n0, n1, n2, bswap32(cbase + (2 * j + 1) * G)};
-                        aes_encrypt2<ROUNDS>(lds, lb_aes, rk, k0, k1);
-                        y = gh_mul_main(lds, gl, gh_mul_main(lds, gl, y, c0), c1);
-                        store_block<true>(dst + o, 16, v4xor(c0, k0));
-                        store_block<true>(dst + o + 16 * G, 16, v4xor(c1, k1));
+            for (int j = 0; j < (npure ? pm0 : iters); ++j)
+                generic_iter_m(j);
+            if (npure) {
+                const uint8_t *src = in_p + 16 * (size_t)(i0 - na + pm0 * G);
+                uint8_t *dst = out_p + 16 * (size_t)(i0 - na + pm0 * G);
+                const uint32_t cbase = (uint32_t)(i0 - na + pm0 * G) + 2u;
+                V4 pend[KP], bufA[KP], bufB[KP];
+                /* ping-pong prefetch: iteration `it` consumes the buffer loaded one iteration earlier and refills
+                 * the other one for it + 1 (clamped to the last iteration so the body stays branch-free).  Two
+                 * named buffers instead of a copy keep the compiler from waiting on the fresh loads. */
+#pragma unroll
+                for (int b = 0; b < KP; ++b)
+                    bufA[b] = load_block<true>(src + 16 * b * G, 16);
+                /* one branch-free iteration; `hash_pending` is a literal at every call site */
+                auto pure_iter = [&](int it, bool hash_pending, V4(&d)[KP], V4(&dn)[KP]) {
+                    const size_t o = (size_t)(it * KP * G) * 16;
+                    const size_t on = (size_t)(min(it + 1, npure - 1) * KP * G) * 16;
+                    V4 k[KP];
+#pragma unroll
+                    for (int b = 0; b < KP; ++b) {
+                        dn[b] = load_block<true>(src + on + 16 * b * G, 16);
+                        k[b] = V4{n0, n1, n2, bswap32(cbase + (uint32_t)((it * KP + b) * G))};
                     }
-                } else {
-                    /* software pipelined: the ciphertext of iteration j is hashed during iteration j + 1 */
-                    V4 p0, p1;
-                    {
-                        const size_t o = (size_t)(2 * jlo * G) * 16;
-                        const V4 a0 = load_block<true>(src + o, 16), a1 = load_block<true>(src + o + 16 * G, 16);
-                        V4 k0 = V4{n0, n1, n2, bswap32(cbase + 2 * jlo * G)}, k1 = V4{n0, n1, n2, bswap32(cbase + (2 * jlo + 1) * G)};
-                        aes_encrypt2<ROUNDS>(lds, lb_aes, rk, k0, k1);
-                        p0 = v4xor(a0, k0);
-                        p1 = v4xor(a1, k1);
-                        store_block<true>(dst + o, 16, p0);
-                        store_block<true>(dst + o + 16 * G, 16, p1);
+#if PREFETCH_BARRIER
+                    __builtin_amdgcn_sched_barrier(0); /* keep the prefetch at the top of the iteration */
+#endif
+#if ABLATE_AES /* timing-only diagnostic build: keystream = counter block */
+#else
+                    aes_encrypt_n<ROUNDS, KP>(lds, lb_aes, rk, k);
+#endif
+                    if (OPEN) {
+                        /* the input is the ciphertext: hash it in the same iteration */
+#pragma unroll
+                        for (int b = 0; b < KP; ++b)
+                            y = gh_mul_main(lds, gl, y, d[b]);
+#pragma unroll
+                        for (int b = 0; b < KP; ++b)
+                            store_block<true>(dst + o + 16 * b * G, 16, v4xor(d[b], k[b]));
+                    } else {
+                        /* software pipelined: the ciphertext of iteration it is hashed during iteration it + 1 */
+                        if (hash_pending) {
+#pragma unroll
+                            for (int b = 0; b < KP; ++b)
+#if ABLATE_GHASH /* timing-only diagnostic build */
+                                y = v4xor(y, pend[b]);
+#else
+                                y = gh_mul_main(lds, gl, y, pend[b]);
+#endif
+                        }
+#pragma unroll
+                        for (int b = 0; b < KP; ++b) {
+                            pend[b] = v4xor(d[b], k[b]);
+                            store_block<true>(dst + o + 16 * b * G, 16, pend[b]);
+                        }
                     }
-                    for (int j = jlo + 1; j < jhi; ++j) {
-                        const size_t o = (size_t)(2 * j * G) * 16;
-                        const V4 a0 = load_block<true>(src + o, 16), a1 = load_block<true>(src + o + 16 * G, 16);
-                        V4 k0 = V4{n0, n1, n2, bswap32(cbase + 2 * j * G)}, k1 = V4{n0, n1, n2, bswap32(cbase + (2 * j + 1) * G)};
-                        aes_encrypt2<ROUNDS>(lds, lb_aes, rk, k0, k1);
-                        y = gh_mul_main(lds, gl, gh_mul_main(lds, gl, y, p0), p1);
-                        p0 = v4xor(a0, k0);
-                        p1 = v4xor(a1, k1);
-                        store_block<true>(dst + o, 16, p0);
-                        store_block<true>(dst + o + 16 * G, 16, p1);
-                    }
-                    y = gh_mul_main(lds, gl, gh_mul_main(lds, gl, y, p0), p1);
+                };
+                pure_iter(0, false, bufA, bufB);
+                int it = 1;
+                for (; it + 1 < npure; it += 2) {
+                    pure_iter(it, true, bufB, bufA);
+                    pure_iter(it + 1, true, bufA, bufB);
                 }
-                for (int j = jhi; j < jt; ++j)
-                    generic_iter(j);
+                if (it < npure)
+                    pure_iter(it, true, bufB, bufA);
+                if (!OPEN) {
+#pragma unroll
+                    for (int b = 0; b < KP; ++b)
+                        y = gh_mul_main(lds, gl, y, pend[b]);
+                }
+                for (int j = pm1; j < iters; ++j)
+                    generic_iter_m(j);
             }
 
             /* combine the G partial sums of each record: position q = distance of a lane's last element

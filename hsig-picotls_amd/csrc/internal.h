@@ -18,7 +18,10 @@ namespace ptls_hip {
 
 constexpr int NPOW = 4;          /* H^1, H^2, H^4, H^8 */
 constexpr int MAX_LANES = 8;     /* lanes per record (G) supported: 1, 2, 4, 8 */
-constexpr int WG_THREADS = 512;  /* 8 waves: one workgroup per CU (LDS-limited), 2 waves per SIMD */
+#ifndef PTLS_HIP_WG_THREADS
+#define PTLS_HIP_WG_THREADS 1024
+#endif
+constexpr int WG_THREADS = PTLS_HIP_WG_THREADS; /* one workgroup per CU (LDS-limited): 16 waves = 4 per SIMD */
 constexpr int WAVES_PER_WG = WG_THREADS / 64;
 
 struct KeySlot {

@@ -10,7 +10,7 @@ import os
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libptls_hip.so")
+LIB_PATH = os.environ.get("PTLS_HIP_LIB") or os.path.join(HERE, "libptls_hip.so")
 UINT64_MAX = (1 << 64) - 1
 
 RECORD_DTYPE = np.dtype([("in_off", "<u8"), ("out_off", "<u8"), ("aad_off", "<u8"), ("seq", "<u8"),
