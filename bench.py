@@ -202,6 +202,57 @@ def golden_check(cfg_name, idx, recs, d_ct):
     return checked
 
 
+def host_e2e(args, cfg, eng, ks, recs, lens, d_pt, d_aad, aad_len):
+    """Records start and end in pinned host memory (socket-buffer case): ptls_hip_pipeline_seal/open slice the
+    batch and overlap H2D -> kernel -> D2H on three streams.  Timed wall-clock around the whole call."""
+    import torch
+    import ptls_hip
+    L_mean = float(lens.mean())
+    n = args.e2e_records or max(1, min(len(recs), int((1 << 30) / L_mean)))
+    sub = recs[:n].copy()
+    in_lo, out_lo = int(sub["in_off"][0]), int(sub["out_off"][0])
+    in_hi = int(sub["in_off"][-1] + sub["len"][-1] + 16)
+    out_hi = int(sub["out_off"][-1] + sub["len"][-1] + 16)
+    sub["in_off"] -= np.uint64(in_lo)
+    sub["out_off"] -= np.uint64(out_lo)
+    sub["aad_off"] = np.arange(n, dtype=np.uint64) * np.uint64(16)
+    h_in = torch.empty(in_hi - in_lo, dtype=torch.uint8).pin_memory()
+    h_in.copy_(d_pt[in_lo:in_hi])
+    h_aad = torch.empty(n * 16, dtype=torch.uint8).pin_memory()
+    h_aad.copy_(d_aad[: n * 16])
+    h_ct = torch.empty(out_hi - out_lo, dtype=torch.uint8).pin_memory()
+    h_pt = torch.empty(in_hi - in_lo, dtype=torch.uint8).pin_memory()
+    h_res = torch.zeros(n, dtype=torch.int64).pin_memory()
+    sub_o = sub.copy()
+    sub_o["in_off"], sub_o["out_off"] = sub["out_off"], sub["in_off"]
+    pipe = ptls_hip.Pipeline(eng, 64 << 20)
+    pipe.seal(ks, sub, h_in, h_aad, h_ct)  # warm-up
+    ts, to = [], []
+    for _ in range(3):
+        t0 = time.perf_counter()
+        pipe.seal(ks, sub, h_in, h_aad, h_ct)
+        ts.append(time.perf_counter() - t0)
+        t0 = time.perf_counter()
+        pipe.open(ks, sub_o, h_ct, h_aad, h_pt, h_res)
+        to.append(time.perf_counter() - t0)
+    pipe.close()
+    # compare record bytes only (gaps between 16-byte aligned records are never written)
+    edge = np.zeros(in_hi - in_lo + 1, dtype=np.int32)
+    np.add.at(edge, sub["in_off"].astype(np.int64), 1)
+    np.add.at(edge, (sub["in_off"] + sub["len"]).astype(np.int64), -1)
+    mask = np.cumsum(edge[:-1]) > 0
+    ok = bool((h_res.numpy() == sub["len"].astype(np.int64)).all()) and \
+        bool(np.array_equal(h_pt.numpy()[mask], h_in.numpy()[mask]))
+    if not ok:
+        raise AssertionError("host-resident round trip failed")
+    sumL = float(sub["len"].sum())
+    t_s, t_o = float(np.median(ts)), float(np.median(to))
+    return dict(records=n, bytes_in=int(sumL), slice_bytes=64 << 20, streams=3,
+                seal_gibps=round(sumL / t_s / GIB, 2), open_gibps=round(sumL / t_o / GIB, 2),
+                seal_open_gibps=round(2 * sumL / (t_s + t_o) / GIB, 2), roundtrip_ok=ok,
+                note="pinned host buffers; wall clock around ptls_hip_pipeline_seal/open incl. H2D + D2H")
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -211,6 +262,8 @@ def main():
     ap.add_argument("--lanes", type=int, default=0)
     ap.add_argument("--records", type=int, default=0, help="override records per GPU (smaller runs)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-e2e", action="store_true", help="skip the host-resident (pinned H2D/D2H) measurement")
+    ap.add_argument("--e2e-records", type=int, default=0, help="records in the host-resident sample (default: 1 GiB)")
     args = ap.parse_args()
 
     import torch
@@ -332,6 +385,8 @@ def main():
                      "kernel": "aesgcm_batch_kernel (seal)", "algorithmic_bytes_per_launch": alg_bytes},
         "parity": {"open_all_ok": ok_open, "roundtrip_bytes_equal": ok_pt, "golden_records_checked": golden_n},
     }
+    if not args.no_e2e:
+        result["host_e2e"] = host_e2e(args, cfg, eng, ks, recs, lens, d_pt, d_aad, aad_len)
     tfile = os.path.join(ROOT, "profiles", f"traffic_{args.config}.json")
     if os.path.exists(tfile):
         with open(tfile) as f:

@@ -325,35 +325,39 @@ static int choose_lanes(const std::vector<ptls_hip_record_t> &recs)
     return mean >= 128 ? 8 : mean >= 48 ? 4 : mean >= 16 ? 2 : 1;
 }
 
-static int plan_chunks(ptls_hip_batch_t *b)
+/* chunk = run of records with one key slot, sized to keep all waves of a workgroup busy for a few tasks */
+static void build_chunks(const ptls_hip_record_t *recs, size_t n, int lanes, std::vector<Chunk> &ch, bool &all_aligned)
 {
-    /* chunk = run of records with one key slot, sized to keep all 8 waves busy for a few tasks */
-    const uint32_t per_task = 64u / (uint32_t)b->lanes;
+    const uint32_t per_task = 64u / (uint32_t)lanes;
     const uint32_t max_chunk = per_task * WAVES_PER_WG * 2;
-    std::vector<Chunk> ch;
+    ch.clear();
+    all_aligned = true;
     size_t i = 0;
-    while (i < b->n) {
+    while (i < n) {
         Chunk c;
         c.first = (uint32_t)i;
-        c.key = b->h_recs[i].key;
+        c.key = recs[i].key;
         c.count = 0;
         c.flags = 1;
-        while (i < b->n && b->h_recs[i].key == c.key && c.count < max_chunk) {
-            const auto &r = b->h_recs[i];
-            if (((r.in_off | r.out_off | r.aad_off) & 15) != 0)
+        while (i < n && recs[i].key == c.key && c.count < max_chunk) {
+            if (((recs[i].in_off | recs[i].out_off | recs[i].aad_off) & 15) != 0)
                 c.flags = 0;
             ++c.count;
             ++i;
         }
+        all_aligned = all_aligned && (c.flags & 1u);
         ch.push_back(c);
     }
+}
+
+static int plan_chunks(ptls_hip_batch_t *b)
+{
+    std::vector<Chunk> ch;
+    build_chunks(b->h_recs.data(), b->n, b->lanes, ch, b->all_aligned);
     if (b->d_chunks != nullptr)
         (void)hipFree(b->d_chunks);
     b->d_chunks = nullptr;
     b->nchunks = (uint32_t)ch.size();
-    b->all_aligned = true;
-    for (const auto &c : ch)
-        b->all_aligned = b->all_aligned && (c.flags & 1u);
     if (ch.empty())
         return 0;
     HIP_TRY(hipMalloc(&b->d_chunks, ch.size() * sizeof(Chunk)), PTLS_HIP_ENOMEM);
@@ -480,6 +484,211 @@ extern "C" int ptls_hip_fill_records(ptls_hip_batch_t *b, void *buf, uint64_t se
     if (e != 0)
         return fail(PTLS_HIP_ELAUNCH, "fill launch failed: %s", hipGetErrorString((hipError_t)e));
     return 0;
+}
+
+/* ---------------------------------------------------------------------------------------------- */
+/* host-resident pipeline: pinned H2D -> kernel -> D2H, overlapped over NSLOT streams                */
+/* ---------------------------------------------------------------------------------------------- */
+
+static const int NSLOT = 3;
+
+struct PipeSlot {
+    hipStream_t stream;
+    hipEvent_t done;
+    uint8_t *d_in, *d_out, *d_aad;
+    ptls_hip_record_t *d_recs;
+    Chunk *d_chunks;
+    uint64_t *d_result;
+    /* pinned host staging for the slice's descriptors / chunks / results */
+    ptls_hip_record_t *h_recs;
+    Chunk *h_chunks;
+    bool busy;
+};
+
+struct st_ptls_hip_pipeline_t {
+    ptls_hip_engine_t *eng;
+    size_t slice_bytes, max_recs;
+    PipeSlot slot[NSLOT];
+};
+
+extern "C" ptls_hip_pipeline_t *ptls_hip_pipeline_new(ptls_hip_engine_t *eng, size_t slice_bytes)
+{
+    if (eng == nullptr || slice_bytes < (1u << 16)) {
+        fail(PTLS_HIP_EINVAL, "pipeline_new: bad arguments");
+        return nullptr;
+    }
+    DeviceGuard g(eng->device);
+    auto *p = new st_ptls_hip_pipeline_t();
+    p->eng = eng;
+    p->slice_bytes = slice_bytes;
+    p->max_recs = slice_bytes / 16 + 1;
+    bool ok = true;
+    for (auto &s : p->slot) {
+        ok = ok && hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking) == hipSuccess &&
+             hipEventCreateWithFlags(&s.done, hipEventDisableTiming) == hipSuccess &&
+             hipMalloc(&s.d_in, slice_bytes + 64) == hipSuccess && hipMalloc(&s.d_out, slice_bytes + 64) == hipSuccess &&
+             hipMalloc(&s.d_aad, slice_bytes / 4 + 64) == hipSuccess &&
+             hipMalloc(&s.d_recs, p->max_recs * sizeof(ptls_hip_record_t)) == hipSuccess &&
+             hipMalloc(&s.d_chunks, p->max_recs * sizeof(Chunk)) == hipSuccess &&
+             hipMalloc(&s.d_result, p->max_recs * sizeof(uint64_t)) == hipSuccess &&
+             hipHostMalloc(&s.h_recs, p->max_recs * sizeof(ptls_hip_record_t), hipHostMallocDefault) == hipSuccess &&
+             hipHostMalloc(&s.h_chunks, p->max_recs * sizeof(Chunk), hipHostMallocDefault) == hipSuccess;
+        s.busy = false;
+    }
+    if (!ok) {
+        fail(PTLS_HIP_ENOMEM, "pipeline_new: cannot allocate %d x %zu bytes of staging", NSLOT, slice_bytes);
+        ptls_hip_pipeline_free(p);
+        return nullptr;
+    }
+    return p;
+}
+
+extern "C" void ptls_hip_pipeline_free(ptls_hip_pipeline_t *p)
+{
+    if (p == nullptr)
+        return;
+    DeviceGuard g(p->eng->device);
+    for (auto &s : p->slot) {
+        if (s.stream != nullptr)
+            (void)hipStreamSynchronize(s.stream);
+        (void)hipFree(s.d_in);
+        (void)hipFree(s.d_out);
+        (void)hipFree(s.d_aad);
+        (void)hipFree(s.d_recs);
+        (void)hipFree(s.d_chunks);
+        (void)hipFree(s.d_result);
+        (void)hipHostFree(s.h_recs);
+        (void)hipHostFree(s.h_chunks);
+        if (s.done != nullptr)
+            (void)hipEventDestroy(s.done);
+        if (s.stream != nullptr)
+            (void)hipStreamDestroy(s.stream);
+    }
+    delete p;
+}
+
+extern "C" int ptls_hip_host_register(void *ptr, size_t len)
+{
+    HIP_TRY(hipHostRegister(ptr, len, hipHostRegisterDefault), PTLS_HIP_ENODEV);
+    return 0;
+}
+
+extern "C" int ptls_hip_host_unregister(void *ptr)
+{
+    HIP_TRY(hipHostUnregister(ptr), PTLS_HIP_ENODEV);
+    return 0;
+}
+
+/* byte span [lo, hi) of a field over records [a, b) */
+struct Span {
+    uint64_t lo, hi;
+};
+
+static int pipeline_run(ptls_hip_pipeline_t *p, ptls_hip_keyset_t *ks, const ptls_hip_record_t *recs, size_t n, const void *h_in,
+                        const void *h_aad, void *h_out, uint64_t *h_result, bool open)
+{
+    if (p == nullptr || ks == nullptr || ks->eng != p->eng || (n != 0 && (recs == nullptr || h_in == nullptr || h_out == nullptr)) ||
+        (open && h_result == nullptr))
+        return fail(PTLS_HIP_EINVAL, "pipeline seal/open: bad arguments");
+    DeviceGuard g(p->eng->device);
+    const int rounds = ks->key_size == 16 ? 10 : 14;
+    const size_t tag_in = open ? 16 : 0, tag_out = open ? 0 : 16;
+    const uint8_t *hin = static_cast<const uint8_t *>(h_in), *haad = static_cast<const uint8_t *>(h_aad);
+    uint8_t *hout = static_cast<uint8_t *>(h_out);
+    std::vector<Chunk> ch;
+    size_t i = 0;
+    int k = 0;
+    while (i < n) {
+        /* grow the slice while every span fits the staging buffers */
+        Span in{UINT64_MAX, 0}, out{UINT64_MAX, 0}, ad{UINT64_MAX, 0};
+        size_t j = i;
+        while (j < n && j - i < p->max_recs - 1) {
+            const ptls_hip_record_t &r = recs[j];
+            Span ni{std::min(in.lo, r.in_off), std::max(in.hi, r.in_off + r.len + tag_in)};
+            Span no{std::min(out.lo, r.out_off), std::max(out.hi, r.out_off + r.len + tag_out)};
+            Span na{std::min(ad.lo, r.aad_off), std::max(ad.hi, r.aad_off + r.aad_len)};
+            if (j > i && (ni.hi - ni.lo > p->slice_bytes || no.hi - no.lo > p->slice_bytes || na.hi - na.lo > p->slice_bytes / 4))
+                break;
+            in = ni;
+            out = no;
+            ad = na;
+            ++j;
+        }
+        if (in.hi - in.lo > p->slice_bytes || out.hi - out.lo > p->slice_bytes || ad.hi - ad.lo > p->slice_bytes / 4)
+            return fail(PTLS_HIP_EINVAL, "pipeline: record %zu does not fit a %zu-byte slice", i, p->slice_bytes);
+        PipeSlot &s = p->slot[k % NSLOT];
+        if (s.busy)
+            HIP_TRY(hipEventSynchronize(s.done), PTLS_HIP_ENODEV);
+        const size_t cnt = j - i;
+        /* slice-local descriptors keep the same relative 16-byte alignment as the caller's buffers */
+        const uint64_t in_base = in.lo & ~(uint64_t)15, out_base = out.lo & ~(uint64_t)15, aad_base = ad.lo & ~(uint64_t)15;
+        for (size_t t = 0; t < cnt; ++t) {
+            s.h_recs[t] = recs[i + t];
+            s.h_recs[t].in_off -= in_base;
+            s.h_recs[t].out_off -= out_base;
+            s.h_recs[t].aad_off -= aad_base;
+        }
+        int lanes;
+        {
+            std::vector<ptls_hip_record_t> tmp(s.h_recs, s.h_recs + cnt);
+            lanes = choose_lanes(tmp);
+        }
+        bool aligned;
+        build_chunks(s.h_recs, cnt, lanes, ch, aligned);
+        std::memcpy(s.h_chunks, ch.data(), ch.size() * sizeof(Chunk));
+        HIP_TRY(hipMemcpyAsync(s.d_recs, s.h_recs, cnt * sizeof(ptls_hip_record_t), hipMemcpyHostToDevice, s.stream),
+                PTLS_HIP_ENODEV);
+        HIP_TRY(hipMemcpyAsync(s.d_chunks, s.h_chunks, ch.size() * sizeof(Chunk), hipMemcpyHostToDevice, s.stream), PTLS_HIP_ENODEV);
+        HIP_TRY(hipMemcpyAsync(s.d_in + (in.lo - in_base), hin + in.lo, in.hi - in.lo, hipMemcpyHostToDevice, s.stream),
+                PTLS_HIP_ENODEV);
+        if (ad.hi > ad.lo)
+            HIP_TRY(hipMemcpyAsync(s.d_aad + (ad.lo - aad_base), haad + ad.lo, ad.hi - ad.lo, hipMemcpyHostToDevice, s.stream),
+                    PTLS_HIP_ENODEV);
+        KernelArgs a{};
+        a.recs = s.d_recs;
+        a.chunks = s.d_chunks;
+        a.nchunks = (uint32_t)ch.size();
+        a.in = s.d_in;
+        a.aad = s.d_aad;
+        a.out = s.d_out;
+        a.result = s.d_result;
+        a.slots = ks->d_slots;
+        a.basis = ks->d_basis;
+        a.t0 = p->eng->d_t0;
+        const unsigned grid = std::min<unsigned>((unsigned)ch.size(), (unsigned)p->eng->ncu);
+        const int e = launch_batch(lanes, rounds, open, grid, s.stream, a, aligned);
+        if (e != 0)
+            return fail(PTLS_HIP_ELAUNCH, "pipeline: kernel launch failed: %s", hipGetErrorString((hipError_t)e));
+        HIP_TRY(hipMemcpyAsync(hout + out.lo, s.d_out + (out.lo - out_base), out.hi - out.lo, hipMemcpyDeviceToHost, s.stream),
+                PTLS_HIP_ENODEV);
+        if (open) {
+            /* results come back in slice order; the caller's array is indexed like recs */
+            HIP_TRY(hipMemcpyAsync(h_result + i, s.d_result, cnt * sizeof(uint64_t), hipMemcpyDeviceToHost, s.stream),
+                    PTLS_HIP_ENODEV);
+        }
+        HIP_TRY(hipEventRecord(s.done, s.stream), PTLS_HIP_ENODEV);
+        s.busy = true;
+        i = j;
+        ++k;
+    }
+    for (auto &s : p->slot) {
+        if (s.busy)
+            HIP_TRY(hipEventSynchronize(s.done), PTLS_HIP_ENODEV);
+        s.busy = false;
+    }
+    return 0;
+}
+
+extern "C" int ptls_hip_pipeline_seal(ptls_hip_pipeline_t *p, ptls_hip_keyset_t *ks, const ptls_hip_record_t *recs, size_t n,
+                                      const void *h_in, const void *h_aad, void *h_out)
+{
+    return pipeline_run(p, ks, recs, n, h_in, h_aad, h_out, nullptr, false);
+}
+
+extern "C" int ptls_hip_pipeline_open(ptls_hip_pipeline_t *p, ptls_hip_keyset_t *ks, const ptls_hip_record_t *recs, size_t n,
+                                      const void *h_in, const void *h_aad, void *h_out, uint64_t *h_result)
+{
+    return pipeline_run(p, ks, recs, n, h_in, h_aad, h_out, h_result, true);
 }
 
 /* ---------------------------------------------------------------------------------------------- */

@@ -41,6 +41,12 @@ SIGNATURES = {
     "ptls_hip_aesgcm_seal_batch": (_i, [_vp, _vp, _vp, _vp, _vp, _vp]),
     "ptls_hip_aesgcm_open_batch": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "ptls_hip_fill_records": (_i, [_vp, _vp, _u64, _u64, _vp, _vp]),
+    "ptls_hip_pipeline_new": (_vp, [_vp, _sz]),
+    "ptls_hip_pipeline_free": (None, [_vp]),
+    "ptls_hip_pipeline_seal": (_i, [_vp, _vp, _vp, _sz, _vp, _vp, _vp]),
+    "ptls_hip_pipeline_open": (_i, [_vp, _vp, _vp, _sz, _vp, _vp, _vp, _vp]),
+    "ptls_hip_host_register": (_i, [_vp, _sz]),
+    "ptls_hip_host_unregister": (_i, [_vp]),
 }
 DATA_SYMBOLS = ("ptls_hip_aes128gcm", "ptls_hip_aes256gcm")
 
@@ -178,6 +184,31 @@ class Batch:
     def close(self):
         if self.ptr:
             lib().ptls_hip_batch_free(self.ptr)
+            self.ptr = None
+
+
+class Pipeline:
+    """host-resident seal/open: pinned H2D -> kernel -> D2H overlapped over three streams"""
+
+    def __init__(self, engine, slice_bytes=64 << 20):
+        self.engine = engine
+        self.ptr = lib().ptls_hip_pipeline_new(engine.ptr, slice_bytes)
+        if not self.ptr:
+            raise HipError(f"ptls_hip_pipeline_new: {last_error()}")
+
+    def seal(self, keyset, recs, h_in, h_aad, h_out):
+        recs = np.ascontiguousarray(recs, dtype=RECORD_DTYPE)
+        _check(lib().ptls_hip_pipeline_seal(self.ptr, keyset.ptr, recs.ctypes.data, len(recs), _ptr(h_in), _ptr(h_aad),
+                                            _ptr(h_out)), "pipeline_seal")
+
+    def open(self, keyset, recs, h_in, h_aad, h_out, h_result):
+        recs = np.ascontiguousarray(recs, dtype=RECORD_DTYPE)
+        _check(lib().ptls_hip_pipeline_open(self.ptr, keyset.ptr, recs.ctypes.data, len(recs), _ptr(h_in), _ptr(h_aad),
+                                            _ptr(h_out), _ptr(h_result)), "pipeline_open")
+
+    def close(self):
+        if self.ptr:
+            lib().ptls_hip_pipeline_free(self.ptr)
             self.ptr = None
 
 

@@ -119,6 +119,25 @@ int ptls_hip_aesgcm_open_batch(ptls_hip_batch_t *batch, ptls_hip_keyset_t *ks, c
                                uint64_t *result, void *stream);
 
 /* ------------------------------------------------------------------------------------------ *
+ * 2b. host-resident records (records arrive in and leave through host memory: socket buffers)  *
+ * ------------------------------------------------------------------------------------------ */
+
+/* A pipeline owns three device staging slots of `slice_bytes` each and three streams.  seal/open
+ * cut the record list into slices whose input / output / AAD byte spans fit a slot and overlap, per
+ * slice, H2D copy -> kernel -> D2H copy.  Offsets in `recs` are relative to the host buffers.  The
+ * call returns when every output byte (and result) is in host memory.  Host buffers should be
+ * pinned (hipHostMalloc'd, or ptls_hip_host_register'ed) for the copies to run asynchronously. */
+typedef struct st_ptls_hip_pipeline_t ptls_hip_pipeline_t;
+ptls_hip_pipeline_t *ptls_hip_pipeline_new(ptls_hip_engine_t *engine, size_t slice_bytes);
+void ptls_hip_pipeline_free(ptls_hip_pipeline_t *p);
+int ptls_hip_pipeline_seal(ptls_hip_pipeline_t *p, ptls_hip_keyset_t *ks, const ptls_hip_record_t *recs, size_t n,
+                           const void *h_in, const void *h_aad, void *h_out);
+int ptls_hip_pipeline_open(ptls_hip_pipeline_t *p, ptls_hip_keyset_t *ks, const ptls_hip_record_t *recs, size_t n,
+                           const void *h_in, const void *h_aad, void *h_out, uint64_t *h_result);
+int ptls_hip_host_register(void *ptr, size_t len);
+int ptls_hip_host_unregister(void *ptr);
+
+/* ------------------------------------------------------------------------------------------ *
  * 3. synthetic workload (bench / tests): the payload of descriptor i is the splitmix64 stream     *
  *    seeded with seed ^ g(i), written at buf + recs[i].in_off for recs[i].len     *
  *    bytes, where g(i) = index[i] if `index` (device array of n uint64) is given, else base + i.     *
