@@ -35,6 +35,14 @@ constexpr uint32_t LDS_BYTES = LDS_GTREE + 3 * LDS_TREE_STRIDE; /* 152 KiB of th
 #ifndef PREFETCH_BARRIER
 #define PREFETCH_BARRIER 1
 #endif
+#ifndef REMAT_LANE
+#define REMAT_LANE 0
+#endif
+#if REMAT_LANE /* measured: no gain over keeping the constants (same-box A/B), default off */
+#define LANE_FRESH gh_lane_fresh()
+#else
+#define LANE_FRESH gl
+#endif
 #ifndef ABLATE_AES
 #define ABLATE_AES 0
 #endif
@@ -243,26 +251,35 @@ struct GhLane {
     bool rot1, rot2;             /* word rotation by (lane >> 2) & 3 */
 };
 
-__device__ __forceinline__ GhLane gh_lane_init(int lane)
+__device__ __forceinline__ GhLane gh_lane_from(uint32_t lane)
 {
     GhLane g;
-    uint32_t lb[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        uint32_t v = 0;
-#pragma unroll
-        for (int m = 0; m < 4; ++m)
-            v |= (uint32_t)(((4 * i + m + lane) & 15) * 16) << (8 * m);
-        lb[i] = v;
-    }
-    g.lb0 = lb[0];
-    g.lb1 = lb[1];
-    g.lb2 = lb[2];
-    g.lb3 = lb[3];
+    /* byte m of lbI = ((lane + 4I + m) & 15) * 16: all four bytes at once (no carries: values < 256) */
+    const uint32_t base = lane * 0x01010101u + 0x03020100u;
+    g.lb0 = ((base + 0x00000000u) & 0x0f0f0f0fu) << 4;
+    g.lb1 = ((base + 0x04040404u) & 0x0f0f0f0fu) << 4;
+    g.lb2 = ((base + 0x08080808u) & 0x0f0f0f0fu) << 4;
+    g.lb3 = ((base + 0x0c0c0c0cu) & 0x0f0f0f0fu) << 4;
     g.shift = 8u * (lane & 3);
     g.rot1 = ((lane >> 2) & 1) != 0;
     g.rot2 = ((lane >> 3) & 1) != 0;
     return g;
+}
+
+__device__ __forceinline__ GhLane gh_lane_init(int lane)
+{
+    return gh_lane_from((uint32_t)lane);
+}
+
+/* Lane id through an opaque asm statement: the compiler can neither hoist nor keep the derived lane
+ * constants alive across the hot loop, so they are rematerialised (a few VALU) instead of being
+ * spilled to scratch, whose reload waits would also drain this wave's in-flight stores (vmcnt is
+ * in-order). */
+__device__ __forceinline__ GhLane gh_lane_fresh()
+{
+    uint32_t lane;
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lane));
+    return gh_lane_from(lane);
 }
 
 template <int K>
@@ -329,7 +346,7 @@ __device__ __forceinline__ V4 ld_basis(const uint32_t *b, int e)
 /* AES tables: row v = [T0[v] x 32 | rotl16(T0[v]) x 32] */
 __device__ void build_aes_tables(uint8_t *lds, const uint32_t *__restrict__ t0)
 {
-    for (int e = threadIdx.x; e < 256 * 32; e += WG_THREADS) {
+    for (int e = threadIdx.x; e < 256 * 32; e += blockDim.x) {
         const int v = e >> 5, s = e & 31; /* row v, lane slot s */
         const uint32_t t = t0[v];
         *reinterpret_cast<uint32_t *>(lds + LDS_AES + v * 256 + s * 4) = t;
@@ -342,7 +359,7 @@ __device__ void build_aes_tables(uint8_t *lds, const uint32_t *__restrict__ t0)
 __device__ void build_ghash_tables(uint8_t *lds, const uint32_t *__restrict__ basis, int log2g)
 {
     const uint32_t *bm = basis + log2g * 128 * 4;
-    for (int e = threadIdx.x; e < 16 * 256; e += WG_THREADS) {
+    for (int e = threadIdx.x; e < 16 * 256; e += blockDim.x) {
         const int p = e >> 8, v = e & 255;
         V4 acc = V4{0, 0, 0, 0};
 #pragma unroll
@@ -351,7 +368,7 @@ __device__ void build_ghash_tables(uint8_t *lds, const uint32_t *__restrict__ ba
                 acc = v4xor(acc, ld_basis(bm, 8 * p + 7 - t));
         lds128_store(lds, LDS_GMAIN + v * 256 + p * 16, acc);
     }
-    for (int e = threadIdx.x; e < 3 * 512; e += WG_THREADS) {
+    for (int e = threadIdx.x; e < 3 * 512; e += blockDim.x) {
         const int d = e >> 9, p = (e >> 4) & 31, v = e & 15;
         const int w = p >> 3, j = p & 7;
         const uint32_t *bt = basis + d * 128 * 4;
@@ -496,8 +513,8 @@ __device__ __forceinline__ V4 finish_elem(const Elem &e, V4 in_blk, V4 ks, const
 /* Pointers are separate __restrict__ kernel parameters (not a struct) so the compiler can prove that
  * the key slots, tables and descriptors are never written by the kernel and read them through the
  * scalar unit (s_load into SGPRs) instead of per-lane vector loads.  in/out may alias (in place). */
-template <int G, int ROUNDS, bool OPEN, bool ALIGNED>
-__global__ void __launch_bounds__(WG_THREADS)
+template <int G, int ROUNDS, bool OPEN, bool ALIGNED, int WGT>
+__global__ void __launch_bounds__(WGT)
     aesgcm_batch_kernel(const ptls_hip_record_t *__restrict__ recs, const Chunk *__restrict__ chunks, uint32_t nchunks,
                         const uint8_t *in, const uint8_t *__restrict__ aad, uint8_t *out, uint64_t *__restrict__ result,
                         const KeySlot *__restrict__ slots, const uint32_t *__restrict__ basis, const uint32_t *__restrict__ t0)
@@ -528,7 +545,7 @@ __global__ void __launch_bounds__(WG_THREADS)
         const uint32_t *__restrict__ rk = slot->rk;
         const int ntasks = (int)((ch.count + R - 1) / R);
 
-        for (int t = wave; t < ntasks; t += WAVES_PER_WG) {
+        for (int t = wave; t < ntasks; t += WGT / 64) {
             const uint32_t ridx = (uint32_t)t * R + grp;
             const bool valid = ridx < ch.count;
             const uint32_t rec_i = ch.first + (valid ? ridx : 0);
@@ -609,7 +626,7 @@ __global__ void __launch_bounds__(WG_THREADS)
                         /* the input is the ciphertext: hash it in the same iteration */
 #pragma unroll
                         for (int b = 0; b < KP; ++b)
-                            y = gh_mul_main(lds, gl, y, d[b]);
+                            y = gh_mul_main(lds, LANE_FRESH, y, d[b]);
 #pragma unroll
                         for (int b = 0; b < KP; ++b)
                             store_block<true>(dst + o + 16 * b * G, 16, v4xor(d[b], k[b]));
@@ -621,7 +638,7 @@ __global__ void __launch_bounds__(WG_THREADS)
 #if ABLATE_GHASH /* timing-only diagnostic build */
                                 y = v4xor(y, pend[b]);
 #else
-                                y = gh_mul_main(lds, gl, y, pend[b]);
+                                y = gh_mul_main(lds, LANE_FRESH, y, pend[b]);
 #endif
                         }
 #pragma unroll
@@ -683,19 +700,18 @@ __global__ void __launch_bounds__(WG_THREADS)
     }
 }
 
-#define INST(G, R, O, A)                                                                                                   \
-    template __global__ void aesgcm_batch_kernel<G, R, O, A>(const ptls_hip_record_t *__restrict__, const Chunk *__restrict__, \
-                                                             uint32_t, const uint8_t *, const uint8_t *__restrict__, uint8_t *,  \
-                                                             uint64_t *__restrict__, const KeySlot *__restrict__,                \
-                                                             const uint32_t *__restrict__, const uint32_t *__restrict__);
-#define INST_G(G)                                                                                                          \
-    INST(G, 10, false, true) INST(G, 10, true, true) INST(G, 14, false, true) INST(G, 14, true, true)                       \
-    INST(G, 10, false, false) INST(G, 10, true, false) INST(G, 14, false, false) INST(G, 14, true, false)
+#define INST(G, R, O, A, W)                                                                                                \
+    template __global__ void aesgcm_batch_kernel<G, R, O, A, W>(                                                           \
+        const ptls_hip_record_t *__restrict__, const Chunk *__restrict__, uint32_t, const uint8_t *, const uint8_t *__restrict__, \
+        uint8_t *, uint64_t *__restrict__, const KeySlot *__restrict__, const uint32_t *__restrict__, const uint32_t *__restrict__);
+#define INST_W(G, A, W) INST(G, 10, false, A, W) INST(G, 10, true, A, W) INST(G, 14, false, A, W) INST(G, 14, true, A, W)
+#define INST_G(G) INST_W(G, true, 512) INST_W(G, false, 512) INST_W(G, true, 1024) INST_W(G, false, 1024)
 INST_G(1)
 INST_G(2)
 INST_G(4)
 INST_G(8)
 #undef INST_G
+#undef INST_W
 #undef INST
 
 /* ======================================================================================= *
@@ -879,43 +895,49 @@ __global__ void fill_records_kernel(const ptls_hip_record_t *recs, uint32_t n, u
  * ======================================================================================= */
 namespace ptls_hip {
 
-template <int G, int R, bool O>
+template <int G, int R, bool O, int W>
 static hipError_t launch_one(unsigned grid, hipStream_t s, const KernelArgs &a, bool aligned)
 {
     if (aligned)
-        hipLaunchKernelGGL((aesgcm_batch_kernel<G, R, O, true>), dim3(grid), dim3(WG_THREADS), 0, s, a.recs, a.chunks, a.nchunks,
-                           a.in, a.aad, a.out, a.result, a.slots, a.basis, a.t0);
+        hipLaunchKernelGGL((aesgcm_batch_kernel<G, R, O, true, W>), dim3(grid), dim3(W), 0, s, a.recs, a.chunks, a.nchunks, a.in,
+                           a.aad, a.out, a.result, a.slots, a.basis, a.t0);
     else
-        hipLaunchKernelGGL((aesgcm_batch_kernel<G, R, O, false>), dim3(grid), dim3(WG_THREADS), 0, s, a.recs, a.chunks,
-                           a.nchunks, a.in, a.aad, a.out, a.result, a.slots, a.basis, a.t0);
+        hipLaunchKernelGGL((aesgcm_batch_kernel<G, R, O, false, W>), dim3(grid), dim3(W), 0, s, a.recs, a.chunks, a.nchunks,
+                           a.in, a.aad, a.out, a.result, a.slots, a.basis, a.t0);
     return hipGetLastError();
 }
 
+template <int G, int R, bool O>
+static hipError_t launch_w(int wg, unsigned grid, hipStream_t s, const KernelArgs &a, bool aligned)
+{
+    return wg == 512 ? launch_one<G, R, O, 512>(grid, s, a, aligned) : launch_one<G, R, O, 1024>(grid, s, a, aligned);
+}
+
 template <int G>
-static hipError_t launch_g(int rounds, bool open, unsigned grid, hipStream_t s, const KernelArgs &a, bool al)
+static hipError_t launch_g(int rounds, bool open, int wg, unsigned grid, hipStream_t s, const KernelArgs &a, bool al)
 {
     if (rounds == 10)
-        return open ? launch_one<G, 10, true>(grid, s, a, al) : launch_one<G, 10, false>(grid, s, a, al);
-    return open ? launch_one<G, 14, true>(grid, s, a, al) : launch_one<G, 14, false>(grid, s, a, al);
+        return open ? launch_w<G, 10, true>(wg, grid, s, a, al) : launch_w<G, 10, false>(wg, grid, s, a, al);
+    return open ? launch_w<G, 14, true>(wg, grid, s, a, al) : launch_w<G, 14, false>(wg, grid, s, a, al);
 }
 
 /* `aligned`: every record's in/out/aad offset and the three base pointers are 16-byte aligned */
-int launch_batch(int lanes, int rounds, bool open, unsigned grid, void *stream, const KernelArgs &a, bool aligned)
+int launch_batch(int lanes, int rounds, bool open, int wg, unsigned grid, void *stream, const KernelArgs &a, bool aligned)
 {
     hipStream_t s = static_cast<hipStream_t>(stream);
     hipError_t e;
     switch (lanes) {
     case 1:
-        e = launch_g<1>(rounds, open, grid, s, a, aligned);
+        e = launch_g<1>(rounds, open, wg, grid, s, a, aligned);
         break;
     case 2:
-        e = launch_g<2>(rounds, open, grid, s, a, aligned);
+        e = launch_g<2>(rounds, open, wg, grid, s, a, aligned);
         break;
     case 4:
-        e = launch_g<4>(rounds, open, grid, s, a, aligned);
+        e = launch_g<4>(rounds, open, wg, grid, s, a, aligned);
         break;
     case 8:
-        e = launch_g<8>(rounds, open, grid, s, a, aligned);
+        e = launch_g<8>(rounds, open, wg, grid, s, a, aligned);
         break;
     default:
         return (int)hipErrorInvalidValue;

@@ -118,6 +118,8 @@ struct st_ptls_hip_batch_t {
     Chunk *d_chunks;
     uint32_t nchunks;
     int lanes;      /* in use */
+    int wg;         /* threads per workgroup */
+    int forced_wg;  /* 0 = plan_wg */
     bool all_aligned; /* every descriptor's in/out/aad offset is a multiple of 16 */
     int auto_lanes; /* chosen from the record lengths */
     bool forced;
@@ -326,10 +328,24 @@ static int choose_lanes(const std::vector<ptls_hip_record_t> &recs)
 }
 
 /* chunk = run of records with one key slot, sized to keep all waves of a workgroup busy for a few tasks */
+static int plan_wg(const std::vector<Chunk> &ch, int lanes)
+{
+    /* Measured on MI355X (tools/tune.py, same-process sweep): 1024 threads (4 waves per SIMD) pays only for
+     * 8 lanes per record with >= 16 wave tasks per chunk (1M x 16 KiB: 926 vs 881 GiB/s seal); with 4 lanes
+     * (4M x 1350 B) 512 threads is faster (742 vs 705), and short key runs leave half of 16 waves idle. */
+    if (ch.empty() || lanes != 8)
+        return 512;
+    double recs = 0;
+    for (const auto &c : ch)
+        recs += c.count;
+    const double tasks = recs / (double)ch.size() / (64.0 / lanes);
+    return tasks >= 16.0 ? 1024 : 512;
+}
+
 static void build_chunks(const ptls_hip_record_t *recs, size_t n, int lanes, std::vector<Chunk> &ch, bool &all_aligned)
 {
     const uint32_t per_task = 64u / (uint32_t)lanes;
-    const uint32_t max_chunk = per_task * WAVES_PER_WG * 2;
+    const uint32_t max_chunk = per_task * (WG_MAX / 64) * 2;
     ch.clear();
     all_aligned = true;
     size_t i = 0;
@@ -354,6 +370,7 @@ static int plan_chunks(ptls_hip_batch_t *b)
 {
     std::vector<Chunk> ch;
     build_chunks(b->h_recs.data(), b->n, b->lanes, ch, b->all_aligned);
+    b->wg = b->forced_wg ? b->forced_wg : plan_wg(ch, b->lanes);
     if (b->d_chunks != nullptr)
         (void)hipFree(b->d_chunks);
     b->d_chunks = nullptr;
@@ -427,6 +444,20 @@ extern "C" int ptls_hip_batch_lanes(ptls_hip_batch_t *b)
     return b->lanes;
 }
 
+extern "C" int ptls_hip_batch_set_workgroup(ptls_hip_batch_t *b, int threads)
+{
+    if (b == nullptr || !(threads == 0 || threads == 512 || threads == 1024))
+        return fail(PTLS_HIP_EINVAL, "batch_set_workgroup: threads must be 0, 512 or 1024");
+    DeviceGuard g(b->eng->device);
+    b->forced_wg = threads;
+    return plan_chunks(b);
+}
+
+extern "C" int ptls_hip_batch_workgroup(ptls_hip_batch_t *b)
+{
+    return b->wg;
+}
+
 static int run_batch(ptls_hip_batch_t *b, ptls_hip_keyset_t *ks, const void *in, const void *aad, void *out, uint64_t *result,
                      void *stream, bool open)
 {
@@ -453,7 +484,7 @@ static int run_batch(ptls_hip_batch_t *b, ptls_hip_keyset_t *ks, const void *in,
     const bool aligned = base_aligned && b->all_aligned;
     const unsigned grid = std::min<unsigned>(b->nchunks, (unsigned)b->eng->ncu);
     const int rounds = ks->key_size == 16 ? 10 : 14;
-    int e = launch_batch(b->lanes, rounds, open, grid, stream, a, aligned);
+    int e = launch_batch(b->lanes, rounds, open, b->wg, grid, stream, a, aligned);
     if (e != 0)
         return fail(PTLS_HIP_ELAUNCH, "kernel launch failed: %s", hipGetErrorString((hipError_t)e));
     return 0;
@@ -656,7 +687,7 @@ static int pipeline_run(ptls_hip_pipeline_t *p, ptls_hip_keyset_t *ks, const ptl
         a.basis = ks->d_basis;
         a.t0 = p->eng->d_t0;
         const unsigned grid = std::min<unsigned>((unsigned)ch.size(), (unsigned)p->eng->ncu);
-        const int e = launch_batch(lanes, rounds, open, grid, s.stream, a, aligned);
+        const int e = launch_batch(lanes, rounds, open, plan_wg(ch, lanes), grid, s.stream, a, aligned);
         if (e != 0)
             return fail(PTLS_HIP_ELAUNCH, "pipeline: kernel launch failed: %s", hipGetErrorString((hipError_t)e));
         HIP_TRY(hipMemcpyAsync(hout + out.lo, s.d_out + (out.lo - out_base), out.hi - out.lo, hipMemcpyDeviceToHost, s.stream),
@@ -816,7 +847,7 @@ static uint64_t plugin_run(hip_aead_state *st, bool open, void *output, const vo
     a.t0 = st->eng->d_t0;
     const size_t n = (aadlen + 15) / 16 + (len + 15) / 16 + 1;
     const int lanes = n >= 128 ? 8 : n >= 48 ? 4 : n >= 16 ? 2 : 1;
-    int e = launch_batch(lanes, st->ks->key_size == 16 ? 10 : 14, open, 1, st->stream, a, true);
+    int e = launch_batch(lanes, st->ks->key_size == 16 ? 10 : 14, open, 512, 1, st->stream, a, true);
     if (e != 0) {
         g_err = hipGetErrorString((hipError_t)e);
         plugin_die("launch");

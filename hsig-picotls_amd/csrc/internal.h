@@ -18,11 +18,9 @@ namespace ptls_hip {
 
 constexpr int NPOW = 4;          /* H^1, H^2, H^4, H^8 */
 constexpr int MAX_LANES = 8;     /* lanes per record (G) supported: 1, 2, 4, 8 */
-#ifndef PTLS_HIP_WG_THREADS
-#define PTLS_HIP_WG_THREADS 1024
-#endif
-constexpr int WG_THREADS = PTLS_HIP_WG_THREADS; /* one workgroup per CU (LDS-limited): 16 waves = 4 per SIMD */
-constexpr int WAVES_PER_WG = WG_THREADS / 64;
+/* one workgroup per CU (LDS-limited).  1024 threads (4 waves per SIMD) unless key runs are too short to
+ * give every wave work, then 512 (chosen per batch by the planner, engine.cpp:plan_wg) */
+constexpr int WG_MAX = 1024;
 
 struct KeySlot {
     uint32_t rk[60];      /* AES round keys, raw byte order as little-endian words (11 or 15 used) */
@@ -55,7 +53,7 @@ struct KernelArgs {
 };
 
 /* host-side launchers, defined next to the kernels (aesgcm_kernels.hip) */
-int launch_batch(int lanes, int rounds, bool open, unsigned grid, void *stream, const KernelArgs &a, bool base_aligned);
+int launch_batch(int lanes, int rounds, bool open, int wg, unsigned grid, void *stream, const KernelArgs &a, bool aligned);
 int launch_keysetup(KeySlot *slots, uint32_t *basis, const uint8_t *keys, const uint8_t *ivs, uint32_t first, uint32_t count,
                     int key_size, const uint32_t *t0, void *stream);
 int launch_fill(const ptls_hip_record_t *recs, uint32_t n, uint8_t *buf, uint64_t seed, uint64_t index_base,

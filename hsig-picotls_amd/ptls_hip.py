@@ -38,6 +38,8 @@ SIGNATURES = {
     "ptls_hip_batch_count": (_sz, [_vp]),
     "ptls_hip_batch_set_lanes": (_i, [_vp, _i]),
     "ptls_hip_batch_lanes": (_i, [_vp]),
+    "ptls_hip_batch_set_workgroup": (_i, [_vp, _i]),
+    "ptls_hip_batch_workgroup": (_i, [_vp]),
     "ptls_hip_aesgcm_seal_batch": (_i, [_vp, _vp, _vp, _vp, _vp, _vp]),
     "ptls_hip_aesgcm_open_batch": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "ptls_hip_fill_records": (_i, [_vp, _vp, _u64, _u64, _vp, _vp]),
@@ -167,6 +169,13 @@ class Batch:
 
     def set_lanes(self, lanes):
         _check(lib().ptls_hip_batch_set_lanes(self.ptr, lanes), "batch_set_lanes")
+
+    @property
+    def workgroup(self):
+        return lib().ptls_hip_batch_workgroup(self.ptr)
+
+    def set_workgroup(self, threads):
+        _check(lib().ptls_hip_batch_set_workgroup(self.ptr, threads), "batch_set_workgroup")
 
     def seal(self, keyset, inp, aad, out, stream=None):
         _check(lib().ptls_hip_aesgcm_seal_batch(self.ptr, keyset.ptr, _ptr(inp), _ptr(aad), _ptr(out), _stream(stream)),

@@ -111,6 +111,9 @@ size_t ptls_hip_batch_count(ptls_hip_batch_t *batch);
 /* lanes cooperating on one record (1, 2, 4 or 8); 0 = automatic (default).  For tuning and tests. */
 int ptls_hip_batch_set_lanes(ptls_hip_batch_t *batch, int lanes);
 int ptls_hip_batch_lanes(ptls_hip_batch_t *batch);
+/* threads per workgroup of the batch kernel (512 or 1024); 0 = automatic (default).  For tuning. */
+int ptls_hip_batch_set_workgroup(ptls_hip_batch_t *batch, int threads);
+int ptls_hip_batch_workgroup(ptls_hip_batch_t *batch);
 
 /* Asynchronous on `stream`; all pointers are device (or device-accessible) memory. */
 int ptls_hip_aesgcm_seal_batch(ptls_hip_batch_t *batch, ptls_hip_keyset_t *ks, const void *in, const void *aad, void *out,
