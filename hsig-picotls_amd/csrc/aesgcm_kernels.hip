@@ -35,6 +35,9 @@ constexpr uint32_t LDS_BYTES = LDS_GTREE + 3 * LDS_TREE_STRIDE; /* 152 KiB of th
 #ifndef PREFETCH_BARRIER
 #define PREFETCH_BARRIER 1
 #endif
+#ifndef CTR_SHORTCUT
+#define CTR_SHORTCUT 1
+#endif
 #ifndef REMAT_LANE
 #define REMAT_LANE 0
 #endif
@@ -199,6 +202,91 @@ __device__ __forceinline__ void aes_encrypt2(const uint8_t *lds, uint32_t lb, co
     const uint32_t v3 = aes_col_last(lds, lb, u.w3, u.w0, u.w1, u.w2, k3);
     s = V4{t0, t1, t2, t3};
     u = V4{v0, v1, v2, v3};
+}
+
+/* single table lookups: T0, T1 = rotl8(T0), T2 = rotl16(T0), T3 = rotl8(T2), byte K of x */
+template <int K>
+__device__ __forceinline__ uint32_t lT0(const uint8_t *lds, uint32_t x, uint32_t lb)
+{
+    return lds32(lds, aes_addr<K>(x, lb));
+}
+template <int K>
+__device__ __forceinline__ uint32_t lT2(const uint8_t *lds, uint32_t x, uint32_t lb)
+{
+    return lds32(lds, 128 + aes_addr<K>(x, lb));
+}
+
+/* Counter-mode shortcut (rounds 1-2).  For a record whose block counters stay below 2^16, the counter
+ * word is 00 00 hi lo and everything else of the AES input is fixed per record, so after round 1 only
+ * state columns 0 and 1 vary (they take counter bytes 15 and 14) and after round 2 every column is
+ * (constant ^ two lookups).  CtrConst holds those per-record constants. */
+struct CtrConst {
+    uint32_t k10, k11; /* round-1 columns 0, 1 without their counter-byte term */
+    uint32_t k20, k21, k22, k23; /* round-2 columns without the terms from round-1 columns 0 and 1 */
+    uint32_t r03;      /* round key 0 word 3 (the counter word's whitening) */
+};
+
+__device__ __forceinline__ CtrConst ctr_const(const uint8_t *lds, uint32_t lb, const uint32_t *__restrict__ rk, uint32_t n0,
+                                              uint32_t n1, uint32_t n2)
+{
+    const uint32_t s0 = n0 ^ rk[0], s1 = n1 ^ rk[1], s2 = n2 ^ rk[2], s3 = rk[3]; /* counter bytes 12,13 = 0 */
+    CtrConst c;
+    c.r03 = rk[3];
+    /* round 1: t_c = T0[s_c.b0] ^ T1[s_{c+1}.b1] ^ T2[s_{c+2}.b2] ^ T3[s_{c+3}.b3] ^ rk1_c */
+    c.k10 = lT0<0>(lds, s0, lb) ^ rotl8(lT0<1>(lds, s1, lb)) ^ lT2<2>(lds, s2, lb) ^ rk[4]; /* - T3[s3.b3] */
+    c.k11 = lT0<0>(lds, s1, lb) ^ rotl8(lT0<1>(lds, s2, lb)) ^ rotl8(lT2<3>(lds, s0, lb)) ^ rk[5]; /* - T2[s3.b2] */
+    const uint32_t t2 = lT0<0>(lds, s2, lb) ^ rotl8(lT0<1>(lds, s3, lb)) ^ lT2<2>(lds, s0, lb) ^ rotl8(lT2<3>(lds, s1, lb)) ^ rk[6];
+    const uint32_t t3 = lT0<0>(lds, s3, lb) ^ rotl8(lT0<1>(lds, s0, lb)) ^ lT2<2>(lds, s1, lb) ^ rotl8(lT2<3>(lds, s2, lb)) ^ rk[7];
+    /* round 2 constant parts (terms reading t2, t3) */
+    c.k20 = lT2<2>(lds, t2, lb) ^ rotl8(lT2<3>(lds, t3, lb)) ^ rk[8];
+    c.k21 = rotl8(lT0<1>(lds, t2, lb)) ^ lT2<2>(lds, t3, lb) ^ rk[9];
+    c.k22 = lT0<0>(lds, t2, lb) ^ rotl8(lT0<1>(lds, t3, lb)) ^ rk[10];
+    c.k23 = lT0<0>(lds, t3, lb) ^ rotl8(lT2<3>(lds, t2, lb)) ^ rk[11];
+    return c;
+}
+
+/* AES of K counter blocks (n0, n1, n2, bswap(ctr_b)) with ctr_b < 2^16, using the per-record constants */
+template <int ROUNDS, int K>
+__device__ __forceinline__ void aes_ctr_n(const uint8_t *lds, uint32_t lb, const uint32_t *__restrict__ rk, const CtrConst &cc,
+                                          const uint32_t (&ctrw)[K], V4 (&s)[K])
+{
+#pragma unroll
+    for (int b = 0; b < K; ++b) {
+        const uint32_t x3 = ctrw[b] ^ cc.r03;                                     /* state column 3 after round 0 */
+        const uint32_t t0 = cc.k10 ^ rotl8(lT2<3>(lds, x3, lb));                  /* + T3[x3.b3] */
+        const uint32_t t1 = cc.k11 ^ lT2<2>(lds, x3, lb);                         /* + T2[x3.b2] */
+        s[b].w0 = xor3(cc.k20, lT0<0>(lds, t0, lb), rotl8(lT0<1>(lds, t1, lb)));  /* T0[t0.b0] ^ T1[t1.b1] */
+        s[b].w1 = xor3(cc.k21, lT0<0>(lds, t1, lb), rotl8(lT2<3>(lds, t0, lb)));  /* T0[t1.b0] ^ T3[t0.b3] */
+        s[b].w2 = xor3(cc.k22, lT2<2>(lds, t0, lb), rotl8(lT2<3>(lds, t1, lb)));  /* T2[t0.b2] ^ T3[t1.b3] */
+        s[b].w3 = xor3(cc.k23, rotl8(lT0<1>(lds, t0, lb)), lT2<2>(lds, t1, lb));  /* T1[t0.b1] ^ T2[t1.b2] */
+    }
+#pragma unroll
+    for (int r = 3; r < ROUNDS; ++r) {
+        const uint32_t k0 = rk[4 * r + 0], k1 = rk[4 * r + 1], k2 = rk[4 * r + 2], k3 = rk[4 * r + 3];
+        V4 t[K];
+#pragma unroll
+        for (int b = 0; b < K; ++b) {
+            t[b].w0 = aes_col(lds, lb, s[b].w0, s[b].w1, s[b].w2, s[b].w3, k0);
+            t[b].w1 = aes_col(lds, lb, s[b].w1, s[b].w2, s[b].w3, s[b].w0, k1);
+            t[b].w2 = aes_col(lds, lb, s[b].w2, s[b].w3, s[b].w0, s[b].w1, k2);
+            t[b].w3 = aes_col(lds, lb, s[b].w3, s[b].w0, s[b].w1, s[b].w2, k3);
+        }
+#pragma unroll
+        for (int b = 0; b < K; ++b)
+            s[b] = t[b];
+    }
+    const uint32_t k0 = rk[4 * ROUNDS + 0], k1 = rk[4 * ROUNDS + 1], k2 = rk[4 * ROUNDS + 2], k3 = rk[4 * ROUNDS + 3];
+    V4 t[K];
+#pragma unroll
+    for (int b = 0; b < K; ++b) {
+        t[b].w0 = aes_col_last(lds, lb, s[b].w0, s[b].w1, s[b].w2, s[b].w3, k0);
+        t[b].w1 = aes_col_last(lds, lb, s[b].w1, s[b].w2, s[b].w3, s[b].w0, k1);
+        t[b].w2 = aes_col_last(lds, lb, s[b].w2, s[b].w3, s[b].w0, s[b].w1, k2);
+        t[b].w3 = aes_col_last(lds, lb, s[b].w3, s[b].w0, s[b].w1, s[b].w2, k3);
+    }
+#pragma unroll
+    for (int b = 0; b < K; ++b)
+        s[b] = t[b];
 }
 
 /* K independent blocks, round-interleaved */
@@ -515,7 +603,8 @@ __device__ __forceinline__ V4 finish_elem(const Elem &e, V4 in_blk, V4 ks, const
  * scalar unit (s_load into SGPRs) instead of per-lane vector loads.  in/out may alias (in place). */
 template <int G, int ROUNDS, bool OPEN, bool ALIGNED, int WGT>
 __global__ void __launch_bounds__(WGT)
-    aesgcm_batch_kernel(const ptls_hip_record_t *__restrict__ recs, const Chunk *__restrict__ chunks, uint32_t nchunks,
+    aesgcm_batch_kernel(const ptls_hip_record_t *__restrict__ recs, const uint32_t *__restrict__ order,
+                        const Chunk *__restrict__ chunks, uint32_t nchunks,
                         const uint8_t *in, const uint8_t *__restrict__ aad, uint8_t *out, uint64_t *__restrict__ result,
                         const KeySlot *__restrict__ slots, const uint32_t *__restrict__ basis, const uint32_t *__restrict__ t0)
 {
@@ -548,7 +637,7 @@ __global__ void __launch_bounds__(WGT)
         for (int t = wave; t < ntasks; t += WGT / 64) {
             const uint32_t ridx = (uint32_t)t * R + grp;
             const bool valid = ridx < ch.count;
-            const uint32_t rec_i = ch.first + (valid ? ridx : 0);
+            const uint32_t rec_i = order[ch.first + (valid ? ridx : 0)];
             const ptls_hip_record_t rec = recs[rec_i];
             const int L = valid ? (int)rec.len : 0;
             const int A = valid ? (int)rec.aad_len : 0;
@@ -586,7 +675,9 @@ __global__ void __launch_bounds__(WGT)
             constexpr int KP = PURE_BLOCKS;
             const int nf = L >> 4;
             const int my_mlo = na > i0 ? (na - i0 + G - 1) >> LOG2G : 0;
-            const int my_mhi = (ALIGNED && valid && na + nf - 1 - i0 >= 0) ? ((na + nf - 1 - i0) >> LOG2G) + 1 : 0;
+            /* full blocks only, and (for the counter-mode shortcut) block counters c + 2 < 2^16 */
+            const int lastc = min(nf, 65534) - 1; /* last data block index allowed in the pure stretch */
+            const int my_mhi = (ALIGNED && valid && na + lastc - i0 >= 0) ? ((na + lastc - i0) >> LOG2G) + 1 : 0;
             const int pm0 = wave_max(my_mlo);
             const int pm_hi = -wave_max(-my_mhi);
             const int npure = pm_hi > pm0 ? (pm_hi - pm0) / KP : 0;
@@ -598,6 +689,9 @@ __global__ void __launch_bounds__(WGT)
                 const uint8_t *src = in_p + 16 * (size_t)(i0 - na + pm0 * G);
                 uint8_t *dst = out_p + 16 * (size_t)(i0 - na + pm0 * G);
                 const uint32_t cbase = (uint32_t)(i0 - na + pm0 * G) + 2u;
+#if CTR_SHORTCUT
+                const CtrConst cc = ctr_const(lds, lb_aes, rk, n0, n1, n2);
+#endif
                 V4 pend[KP], bufA[KP], bufB[KP];
                 /* ping-pong prefetch: iteration `it` consumes the buffer loaded one iteration earlier and refills
                  * the other one for it + 1 (clamped to the last iteration so the body stays branch-free).  Two
@@ -610,15 +704,19 @@ __global__ void __launch_bounds__(WGT)
                     const size_t o = (size_t)(it * KP * G) * 16;
                     const size_t on = (size_t)(min(it + 1, npure - 1) * KP * G) * 16;
                     V4 k[KP];
+                    uint32_t cw[KP];
 #pragma unroll
                     for (int b = 0; b < KP; ++b) {
                         dn[b] = load_block<true>(src + on + 16 * b * G, 16);
-                        k[b] = V4{n0, n1, n2, bswap32(cbase + (uint32_t)((it * KP + b) * G))};
+                        cw[b] = bswap32(cbase + (uint32_t)((it * KP + b) * G));
+                        k[b] = V4{n0, n1, n2, cw[b]};
                     }
 #if PREFETCH_BARRIER
                     __builtin_amdgcn_sched_barrier(0); /* keep the prefetch at the top of the iteration */
 #endif
 #if ABLATE_AES /* timing-only diagnostic build: keystream = counter block */
+#elif CTR_SHORTCUT
+                    aes_ctr_n<ROUNDS, KP>(lds, lb_aes, rk, cc, cw, k);
 #else
                     aes_encrypt_n<ROUNDS, KP>(lds, lb_aes, rk, k);
 #endif
@@ -702,7 +800,8 @@ __global__ void __launch_bounds__(WGT)
 
 #define INST(G, R, O, A, W)                                                                                                \
     template __global__ void aesgcm_batch_kernel<G, R, O, A, W>(                                                           \
-        const ptls_hip_record_t *__restrict__, const Chunk *__restrict__, uint32_t, const uint8_t *, const uint8_t *__restrict__, \
+        const ptls_hip_record_t *__restrict__, const uint32_t *__restrict__, const Chunk *__restrict__, uint32_t,              \
+        const uint8_t *, const uint8_t *__restrict__,                                                                      \
         uint8_t *, uint64_t *__restrict__, const KeySlot *__restrict__, const uint32_t *__restrict__, const uint32_t *__restrict__);
 #define INST_W(G, A, W) INST(G, 10, false, A, W) INST(G, 10, true, A, W) INST(G, 14, false, A, W) INST(G, 14, true, A, W)
 #define INST_G(G) INST_W(G, true, 512) INST_W(G, false, 512) INST_W(G, true, 1024) INST_W(G, false, 1024)
@@ -899,11 +998,11 @@ template <int G, int R, bool O, int W>
 static hipError_t launch_one(unsigned grid, hipStream_t s, const KernelArgs &a, bool aligned)
 {
     if (aligned)
-        hipLaunchKernelGGL((aesgcm_batch_kernel<G, R, O, true, W>), dim3(grid), dim3(W), 0, s, a.recs, a.chunks, a.nchunks, a.in,
-                           a.aad, a.out, a.result, a.slots, a.basis, a.t0);
+        hipLaunchKernelGGL((aesgcm_batch_kernel<G, R, O, true, W>), dim3(grid), dim3(W), 0, s, a.recs, a.order, a.chunks,
+                           a.nchunks, a.in, a.aad, a.out, a.result, a.slots, a.basis, a.t0);
     else
-        hipLaunchKernelGGL((aesgcm_batch_kernel<G, R, O, false, W>), dim3(grid), dim3(W), 0, s, a.recs, a.chunks, a.nchunks,
-                           a.in, a.aad, a.out, a.result, a.slots, a.basis, a.t0);
+        hipLaunchKernelGGL((aesgcm_batch_kernel<G, R, O, false, W>), dim3(grid), dim3(W), 0, s, a.recs, a.order, a.chunks,
+                           a.nchunks, a.in, a.aad, a.out, a.result, a.slots, a.basis, a.t0);
     return hipGetLastError();
 }
 

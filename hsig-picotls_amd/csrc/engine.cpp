@@ -116,6 +116,7 @@ struct st_ptls_hip_batch_t {
     ptls_hip_record_t *d_recs;
     std::vector<ptls_hip_record_t> h_recs;
     Chunk *d_chunks;
+    uint32_t *d_order;
     uint32_t nchunks;
     int lanes;      /* in use */
     int wg;         /* threads per workgroup */
@@ -327,26 +328,26 @@ static int choose_lanes(const std::vector<ptls_hip_record_t> &recs)
     return mean >= 128 ? 8 : mean >= 48 ? 4 : mean >= 16 ? 2 : 1;
 }
 
-/* chunk = run of records with one key slot, sized to keep all waves of a workgroup busy for a few tasks */
 static int plan_wg(const std::vector<Chunk> &ch, int lanes)
 {
-    /* Measured on MI355X (tools/tune.py, same-process sweep): 1024 threads (4 waves per SIMD) pays only for
-     * 8 lanes per record with >= 16 wave tasks per chunk (1M x 16 KiB: 926 vs 881 GiB/s seal); with 4 lanes
-     * (4M x 1350 B) 512 threads is faster (742 vs 705), and short key runs leave half of 16 waves idle. */
-    if (ch.empty() || lanes != 8)
-        return 512;
-    double recs = 0;
-    for (const auto &c : ch)
-        recs += c.count;
-    const double tasks = recs / (double)ch.size() / (64.0 / lanes);
-    return tasks >= 16.0 ? 1024 : 512;
+    /* Measured on MI355X (tools/tune.py, same-process sweep): with the counter-mode AES shortcut, 512
+     * threads (2 waves per SIMD, 256-VGPR budget, no spills) is as fast or faster than 1024 for every
+     * BASELINE shape (1M x 16 KiB: 1011 vs 995 GiB/s seal; 4M x 1350 B: 821 vs 721; 64K keys: 284 vs 201). */
+    (void)ch;
+    (void)lanes;
+    return 512;
 }
 
-static void build_chunks(const ptls_hip_record_t *recs, size_t n, int lanes, std::vector<Chunk> &ch, bool &all_aligned)
+/* chunk = run of records with one key slot, sized to keep all waves of a workgroup busy for a few tasks.
+ * Inside a chunk the records are ordered by decreasing length, so the 64/lanes records a wave processes
+ * together have similar lengths (their branch-free full-block stretch is limited by the shortest). */
+static void build_chunks(const ptls_hip_record_t *recs, size_t n, int lanes, std::vector<Chunk> &ch, std::vector<uint32_t> &order,
+                         bool &all_aligned)
 {
     const uint32_t per_task = 64u / (uint32_t)lanes;
     const uint32_t max_chunk = per_task * (WG_MAX / 64) * 2;
     ch.clear();
+    order.resize(n);
     all_aligned = true;
     size_t i = 0;
     while (i < n) {
@@ -355,12 +356,19 @@ static void build_chunks(const ptls_hip_record_t *recs, size_t n, int lanes, std
         c.key = recs[i].key;
         c.count = 0;
         c.flags = 1;
+        bool sorted = true;
         while (i < n && recs[i].key == c.key && c.count < max_chunk) {
             if (((recs[i].in_off | recs[i].out_off | recs[i].aad_off) & 15) != 0)
                 c.flags = 0;
+            if (c.count != 0 && recs[i].len > recs[i - 1].len)
+                sorted = false;
+            order[i] = (uint32_t)i;
             ++c.count;
             ++i;
         }
+        if (!sorted)
+            std::stable_sort(order.begin() + c.first, order.begin() + c.first + c.count,
+                             [&](uint32_t x, uint32_t y) { return recs[x].len > recs[y].len; });
         all_aligned = all_aligned && (c.flags & 1u);
         ch.push_back(c);
     }
@@ -369,16 +377,22 @@ static void build_chunks(const ptls_hip_record_t *recs, size_t n, int lanes, std
 static int plan_chunks(ptls_hip_batch_t *b)
 {
     std::vector<Chunk> ch;
-    build_chunks(b->h_recs.data(), b->n, b->lanes, ch, b->all_aligned);
+    std::vector<uint32_t> order;
+    build_chunks(b->h_recs.data(), b->n, b->lanes, ch, order, b->all_aligned);
     b->wg = b->forced_wg ? b->forced_wg : plan_wg(ch, b->lanes);
     if (b->d_chunks != nullptr)
         (void)hipFree(b->d_chunks);
+    if (b->d_order != nullptr)
+        (void)hipFree(b->d_order);
     b->d_chunks = nullptr;
+    b->d_order = nullptr;
     b->nchunks = (uint32_t)ch.size();
     if (ch.empty())
         return 0;
     HIP_TRY(hipMalloc(&b->d_chunks, ch.size() * sizeof(Chunk)), PTLS_HIP_ENOMEM);
     HIP_TRY(hipMemcpy(b->d_chunks, ch.data(), ch.size() * sizeof(Chunk), hipMemcpyHostToDevice), PTLS_HIP_ENODEV);
+    HIP_TRY(hipMalloc(&b->d_order, order.size() * sizeof(uint32_t)), PTLS_HIP_ENOMEM);
+    HIP_TRY(hipMemcpy(b->d_order, order.data(), order.size() * sizeof(uint32_t), hipMemcpyHostToDevice), PTLS_HIP_ENODEV);
     return 0;
 }
 
@@ -405,8 +419,7 @@ extern "C" ptls_hip_batch_t *ptls_hip_batch_new(ptls_hip_engine_t *eng, const pt
         }
     }
     if (plan_chunks(b) != 0) {
-        (void)hipFree(b->d_recs);
-        delete b;
+        ptls_hip_batch_free(b);
         return nullptr;
     }
     return b;
@@ -419,6 +432,7 @@ extern "C" void ptls_hip_batch_free(ptls_hip_batch_t *b)
     DeviceGuard g(b->eng->device);
     (void)hipFree(b->d_recs);
     (void)hipFree(b->d_chunks);
+    (void)hipFree(b->d_order);
     delete b;
 }
 
@@ -470,6 +484,7 @@ static int run_batch(ptls_hip_batch_t *b, ptls_hip_keyset_t *ks, const void *in,
     DeviceGuard g(b->eng->device);
     KernelArgs a{};
     a.recs = b->d_recs;
+    a.order = b->d_order;
     a.chunks = b->d_chunks;
     a.nchunks = b->nchunks;
     a.in = static_cast<const uint8_t *>(in);
@@ -529,10 +544,12 @@ struct PipeSlot {
     uint8_t *d_in, *d_out, *d_aad;
     ptls_hip_record_t *d_recs;
     Chunk *d_chunks;
+    uint32_t *d_order;
     uint64_t *d_result;
-    /* pinned host staging for the slice's descriptors / chunks / results */
+    /* pinned host staging for the slice's descriptors / chunks / record order */
     ptls_hip_record_t *h_recs;
     Chunk *h_chunks;
+    uint32_t *h_order;
     bool busy;
 };
 
@@ -561,6 +578,8 @@ extern "C" ptls_hip_pipeline_t *ptls_hip_pipeline_new(ptls_hip_engine_t *eng, si
              hipMalloc(&s.d_aad, slice_bytes / 4 + 64) == hipSuccess &&
              hipMalloc(&s.d_recs, p->max_recs * sizeof(ptls_hip_record_t)) == hipSuccess &&
              hipMalloc(&s.d_chunks, p->max_recs * sizeof(Chunk)) == hipSuccess &&
+             hipMalloc(&s.d_order, p->max_recs * sizeof(uint32_t)) == hipSuccess &&
+             hipHostMalloc(&s.h_order, p->max_recs * sizeof(uint32_t), hipHostMallocDefault) == hipSuccess &&
              hipMalloc(&s.d_result, p->max_recs * sizeof(uint64_t)) == hipSuccess &&
              hipHostMalloc(&s.h_recs, p->max_recs * sizeof(ptls_hip_record_t), hipHostMallocDefault) == hipSuccess &&
              hipHostMalloc(&s.h_chunks, p->max_recs * sizeof(Chunk), hipHostMallocDefault) == hipSuccess;
@@ -587,6 +606,8 @@ extern "C" void ptls_hip_pipeline_free(ptls_hip_pipeline_t *p)
         (void)hipFree(s.d_aad);
         (void)hipFree(s.d_recs);
         (void)hipFree(s.d_chunks);
+        (void)hipFree(s.d_order);
+        (void)hipHostFree(s.h_order);
         (void)hipFree(s.d_result);
         (void)hipHostFree(s.h_recs);
         (void)hipHostFree(s.h_chunks);
@@ -627,6 +648,7 @@ static int pipeline_run(ptls_hip_pipeline_t *p, ptls_hip_keyset_t *ks, const ptl
     const uint8_t *hin = static_cast<const uint8_t *>(h_in), *haad = static_cast<const uint8_t *>(h_aad);
     uint8_t *hout = static_cast<uint8_t *>(h_out);
     std::vector<Chunk> ch;
+    std::vector<uint32_t> order;
     size_t i = 0;
     int k = 0;
     while (i < n) {
@@ -665,8 +687,10 @@ static int pipeline_run(ptls_hip_pipeline_t *p, ptls_hip_keyset_t *ks, const ptl
             lanes = choose_lanes(tmp);
         }
         bool aligned;
-        build_chunks(s.h_recs, cnt, lanes, ch, aligned);
+        build_chunks(s.h_recs, cnt, lanes, ch, order, aligned);
         std::memcpy(s.h_chunks, ch.data(), ch.size() * sizeof(Chunk));
+        std::memcpy(s.h_order, order.data(), cnt * sizeof(uint32_t));
+        HIP_TRY(hipMemcpyAsync(s.d_order, s.h_order, cnt * sizeof(uint32_t), hipMemcpyHostToDevice, s.stream), PTLS_HIP_ENODEV);
         HIP_TRY(hipMemcpyAsync(s.d_recs, s.h_recs, cnt * sizeof(ptls_hip_record_t), hipMemcpyHostToDevice, s.stream),
                 PTLS_HIP_ENODEV);
         HIP_TRY(hipMemcpyAsync(s.d_chunks, s.h_chunks, ch.size() * sizeof(Chunk), hipMemcpyHostToDevice, s.stream), PTLS_HIP_ENODEV);
@@ -677,6 +701,7 @@ static int pipeline_run(ptls_hip_pipeline_t *p, ptls_hip_keyset_t *ks, const ptl
                     PTLS_HIP_ENODEV);
         KernelArgs a{};
         a.recs = s.d_recs;
+        a.order = s.d_order;
         a.chunks = s.d_chunks;
         a.nchunks = (uint32_t)ch.size();
         a.in = s.d_in;
@@ -762,6 +787,7 @@ struct hip_aead_state {
     size_t cap, aad_cap;
     ptls_hip_record_t *d_rec;
     Chunk *d_chunk;
+    uint32_t *d_order;
     uint64_t *d_result;
     uint8_t *h_stage; /* pinned: record + chunk + result */
     uint8_t iv[12];
@@ -827,15 +853,18 @@ static uint64_t plugin_run(hip_aead_state *st, bool open, void *output, const vo
     rec.aad_len = (uint32_t)aadlen;
     rec.key = 0;
     Chunk ch{0, 1, 0, 1};
+    const uint32_t order0 = 0;
     std::memcpy(st->h_stage, &rec, sizeof(rec));
     std::memcpy(st->h_stage + 64, &ch, sizeof(ch));
-    plugin_check(hipMemcpyAsync(st->d_rec, st->h_stage, 64 + sizeof(ch), hipMemcpyHostToDevice, st->stream), "upload(rec)");
+    std::memcpy(st->h_stage + 96, &order0, sizeof(order0));
+    plugin_check(hipMemcpyAsync(st->d_rec, st->h_stage, 100, hipMemcpyHostToDevice, st->stream), "upload(rec)");
     if (in_len != 0)
         plugin_check(hipMemcpyAsync(d_in, input, in_len, hipMemcpyHostToDevice, st->stream), "upload(in)");
     if (aadlen != 0)
         plugin_check(hipMemcpyAsync(d_aad, aad, aadlen, hipMemcpyHostToDevice, st->stream), "upload(aad)");
     KernelArgs a{};
     a.recs = st->d_rec;
+    a.order = st->d_order;
     a.chunks = st->d_chunk;
     a.nchunks = 1;
     a.in = d_in;
@@ -993,6 +1022,7 @@ static int aesgcm_setup(ptls_aead_context_t *_ctx, int is_enc, const void *key, 
         return -1;
     }
     st->d_chunk = reinterpret_cast<Chunk *>(reinterpret_cast<uint8_t *>(st->d_rec) + 64);
+    st->d_order = reinterpret_cast<uint32_t *>(reinterpret_cast<uint8_t *>(st->d_rec) + 96);
     st->d_result = reinterpret_cast<uint64_t *>(reinterpret_cast<uint8_t *>(st->d_rec) + 128);
     std::memcpy(st->iv, iv, 12);
     st->iv_dirty = false;

@@ -32,7 +32,7 @@ struct KeySlot {
 static_assert(sizeof(KeySlot) == 512, "KeySlot must stay 512 bytes");
 
 struct Chunk {
-    uint32_t first; /* index of first record */
+    uint32_t first; /* position of the chunk's first record in the order array */
     uint32_t count; /* records in the chunk, all with the same key slot */
     uint32_t key;   /* key slot */
     uint32_t flags; /* bit0: every record of the chunk is 16-byte aligned (in/out/aad offsets) */
@@ -40,6 +40,7 @@ struct Chunk {
 
 struct KernelArgs {
     const ptls_hip_record_t *recs;
+    const uint32_t *order;  /* chunk positions -> record index (records of a chunk sorted by length) */
     const Chunk *chunks;
     uint32_t nchunks;
     uint32_t pad0;
