@@ -804,7 +804,7 @@ __global__ void __launch_bounds__(WGT)
         const uint8_t *, const uint8_t *__restrict__,                                                                      \
         uint8_t *, uint64_t *__restrict__, const KeySlot *__restrict__, const uint32_t *__restrict__, const uint32_t *__restrict__);
 #define INST_W(G, A, W) INST(G, 10, false, A, W) INST(G, 10, true, A, W) INST(G, 14, false, A, W) INST(G, 14, true, A, W)
-#define INST_G(G) INST_W(G, true, 512) INST_W(G, false, 512) INST_W(G, true, 1024) INST_W(G, false, 1024)
+#define INST_G(G) INST_W(G, true, 512) INST_W(G, false, 512) INST_W(G, true, WG_ALT) INST_W(G, false, WG_ALT)
 INST_G(1)
 INST_G(2)
 INST_G(4)
@@ -1009,7 +1009,7 @@ static hipError_t launch_one(unsigned grid, hipStream_t s, const KernelArgs &a, 
 template <int G, int R, bool O>
 static hipError_t launch_w(int wg, unsigned grid, hipStream_t s, const KernelArgs &a, bool aligned)
 {
-    return wg == 512 ? launch_one<G, R, O, 512>(grid, s, a, aligned) : launch_one<G, R, O, 1024>(grid, s, a, aligned);
+    return wg == 512 ? launch_one<G, R, O, 512>(grid, s, a, aligned) : launch_one<G, R, O, WG_ALT>(grid, s, a, aligned);
 }
 
 template <int G>

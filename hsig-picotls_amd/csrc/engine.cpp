@@ -330,12 +330,12 @@ static int choose_lanes(const std::vector<ptls_hip_record_t> &recs)
 
 static int plan_wg(const std::vector<Chunk> &ch, int lanes)
 {
-    /* Measured on MI355X (tools/tune.py, same-process sweep): with the counter-mode AES shortcut, 512
-     * threads (2 waves per SIMD, 256-VGPR budget, no spills) is as fast or faster than 1024 for every
-     * BASELINE shape (1M x 16 KiB: 1011 vs 995 GiB/s seal; 4M x 1350 B: 821 vs 721; 64K keys: 284 vs 201). */
+    /* Measured on MI355X (tools/tune.py, same-process sweep): 768 threads = 3 waves per SIMD at 168 VGPRs
+     * (no spills for G <= 4) beats 512 (2 waves, 193 VGPRs) on every BASELINE shape: 1M x 16 KiB 1033 vs
+     * 968 GiB/s seal, 4M x 1350 B 864 vs 788, 64K keys 416 vs 415; 1024 threads spills and loses to both. */
     (void)ch;
     (void)lanes;
-    return 512;
+    return WG_ALT;
 }
 
 /* chunk = run of records with one key slot, sized to keep all waves of a workgroup busy for a few tasks.
@@ -460,8 +460,8 @@ extern "C" int ptls_hip_batch_lanes(ptls_hip_batch_t *b)
 
 extern "C" int ptls_hip_batch_set_workgroup(ptls_hip_batch_t *b, int threads)
 {
-    if (b == nullptr || !(threads == 0 || threads == 512 || threads == 1024))
-        return fail(PTLS_HIP_EINVAL, "batch_set_workgroup: threads must be 0, 512 or 1024");
+    if (b == nullptr || !(threads == 0 || threads == 512 || threads == WG_ALT))
+        return fail(PTLS_HIP_EINVAL, "batch_set_workgroup: threads must be 0, 512 or %d", WG_ALT);
     DeviceGuard g(b->eng->device);
     b->forced_wg = threads;
     return plan_chunks(b);

@@ -18,8 +18,8 @@ namespace ptls_hip {
 
 constexpr int NPOW = 4;          /* H^1, H^2, H^4, H^8 */
 constexpr int MAX_LANES = 8;     /* lanes per record (G) supported: 1, 2, 4, 8 */
-/* one workgroup per CU (LDS-limited).  1024 threads (4 waves per SIMD) unless key runs are too short to
- * give every wave work, then 512 (chosen per batch by the planner, engine.cpp:plan_wg) */
+/* one workgroup per CU (LDS-limited); 768 threads (3 waves per SIMD, 168 VGPRs) by default, 512 selectable
+ * per batch (engine.cpp:plan_wg).  WG_MAX bounds the chunk size the planner cuts key runs into. */
 constexpr int WG_MAX = 1024;
 
 struct KeySlot {
@@ -30,6 +30,11 @@ struct KeySlot {
     uint32_t pad[(512 - 240 - 4 - 12 - 16 * NPOW) / 4];
 };
 static_assert(sizeof(KeySlot) == 512, "KeySlot must stay 512 bytes");
+
+/* the second compiled workgroup size (the first is 512); tuning builds override it (tools/build_variant.sh) */
+#ifndef WG_ALT
+#define WG_ALT 768
+#endif
 
 struct Chunk {
     uint32_t first; /* position of the chunk's first record in the order array */

@@ -111,7 +111,7 @@ size_t ptls_hip_batch_count(ptls_hip_batch_t *batch);
 /* lanes cooperating on one record (1, 2, 4 or 8); 0 = automatic (default).  For tuning and tests. */
 int ptls_hip_batch_set_lanes(ptls_hip_batch_t *batch, int lanes);
 int ptls_hip_batch_lanes(ptls_hip_batch_t *batch);
-/* threads per workgroup of the batch kernel (512 or 1024); 0 = automatic (default).  For tuning. */
+/* threads per workgroup of the batch kernel (512 or 768); 0 = automatic (default).  For tuning. */
 int ptls_hip_batch_set_workgroup(ptls_hip_batch_t *batch, int threads);
 int ptls_hip_batch_workgroup(ptls_hip_batch_t *batch);
 

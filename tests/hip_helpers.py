@@ -56,8 +56,9 @@ class HostBatch:
                 buf[rec["in_off"]: rec["in_off"] + len(p)] = np.frombuffer(bytes(p), np.uint8)
         return buf
 
-    def seal(self, lanes=0, in_place=False):
+    def seal(self, lanes=0, in_place=False, wg=0):
         self.batch.set_lanes(lanes)
+        self.batch.set_workgroup(wg)
         d_in = _dev(self._input([r[4] for r in self.records]), self.in_total)
         d_aad = _dev(self.aad, self.aad_total)
         if in_place:  # out_off must then equal in_off: use the input layout for both
@@ -76,9 +77,10 @@ class HostBatch:
         host = d_out.cpu().numpy()
         return [host[r["out_off"]: r["out_off"] + r["len"] + 16].tobytes() for r in self.recs]
 
-    def open(self, sealed, lanes=0):
+    def open(self, sealed, lanes=0, wg=0):
         """sealed: list of ct||tag per record.  Returns (results, plaintexts)."""
         self.batch.set_lanes(lanes)
+        self.batch.set_workgroup(wg)
         d_in = _dev(self._input(sealed), self.in_total)
         d_aad = _dev(self.aad, self.aad_total)
         d_out = _dev(None, self.out_total)

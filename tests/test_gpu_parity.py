@@ -159,6 +159,27 @@ def test_unaligned_layout(engine, oracle, align):
     hb.close()
 
 
+@pytest.mark.parametrize("wg", [512, 768])
+@pytest.mark.parametrize("lanes", [2, 4, 8])
+def test_key_runs_mixed_lengths(engine, oracle, wg, lanes):
+    """BASELINE configs[3] shape in miniature: AES-256, several keys with runs of 150-400 records of
+    random 0..6000-byte lengths (the planner reorders each key chunk by length), every workgroup size"""
+    rng = np.random.default_rng(wg * 10 + lanes)
+    recs = []
+    for k in range(5):
+        key, iv = oracle.gen_key(k, 32)
+        for i in range(int(rng.integers(150, 400))):
+            L = int(rng.integers(0, 6000))
+            recs.append((key, iv, 1000 * k + i, tls_aad(L), oracle.stream(77 * k + i, L)))
+    hb = HostBatch(engine, recs)
+    outs = hb.seal(lanes, wg=wg)
+    bad = [j for j, (r, o) in enumerate(zip(recs, outs)) if o != oracle.seal(*r)]
+    assert not bad, f"{len(bad)} mismatches, first {bad[:8]}"
+    res, pts = hb.open(outs, lanes, wg=wg)
+    assert res == [len(r[4]) for r in recs] and pts == [r[4] for r in recs]
+    hb.close()
+
+
 def test_in_place_seal(engine, oracle):
     """output == input is allowed (fusion, SURVEY.md §7 hard parts)"""
     recs = []

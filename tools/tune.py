@@ -10,7 +10,7 @@ import bench, ptls_hip
 ap = argparse.ArgumentParser()
 ap.add_argument("--configs", default="c2,c3,c4")
 ap.add_argument("--lanes", default="1,2,4,8")
-ap.add_argument("--wg", default="512,1024")
+ap.add_argument("--wg", default="512,768")
 ap.add_argument("--reps", type=int, default=4)
 args = ap.parse_args()
 eng = ptls_hip.Engine(0)
