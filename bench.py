@@ -202,6 +202,37 @@ def golden_check(cfg_name, idx, recs, d_ct):
     return checked
 
 
+def device_copy_gbs(nbytes=4 << 30, reps=5):
+    """achievable HBM bandwidth in this session: device-to-device copy of nbytes (read + write counted),
+    HIP events, median of reps (report against the measured device-copy bandwidth too)"""
+    import torch
+    src = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
+    dst = torch.empty_like(src)
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    dst.copy_(src)
+    ts = []
+    for _ in range(reps):
+        ev[0].record()
+        dst.copy_(src)
+        ev[1].record()
+        torch.cuda.synchronize()
+        ts.append(ev[0].elapsed_time(ev[1]))
+    del src, dst
+    return round(2 * nbytes / (float(np.median(ts)) * 1e-3) / 1e9, 1)
+
+
+def lds_issue_ceiling(key_len):
+    """ALU-side ceiling of the full-block loop: per 16-B block, AES T-table lookups
+    (ds_read_b32, 2 LDS cycles per wave instruction) + 16 GHASH window lookups (ds_read_b128, 4 cycles),
+    MI355X_MICROARCH.md LDS table; 256 CUs at the 2.4 GHz max clock; plaintext GiB/s of seal."""
+    rounds = 10 if key_len == 16 else 14
+    lookups = 2 + 8 + 16 * (rounds - 3) + 16  # counter-mode shortcut: round 1 = 2, round 2 = 8 lookups
+    cyc_per_block = (lookups * 2 + 16 * 4) / 64.0
+    gibps = 256 * 2.4e9 / cyc_per_block * 16 / GIB
+    return dict(aes_lookups_per_block=lookups, ghash_lookups_per_block=16,
+                lds_cycles_per_block_per_cu=round(cyc_per_block, 3), seal_gibps=round(gibps, 1))
+
+
 def host_e2e(args, cfg, eng, ks, recs, lens, d_pt, d_aad, aad_len):
     """Records start and end in pinned host memory (socket-buffer case): ptls_hip_pipeline_seal/open slice the
     batch and overlap H2D -> kernel -> D2H on three streams.  Timed wall-clock around the whole call."""
@@ -385,6 +416,12 @@ def main():
                      "kernel": "aesgcm_batch_kernel (seal)", "algorithmic_bytes_per_launch": alg_bytes},
         "parity": {"open_all_ok": ok_open, "roundtrip_bytes_equal": ok_pt, "golden_records_checked": golden_n},
     }
+    copy_gbs = device_copy_gbs()
+    result["roofline"]["measured_copy_gbs"] = copy_gbs
+    result["roofline"]["frac_of_measured_copy"] = round(achieved / copy_gbs, 4)
+    ceil = lds_issue_ceiling(cfg["key_len"])
+    ceil["frac"] = round(result["seal_gibps"] / world / ceil["seal_gibps"], 4)
+    result["roofline"]["lds_issue_ceiling"] = ceil
     if not args.no_e2e:
         result["host_e2e"] = host_e2e(args, cfg, eng, ks, recs, lens, d_pt, d_aad, aad_len)
     tfile = os.path.join(ROOT, "profiles", f"traffic_{args.config}.json")

@@ -606,7 +606,8 @@ __global__ void __launch_bounds__(WGT)
     aesgcm_batch_kernel(const ptls_hip_record_t *__restrict__ recs, const uint32_t *__restrict__ order,
                         const Chunk *__restrict__ chunks, uint32_t nchunks,
                         const uint8_t *in, const uint8_t *__restrict__ aad, uint8_t *out, uint64_t *__restrict__ result,
-                        const KeySlot *__restrict__ slots, const uint32_t *__restrict__ basis, const uint32_t *__restrict__ t0)
+                        const KeySlot *__restrict__ slots, const uint32_t *__restrict__ basis, const uint32_t *__restrict__ t0,
+                        const ptls_hip_supp_t *__restrict__ supp, const KeySlot *__restrict__ hp_slots, uint8_t *mask)
 {
     __shared__ __attribute__((aligned(16))) uint8_t lds[LDS_BYTES];
     constexpr int LOG2G = G == 1 ? 0 : G == 2 ? 1 : G == 4 ? 2 : 3;
@@ -794,6 +795,42 @@ __global__ void __launch_bounds__(WGT)
                         store_bytes(out_p + L, 16, tag);
                 }
             }
+            if (!OPEN && supp != nullptr) {
+                /* QUIC header protection (fusion's supp, lib/fusion.c:636-650): AES-ECB(hp key, 16 output bytes)
+                 * computed after the record, because the sample may cover the tag.  The sample was written by
+                 * other lanes of this wave: the agent-scope release/acquire pair completes their stores and
+                 * invalidates this CU's L1 before the read. */
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                if (valid && r == 0) {
+                    const ptls_hip_supp_t sp = supp[rec_i];
+                    if (sp.flags & PTLS_HIP_SUPP_ENABLE) {
+                        const V4 sample = load_bytes(out + sp.sample_off, 16);
+                        const V4 m = aes_encrypt<ROUNDS>(lds, lb_aes, hp_slots[sp.hp_key].rk, sample);
+                        store_bytes(mask + sp.mask_off, 16, m);
+                    }
+                }
+            }
+        }
+    }
+}
+
+/* Standalone header-protection masks (receive side): mask + mask_off = AES-ECB(hp key, src + sample_off),
+ * one record per lane, grid-stride.  Same replicated T-tables as the batch kernel (at LDS_AES). */
+template <int ROUNDS>
+__global__ void __launch_bounds__(256) aesecb_batch_kernel(const ptls_hip_supp_t *__restrict__ supp, uint32_t n,
+                                                           const uint8_t *__restrict__ src, uint8_t *__restrict__ mask,
+                                                           const KeySlot *__restrict__ hp_slots, const uint32_t *__restrict__ t0)
+{
+    __shared__ __attribute__((aligned(16))) uint8_t lds[LDS_AES + 65536];
+    build_aes_tables(lds, t0);
+    __syncthreads();
+    const uint32_t lb_aes = (uint32_t)(threadIdx.x & 31) * 4u | LDS_AES;
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        const ptls_hip_supp_t sp = supp[i];
+        if (sp.flags & PTLS_HIP_SUPP_ENABLE) {
+            const V4 m = aes_encrypt<ROUNDS>(lds, lb_aes, hp_slots[sp.hp_key].rk, load_bytes(src + sp.sample_off, 16));
+            store_bytes(mask + sp.mask_off, 16, m);
         }
     }
 }
@@ -802,7 +839,8 @@ __global__ void __launch_bounds__(WGT)
     template __global__ void aesgcm_batch_kernel<G, R, O, A, W>(                                                           \
         const ptls_hip_record_t *__restrict__, const uint32_t *__restrict__, const Chunk *__restrict__, uint32_t,              \
         const uint8_t *, const uint8_t *__restrict__,                                                                      \
-        uint8_t *, uint64_t *__restrict__, const KeySlot *__restrict__, const uint32_t *__restrict__, const uint32_t *__restrict__);
+        uint8_t *, uint64_t *__restrict__, const KeySlot *__restrict__, const uint32_t *__restrict__, const uint32_t *__restrict__, \
+        const ptls_hip_supp_t *__restrict__, const KeySlot *__restrict__, uint8_t *);
 #define INST_W(G, A, W) INST(G, 10, false, A, W) INST(G, 10, true, A, W) INST(G, 14, false, A, W) INST(G, 14, true, A, W)
 #define INST_G(G) INST_W(G, true, 512) INST_W(G, false, 512) INST_W(G, true, WG_ALT) INST_W(G, false, WG_ALT)
 INST_G(1)
@@ -999,10 +1037,10 @@ static hipError_t launch_one(unsigned grid, hipStream_t s, const KernelArgs &a, 
 {
     if (aligned)
         hipLaunchKernelGGL((aesgcm_batch_kernel<G, R, O, true, W>), dim3(grid), dim3(W), 0, s, a.recs, a.order, a.chunks,
-                           a.nchunks, a.in, a.aad, a.out, a.result, a.slots, a.basis, a.t0);
+                           a.nchunks, a.in, a.aad, a.out, a.result, a.slots, a.basis, a.t0, a.supp, a.hp_slots, a.mask);
     else
         hipLaunchKernelGGL((aesgcm_batch_kernel<G, R, O, false, W>), dim3(grid), dim3(W), 0, s, a.recs, a.order, a.chunks,
-                           a.nchunks, a.in, a.aad, a.out, a.result, a.slots, a.basis, a.t0);
+                           a.nchunks, a.in, a.aad, a.out, a.result, a.slots, a.basis, a.t0, a.supp, a.hp_slots, a.mask);
     return hipGetLastError();
 }
 
@@ -1061,4 +1099,16 @@ int launch_fill(const ptls_hip_record_t *recs, uint32_t n, uint8_t *buf, uint64_
     return (int)hipGetLastError();
 }
 
+int launch_aesecb(int rounds, const ptls_hip_supp_t *supp, uint32_t n, const uint8_t *src, uint8_t *mask, const KeySlot *hp_slots,
+                  const uint32_t *t0, unsigned grid, void *stream)
+{
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    if (rounds == 10)
+        hipLaunchKernelGGL(aesecb_batch_kernel<10>, dim3(grid), dim3(256), 0, s, supp, n, src, mask, hp_slots, t0);
+    else
+        hipLaunchKernelGGL(aesecb_batch_kernel<14>, dim3(grid), dim3(256), 0, s, supp, n, src, mask, hp_slots, t0);
+    return (int)hipGetLastError();
+}
+
 } // namespace ptls_hip
+

@@ -250,10 +250,15 @@ extern "C" size_t ptls_hip_keyset_size(ptls_hip_keyset_t *ks)
 extern "C" int ptls_hip_keyset_set(ptls_hip_keyset_t *ks, size_t first, size_t count, const void *keys, const void *ivs,
                                    void *stream)
 {
-    if (ks == nullptr || keys == nullptr || ivs == nullptr || first + count > ks->nslots)
+    if (ks == nullptr || keys == nullptr || first + count > ks->nslots)
         return fail(PTLS_HIP_EINVAL, "keyset_set: bad arguments");
     if (count == 0)
         return 0;
+    std::vector<uint8_t> zero_ivs;
+    if (ivs == nullptr) { /* header-protection / ECB-only keys carry no IV */
+        zero_ivs.assign(count * 12, 0);
+        ivs = zero_ivs.data();
+    }
     DeviceGuard g(ks->eng->device);
     hipStream_t s = static_cast<hipStream_t>(stream);
     uint8_t *d_tmp = nullptr;
@@ -473,10 +478,14 @@ extern "C" int ptls_hip_batch_workgroup(ptls_hip_batch_t *b)
 }
 
 static int run_batch(ptls_hip_batch_t *b, ptls_hip_keyset_t *ks, const void *in, const void *aad, void *out, uint64_t *result,
-                     void *stream, bool open)
+                     void *stream, bool open, ptls_hip_keyset_t *hp_ks = nullptr, const ptls_hip_supp_t *supp = nullptr,
+                     void *mask = nullptr)
 {
     if (b == nullptr || ks == nullptr || ks->eng != b->eng)
         return fail(PTLS_HIP_EINVAL, "seal/open: batch and keyset must belong to the same engine");
+    if (supp != nullptr && (hp_ks == nullptr || hp_ks->eng != b->eng || hp_ks->key_size != ks->key_size || mask == nullptr))
+        return fail(PTLS_HIP_EINVAL, "seal_batch_supp: the header-protection keyset must be on the same engine with the "
+                                     "AEAD's key size, and mask must be given");
     if (b->n == 0)
         return 0;
     if (in == nullptr || out == nullptr || (open && result == nullptr))
@@ -494,6 +503,9 @@ static int run_batch(ptls_hip_batch_t *b, ptls_hip_keyset_t *ks, const void *in,
     a.slots = ks->d_slots;
     a.basis = ks->d_basis;
     a.t0 = b->eng->d_t0;
+    a.supp = supp;
+    a.hp_slots = hp_ks != nullptr ? hp_ks->d_slots : nullptr;
+    a.mask = static_cast<uint8_t *>(mask);
     const bool base_aligned = ((reinterpret_cast<uintptr_t>(in) | reinterpret_cast<uintptr_t>(a.aad) |
                                 reinterpret_cast<uintptr_t>(out)) & 15) == 0;
     const bool aligned = base_aligned && b->all_aligned;
@@ -509,6 +521,32 @@ extern "C" int ptls_hip_aesgcm_seal_batch(ptls_hip_batch_t *b, ptls_hip_keyset_t
                                           void *stream)
 {
     return run_batch(b, ks, in, aad, out, nullptr, stream, false);
+}
+
+extern "C" int ptls_hip_aesgcm_seal_batch_supp(ptls_hip_batch_t *b, ptls_hip_keyset_t *ks, ptls_hip_keyset_t *hp_ks,
+                                               const ptls_hip_supp_t *supp, const void *in, const void *aad, void *out, void *mask,
+                                               void *stream)
+{
+    if (supp == nullptr)
+        return fail(PTLS_HIP_EINVAL, "seal_batch_supp: supp descriptors missing");
+    return run_batch(b, ks, in, aad, out, nullptr, stream, false, hp_ks, supp, mask);
+}
+
+extern "C" int ptls_hip_aesecb_batch(ptls_hip_engine_t *eng, ptls_hip_keyset_t *hp_ks, const ptls_hip_supp_t *supp, size_t n,
+                                     const void *src, void *mask, void *stream)
+{
+    if (eng == nullptr || hp_ks == nullptr || hp_ks->eng != eng || n > 0xffffffffu ||
+        (n != 0 && (supp == nullptr || src == nullptr || mask == nullptr)))
+        return fail(PTLS_HIP_EINVAL, "aesecb_batch: bad arguments");
+    if (n == 0)
+        return 0;
+    DeviceGuard g(eng->device);
+    const unsigned grid = (unsigned)std::min<size_t>((n + 255) / 256, (size_t)eng->ncu * 4);
+    const int e = launch_aesecb(hp_ks->key_size == 16 ? 10 : 14, supp, (uint32_t)n, static_cast<const uint8_t *>(src),
+                                static_cast<uint8_t *>(mask), hp_ks->d_slots, eng->d_t0, grid, stream);
+    if (e != 0)
+        return fail(PTLS_HIP_ELAUNCH, "aesecb_batch: kernel launch failed: %s", hipGetErrorString((hipError_t)e));
+    return 0;
 }
 
 extern "C" int ptls_hip_aesgcm_open_batch(ptls_hip_batch_t *b, ptls_hip_keyset_t *ks, const void *in, const void *aad, void *out,
@@ -813,6 +851,135 @@ static void plugin_check(hipError_t e, const char *what)
     }
 }
 
+/* ---- CTR cipher for header protection (replaces lib/fusion.c:1050-1100) ---------------------------- */
+
+struct hip_ctr_state {
+    ptls_hip_engine_t *eng;
+    ptls_hip_keyset_t *ks;
+    hipStream_t stream;
+    uint8_t *d_buf;   /* [ptls_hip_supp_t @0][input block @32][mask @48] */
+    uint8_t *h_stage; /* pinned, same layout */
+    uint8_t bits[16];
+    bool ready;
+};
+
+struct hip_ctr_context {
+    ptls_cipher_context_t super;
+    hip_ctr_state *st;
+};
+
+extern "C" ptls_cipher_algorithm_t ptls_hip_aes128ctr, ptls_hip_aes256ctr;
+
+static const hip_ctr_state *ctr_state_of(const ptls_cipher_context_t *c)
+{
+    if (c == nullptr || (c->algo != &ptls_hip_aes128ctr && c->algo != &ptls_hip_aes256ctr))
+        return nullptr;
+    return reinterpret_cast<const hip_ctr_context *>(c)->st;
+}
+
+/* do_init: the keystream block AES-ECB(key, iv) on the device (fusion: aesecb_encrypt, :1057-1062) */
+static void ctr_init(ptls_cipher_context_t *_ctx, const void *iv)
+{
+    hip_ctr_state *st = reinterpret_cast<hip_ctr_context *>(_ctx)->st;
+    DeviceGuard g(st->eng->device);
+    const ptls_hip_supp_t sp{32, 48, 0, PTLS_HIP_SUPP_ENABLE};
+    std::memcpy(st->h_stage, &sp, sizeof(sp));
+    std::memcpy(st->h_stage + 32, iv, 16);
+    plugin_check(hipMemcpyAsync(st->d_buf, st->h_stage, 48, hipMemcpyHostToDevice, st->stream), "ctr upload");
+    const int e = launch_aesecb(st->ks->key_size == 16 ? 10 : 14, reinterpret_cast<const ptls_hip_supp_t *>(st->d_buf), 1,
+                                st->d_buf, st->d_buf, st->ks->d_slots, st->eng->d_t0, 1, st->stream);
+    if (e != 0) {
+        g_err = hipGetErrorString((hipError_t)e);
+        plugin_die("ctr launch");
+    }
+    plugin_check(hipMemcpyAsync(st->h_stage + 48, st->d_buf + 48, 16, hipMemcpyDeviceToHost, st->stream), "ctr download");
+    plugin_check(hipStreamSynchronize(st->stream), "ctr sync");
+    std::memcpy(st->bits, st->h_stage + 48, 16);
+    st->ready = true;
+}
+
+/* do_transform: at most 16 bytes per do_init, like fusion's ctr_transform (:1064-1077) */
+static void ctr_transform(ptls_cipher_context_t *_ctx, void *output, const void *input, size_t len)
+{
+    hip_ctr_state *st = reinterpret_cast<hip_ctr_context *>(_ctx)->st;
+    if (!st->ready || len > 16) {
+        fprintf(stderr, "ptls_hip: CTR transformation is supported only once per call to `init` and for at most 16 bytes\n");
+        abort();
+    }
+    st->ready = false;
+    for (size_t i = 0; i < len; ++i)
+        static_cast<uint8_t *>(output)[i] = static_cast<const uint8_t *>(input)[i] ^ st->bits[i];
+}
+
+static void ctr_dispose(ptls_cipher_context_t *_ctx)
+{
+    auto *ctx = reinterpret_cast<hip_ctr_context *>(_ctx);
+    hip_ctr_state *st = ctx->st;
+    if (st == nullptr)
+        return;
+    {
+        DeviceGuard g(st->eng->device);
+        ptls_hip_keyset_free(st->ks);
+        if (st->d_buf != nullptr) {
+            (void)hipMemset(st->d_buf, 0, 64);
+            (void)hipStreamSynchronize(st->stream);
+        }
+        (void)hipFree(st->d_buf);
+        if (st->h_stage != nullptr)
+            std::memset(st->h_stage, 0, 64);
+        (void)hipHostFree(st->h_stage);
+        (void)hipStreamDestroy(st->stream);
+    }
+    std::memset(st->bits, 0, sizeof(st->bits));
+    delete st;
+    ctx->st = nullptr;
+}
+
+static int aesctr_setup(ptls_cipher_context_t *_ctx, int is_enc, const void *key, size_t key_size)
+{
+    (void)is_enc; /* CTR: same operation both ways */
+    auto *ctx = reinterpret_cast<hip_ctr_context *>(_ctx);
+    ctx->st = nullptr;
+    ptls_hip_engine_t *eng = plugin_engine();
+    if (eng == nullptr || key == nullptr)
+        return -1;
+    DeviceGuard g(eng->device);
+    auto *st = new hip_ctr_state();
+    st->eng = eng;
+    if (hipStreamCreateWithFlags(&st->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete st;
+        return -1;
+    }
+    st->ks = ptls_hip_keyset_new(eng, key_size, 1);
+    const bool ok = st->ks != nullptr && hipMalloc(&st->d_buf, 64) == hipSuccess &&
+                    hipHostMalloc(&st->h_stage, 64, hipHostMallocDefault) == hipSuccess &&
+                    ptls_hip_keyset_set(st->ks, 0, 1, key, nullptr, st->stream) == 0;
+    if (!ok) {
+        if (st->ks != nullptr)
+            ptls_hip_keyset_free(st->ks);
+        (void)hipFree(st->d_buf);
+        (void)hipHostFree(st->h_stage);
+        (void)hipStreamDestroy(st->stream);
+        delete st;
+        return -1;
+    }
+    ctx->st = st;
+    ctx->super.do_dispose = ctr_dispose;
+    ctx->super.do_init = ctr_init;
+    ctx->super.do_transform = ctr_transform;
+    return 0;
+}
+
+static int aes128ctr_setup(ptls_cipher_context_t *ctx, int is_enc, const void *key)
+{
+    return aesctr_setup(ctx, is_enc, key, PTLS_AES128_KEY_SIZE);
+}
+
+static int aes256ctr_setup(ptls_cipher_context_t *ctx, int is_enc, const void *key)
+{
+    return aesctr_setup(ctx, is_enc, key, PTLS_AES256_KEY_SIZE);
+}
+
 static void state_reserve(hip_aead_state *st, size_t len, size_t aadlen)
 {
     if (len <= st->cap && aadlen <= st->aad_cap)
@@ -831,9 +998,20 @@ static void state_reserve(hip_aead_state *st, size_t len, size_t aadlen)
     st->aad_cap = aad_cap;
 }
 
+/* fused header protection for one plugin call: sample offset inside the record output, hp key slots */
+struct PluginSupp {
+    uint64_t sample_off;
+    const KeySlot *hp_slots;
+    uint8_t *output; /* host: supp->output */
+};
+
+/* pinned / device staging layout of one plugin call (256 B): record @0, chunk @64, order @96, result @128,
+ * supp descriptor @160, header-protection mask @192 */
+static const size_t ST_REC = 0, ST_CHUNK = 64, ST_ORDER = 96, ST_RESULT = 128, ST_SUPP = 160, ST_MASK = 192;
+
 /* run one record through the batch kernel: in/out/aad are host buffers */
 static uint64_t plugin_run(hip_aead_state *st, bool open, void *output, const void *input, size_t len, uint64_t seq,
-                           const void *aad, size_t aadlen)
+                           const void *aad, size_t aadlen, const PluginSupp *ps = nullptr)
 {
     DeviceGuard g(st->eng->device);
     const size_t in_len = open ? len + 16 : len;
@@ -854,10 +1032,12 @@ static uint64_t plugin_run(hip_aead_state *st, bool open, void *output, const vo
     rec.key = 0;
     Chunk ch{0, 1, 0, 1};
     const uint32_t order0 = 0;
-    std::memcpy(st->h_stage, &rec, sizeof(rec));
-    std::memcpy(st->h_stage + 64, &ch, sizeof(ch));
-    std::memcpy(st->h_stage + 96, &order0, sizeof(order0));
-    plugin_check(hipMemcpyAsync(st->d_rec, st->h_stage, 100, hipMemcpyHostToDevice, st->stream), "upload(rec)");
+    const ptls_hip_supp_t sp{ps != nullptr ? ps->sample_off : 0, 0, 0, PTLS_HIP_SUPP_ENABLE};
+    std::memcpy(st->h_stage + ST_REC, &rec, sizeof(rec));
+    std::memcpy(st->h_stage + ST_CHUNK, &ch, sizeof(ch));
+    std::memcpy(st->h_stage + ST_ORDER, &order0, sizeof(order0));
+    std::memcpy(st->h_stage + ST_SUPP, &sp, sizeof(sp));
+    plugin_check(hipMemcpyAsync(st->d_rec, st->h_stage, ST_SUPP + sizeof(sp), hipMemcpyHostToDevice, st->stream), "upload(rec)");
     if (in_len != 0)
         plugin_check(hipMemcpyAsync(d_in, input, in_len, hipMemcpyHostToDevice, st->stream), "upload(in)");
     if (aadlen != 0)
@@ -874,6 +1054,12 @@ static uint64_t plugin_run(hip_aead_state *st, bool open, void *output, const vo
     a.slots = st->ks->d_slots;
     a.basis = st->ks->d_basis;
     a.t0 = st->eng->d_t0;
+    if (ps != nullptr) {
+        uint8_t *d_stage = reinterpret_cast<uint8_t *>(st->d_rec);
+        a.supp = reinterpret_cast<const ptls_hip_supp_t *>(d_stage + ST_SUPP);
+        a.hp_slots = ps->hp_slots;
+        a.mask = d_stage + ST_MASK;
+    }
     const size_t n = (aadlen + 15) / 16 + (len + 15) / 16 + 1;
     const int lanes = n >= 128 ? 8 : n >= 48 ? 4 : n >= 16 ? 2 : 1;
     int e = launch_batch(lanes, st->ks->key_size == 16 ? 10 : 14, open, 512, 1, st->stream, a, true);
@@ -885,13 +1071,19 @@ static uint64_t plugin_run(hip_aead_state *st, bool open, void *output, const vo
     if (open) {
         if (len != 0)
             plugin_check(hipMemcpyAsync(output, d_out, len, hipMemcpyDeviceToHost, st->stream), "download(out)");
-        plugin_check(hipMemcpyAsync(st->h_stage + 128, st->d_result, 8, hipMemcpyDeviceToHost, st->stream), "download(result)");
+        plugin_check(hipMemcpyAsync(st->h_stage + ST_RESULT, st->d_result, 8, hipMemcpyDeviceToHost, st->stream), "download(result)");
     } else {
         plugin_check(hipMemcpyAsync(output, d_out, len + 16, hipMemcpyDeviceToHost, st->stream), "download(out)");
+        if (ps != nullptr)
+            plugin_check(hipMemcpyAsync(st->h_stage + ST_MASK, reinterpret_cast<uint8_t *>(st->d_rec) + ST_MASK, 16,
+                                        hipMemcpyDeviceToHost, st->stream),
+                         "download(mask)");
     }
     plugin_check(hipStreamSynchronize(st->stream), "hipStreamSynchronize");
     if (open)
-        std::memcpy(&result, st->h_stage + 128, 8);
+        std::memcpy(&result, st->h_stage + ST_RESULT, 8);
+    if (ps != nullptr)
+        std::memcpy(ps->output, st->h_stage + ST_MASK, 16);
     return result;
 }
 
@@ -952,6 +1144,16 @@ static void aead_encrypt(ptls_aead_context_t *_ctx, void *output, const void *in
                          size_t aadlen, ptls_aead_supplementary_encryption_t *supp)
 {
     hip_aead_state *st = reinterpret_cast<hip_aead_context *>(_ctx)->st;
+    if (supp != nullptr) {
+        /* fused (lib/fusion.c:424-428, :636-650): our CTR context, same key size, sample inside the output */
+        const hip_ctr_state *cs = ctr_state_of(supp->ctx);
+        const uint8_t *in = static_cast<const uint8_t *>(supp->input), *o = static_cast<const uint8_t *>(output);
+        if (cs != nullptr && cs->ks->key_size == st->ks->key_size && cs->eng == st->eng && in >= o && in + 16 <= o + inlen + 16) {
+            PluginSupp ps{(uint64_t)(in - o), cs->ks->d_slots, supp->output};
+            plugin_run(st, false, output, input, inlen, seq, aad, aadlen, &ps);
+            return;
+        }
+    }
     plugin_run(st, false, output, input, inlen, seq, aad, aadlen);
     if (supp != nullptr) {
         /* header-protection mask from the caller's cipher context, computed after the AEAD output exists
@@ -1021,9 +1223,9 @@ static int aesgcm_setup(ptls_aead_context_t *_ctx, int is_enc, const void *key, 
         delete st;
         return -1;
     }
-    st->d_chunk = reinterpret_cast<Chunk *>(reinterpret_cast<uint8_t *>(st->d_rec) + 64);
-    st->d_order = reinterpret_cast<uint32_t *>(reinterpret_cast<uint8_t *>(st->d_rec) + 96);
-    st->d_result = reinterpret_cast<uint64_t *>(reinterpret_cast<uint8_t *>(st->d_rec) + 128);
+    st->d_chunk = reinterpret_cast<Chunk *>(reinterpret_cast<uint8_t *>(st->d_rec) + ST_CHUNK);
+    st->d_order = reinterpret_cast<uint32_t *>(reinterpret_cast<uint8_t *>(st->d_rec) + ST_ORDER);
+    st->d_result = reinterpret_cast<uint64_t *>(reinterpret_cast<uint8_t *>(st->d_rec) + ST_RESULT);
     std::memcpy(st->iv, iv, 12);
     st->iv_dirty = false;
     ctx->st = st;
@@ -1049,14 +1251,16 @@ static int aes256gcm_setup(ptls_aead_context_t *ctx, int is_enc, const void *key
     return aesgcm_setup(ctx, is_enc, key, iv, PTLS_AES256_KEY_SIZE);
 }
 
-/* Field-for-field the values of ptls_fusion_aes{128,256}gcm (lib/fusion.c:1231-1256), except that no
- * CTR cipher object is advertised yet (QUIC header protection fused into the batch kernel is a
- * "next" row). */
+/* Field-for-field the values of ptls_fusion_aes{128,256}ctr / aes{128,256}gcm (lib/fusion.c:1219-1256). */
 extern "C" {
+ptls_cipher_algorithm_t ptls_hip_aes128ctr = {"AES128-CTR", PTLS_AES128_KEY_SIZE, 1, PTLS_AES_IV_SIZE, sizeof(hip_ctr_context),
+                                              aes128ctr_setup};
+ptls_cipher_algorithm_t ptls_hip_aes256ctr = {"AES256-CTR", PTLS_AES256_KEY_SIZE, 1, PTLS_AES_IV_SIZE, sizeof(hip_ctr_context),
+                                              aes256ctr_setup};
 ptls_aead_algorithm_t ptls_hip_aes128gcm = {"AES128-GCM",
                                             PTLS_AESGCM_CONFIDENTIALITY_LIMIT,
                                             PTLS_AESGCM_INTEGRITY_LIMIT,
-                                            nullptr,
+                                            &ptls_hip_aes128ctr,
                                             nullptr,
                                             PTLS_AES128_KEY_SIZE,
                                             PTLS_AESGCM_IV_SIZE,
@@ -1069,7 +1273,7 @@ ptls_aead_algorithm_t ptls_hip_aes128gcm = {"AES128-GCM",
 ptls_aead_algorithm_t ptls_hip_aes256gcm = {"AES256-GCM",
                                             PTLS_AESGCM_CONFIDENTIALITY_LIMIT,
                                             PTLS_AESGCM_INTEGRITY_LIMIT,
-                                            nullptr,
+                                            &ptls_hip_aes256ctr,
                                             nullptr,
                                             PTLS_AES256_KEY_SIZE,
                                             PTLS_AESGCM_IV_SIZE,

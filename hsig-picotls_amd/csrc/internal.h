@@ -56,12 +56,18 @@ struct KernelArgs {
     const KeySlot *slots;
     const uint32_t *basis;  /* uint4 [slot][NPOW][128] */
     const uint32_t *t0;     /* AES T0 table, 256 words */
+    /* seal only, optional: QUIC header-protection masks (ptls_hip_aesgcm_seal_batch_supp) */
+    const ptls_hip_supp_t *supp; /* indexed like recs; nullptr = none */
+    const KeySlot *hp_slots;
+    uint8_t *mask;
 };
 
 /* host-side launchers, defined next to the kernels (aesgcm_kernels.hip) */
 int launch_batch(int lanes, int rounds, bool open, int wg, unsigned grid, void *stream, const KernelArgs &a, bool aligned);
 int launch_keysetup(KeySlot *slots, uint32_t *basis, const uint8_t *keys, const uint8_t *ivs, uint32_t first, uint32_t count,
                     int key_size, const uint32_t *t0, void *stream);
+int launch_aesecb(int rounds, const ptls_hip_supp_t *supp, uint32_t n, const uint8_t *src, uint8_t *mask, const KeySlot *hp_slots,
+                  const uint32_t *t0, unsigned grid, void *stream);
 int launch_fill(const ptls_hip_record_t *recs, uint32_t n, uint8_t *buf, uint64_t seed, uint64_t index_base,
                 const uint64_t *index, unsigned grid, void *stream);
 

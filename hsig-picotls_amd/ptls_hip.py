@@ -16,6 +16,9 @@ UINT64_MAX = (1 << 64) - 1
 RECORD_DTYPE = np.dtype([("in_off", "<u8"), ("out_off", "<u8"), ("aad_off", "<u8"), ("seq", "<u8"),
                          ("len", "<u4"), ("aad_len", "<u4"), ("key", "<u4"), ("flags", "<u4")])
 assert RECORD_DTYPE.itemsize == 48
+SUPP_DTYPE = np.dtype([("sample_off", "<u8"), ("mask_off", "<u8"), ("hp_key", "<u4"), ("flags", "<u4")])
+assert SUPP_DTYPE.itemsize == 24
+SUPP_ENABLE = 1
 
 # every function declared in include/ptls_hip.h: (restype, argtypes)
 _vp, _sz, _i, _u64 = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_uint64
@@ -42,6 +45,8 @@ SIGNATURES = {
     "ptls_hip_batch_workgroup": (_i, [_vp]),
     "ptls_hip_aesgcm_seal_batch": (_i, [_vp, _vp, _vp, _vp, _vp, _vp]),
     "ptls_hip_aesgcm_open_batch": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "ptls_hip_aesgcm_seal_batch_supp": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "ptls_hip_aesecb_batch": (_i, [_vp, _vp, _vp, _sz, _vp, _vp, _vp]),
     "ptls_hip_fill_records": (_i, [_vp, _vp, _u64, _u64, _vp, _vp]),
     "ptls_hip_pipeline_new": (_vp, [_vp, _sz]),
     "ptls_hip_pipeline_free": (None, [_vp]),
@@ -50,7 +55,7 @@ SIGNATURES = {
     "ptls_hip_host_register": (_i, [_vp, _sz]),
     "ptls_hip_host_unregister": (_i, [_vp]),
 }
-DATA_SYMBOLS = ("ptls_hip_aes128gcm", "ptls_hip_aes256gcm")
+DATA_SYMBOLS = ("ptls_hip_aes128ctr", "ptls_hip_aes128gcm", "ptls_hip_aes256ctr", "ptls_hip_aes256gcm")
 
 _lib = None
 
@@ -116,6 +121,12 @@ class Engine:
     def cu_count(self):
         return lib().ptls_hip_engine_cu_count(self.ptr)
 
+    def aesecb(self, hp_keyset, supp, src, mask, stream=None):
+        """mask[mask_off] = AES-ECB(hp key, src[sample_off:+16]) for every enabled device descriptor"""
+        n = supp.numel() // SUPP_DTYPE.itemsize if hasattr(supp, "numel") else len(supp)
+        _check(lib().ptls_hip_aesecb_batch(self.ptr, hp_keyset.ptr, _ptr(supp), n, _ptr(src), _ptr(mask), _stream(stream)),
+               "aesecb_batch")
+
     def close(self):
         if self.ptr:
             lib().ptls_hip_engine_free(self.ptr)
@@ -130,9 +141,13 @@ class KeySet:
             raise HipError(f"ptls_hip_keyset_new: {last_error()}")
 
     def set(self, first, keys, ivs, stream=None):
-        keys, ivs = bytes(keys), bytes(ivs)
+        """ivs=None: zero static IVs (header-protection keys)"""
+        keys = bytes(keys)
         count = len(keys) // self.key_size
-        assert len(keys) == count * self.key_size and len(ivs) == count * 12
+        assert len(keys) == count * self.key_size
+        if ivs is not None:
+            ivs = bytes(ivs)
+            assert len(ivs) == count * 12
         _check(lib().ptls_hip_keyset_set(self.ptr, first, count, keys, ivs, _stream(stream)), "keyset_set")
 
     def get_iv(self, slot):
@@ -184,6 +199,11 @@ class Batch:
     def open(self, keyset, inp, aad, out, result, stream=None):
         _check(lib().ptls_hip_aesgcm_open_batch(self.ptr, keyset.ptr, _ptr(inp), _ptr(aad), _ptr(out), _ptr(result),
                                                 _stream(stream)), "open_batch")
+
+    def seal_supp(self, keyset, hp_keyset, supp, inp, aad, out, mask, stream=None):
+        """seal + QUIC header-protection masks in one launch; supp: device array of SUPP_DTYPE, one per record"""
+        _check(lib().ptls_hip_aesgcm_seal_batch_supp(self.ptr, keyset.ptr, hp_keyset.ptr, _ptr(supp), _ptr(inp), _ptr(aad),
+                                                     _ptr(out), _ptr(mask), _stream(stream)), "seal_batch_supp")
 
     def fill(self, buf, seed, index_base=0, index=None, stream=None):
         """index: optional device tensor (int64/uint64) of per-descriptor generator indices"""

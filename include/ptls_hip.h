@@ -48,6 +48,14 @@ const char *ptls_hip_last_error(void);
  * addition implement do_encrypt_v (fusion asserts "FIXME" there, lib/fusion.c:1145-1149). */
 extern ptls_aead_algorithm_t ptls_hip_aes128gcm, ptls_hip_aes256gcm;
 
+/* Replace ptls_fusion_aes128ctr / ptls_fusion_aes256ctr (lib/fusion.c:1050-1100, :1219-1230), the
+ * `ctr_cipher` of the AEAD objects above and the cipher QUIC stacks use for header protection.
+ * Same contract as fusion's: do_init(iv) computes one keystream block AES-ECB(key, iv) on the GPU, and
+ * the following do_transform XORs at most 16 bytes with it (fusion asserts the same, :1064-1077).
+ * When such a context is passed as `supp` to ptls_hip_aes*gcm's do_encrypt (ptls_aead_encrypt_s),
+ * the mask is computed inside the same kernel launch as the record, as fusion does (:636-650). */
+extern ptls_cipher_algorithm_t ptls_hip_aes128ctr, ptls_hip_aes256ctr;
+
 /* Device ordinal used by contexts created through the plugin objects (default 0; also read from
  * the environment variable PTLS_HIP_DEVICE).  Must be called before the first context is made. */
 int ptls_hip_set_default_device(int device);
@@ -72,8 +80,9 @@ int ptls_hip_engine_cu_count(ptls_hip_engine_t *engine);
 ptls_hip_keyset_t *ptls_hip_keyset_new(ptls_hip_engine_t *engine, size_t key_size, size_t nslots);
 void ptls_hip_keyset_free(ptls_hip_keyset_t *ks); /* zeroizes device key material */
 size_t ptls_hip_keyset_size(ptls_hip_keyset_t *ks);
-/* Load `count` keys (count * key_size bytes) and static IVs (count * 12 bytes) from host memory into
- * slots [first, first + count) and expand them on the device (key schedule, H = E_K(0), powers of H).
+/* Load `count` keys (count * key_size bytes) and static IVs (count * 12 bytes; NULL = zero IVs, e.g. for
+ * header-protection keys) from host memory into slots [first, first + count) and expand them on the
+ * device (key schedule, H = E_K(0), powers of H).
  * Equivalent to setup_crypto(ctx, is_enc, key, iv) for each slot (lib/fusion.c:1184-1206). */
 int ptls_hip_keyset_set(ptls_hip_keyset_t *ks, size_t first, size_t count, const void *keys, const void *ivs, void *stream);
 /* Static-IV get/set of one slot (do_get_iv / do_set_iv, lib/fusion.c:1168-1182); with
@@ -120,6 +129,30 @@ int ptls_hip_aesgcm_seal_batch(ptls_hip_batch_t *batch, ptls_hip_keyset_t *ks, c
                                void *stream);
 int ptls_hip_aesgcm_open_batch(ptls_hip_batch_t *batch, ptls_hip_keyset_t *ks, const void *in, const void *aad, void *out,
                                uint64_t *result, void *stream);
+
+/* QUIC header protection for a batch (RFC 9001 §5.4; fusion's `supp`, lib/fusion.c:424-428, :636-650).
+ * One descriptor per record (same index as the batch's descriptors): mask + mask_off receives the
+ * 16-byte AES-ECB(hp key slot `hp_key`, 16 bytes at sample_off) -- for seal the sample is read from
+ * `out` AFTER the record (ciphertext and tag) is written, so it may cover the tag, exactly like
+ * fusion's supplementary block.  Records with (flags & 1) == 0 are skipped.  The header-protection
+ * keyset must have the AEAD keyset's key size (fusion runs the supp block with the AEAD's rounds). */
+typedef struct st_ptls_hip_supp_t {
+    uint64_t sample_off;
+    uint64_t mask_off;
+    uint32_t hp_key;
+    uint32_t flags;
+} ptls_hip_supp_t;
+#define PTLS_HIP_SUPP_ENABLE 1u
+
+/* seal_batch + header-protection masks in the same launch; `supp` is a device array of batch_count. */
+int ptls_hip_aesgcm_seal_batch_supp(ptls_hip_batch_t *batch, ptls_hip_keyset_t *ks, ptls_hip_keyset_t *hp_ks,
+                                    const ptls_hip_supp_t *supp, const void *in, const void *aad, void *out, void *mask,
+                                    void *stream);
+/* Standalone masks (receive side: the sample is ciphertext in the received packet, needed before the
+ * packet number can be read and the record opened): mask + mask_off = AES-ECB(hp key, src + sample_off)
+ * for n device descriptors. */
+int ptls_hip_aesecb_batch(ptls_hip_engine_t *engine, ptls_hip_keyset_t *hp_ks, const ptls_hip_supp_t *supp, size_t n,
+                          const void *src, void *mask, void *stream);
 
 /* ------------------------------------------------------------------------------------------ *
  * 2b. host-resident records (records arrive in and leave through host memory: socket buffers)  *

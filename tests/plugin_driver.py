@@ -25,6 +25,16 @@ class AeadContext(c.Structure):  # include/picotls.h:444-494
                                             "do_decrypt")]
 
 
+class CipherContext(c.Structure):  # include/picotls.h:397-403
+    _fields_ = [(n, c.c_void_p) for n in ("algo", "do_dispose", "do_init", "do_transform")]
+
+
+class Supp(c.Structure):  # ptls_aead_supplementary_encryption_t, include/picotls.h:421-436
+    _fields_ = [("ctx", c.c_void_p), ("input", c.c_void_p), ("output", c.c_uint8 * 16)]
+
+
+CIPHER_INIT = c.CFUNCTYPE(None, c.c_void_p, c.c_void_p)
+CIPHER_TRANSFORM = c.CFUNCTYPE(None, c.c_void_p, c.c_void_p, c.c_void_p, c.c_size_t)
 ENCRYPT = c.CFUNCTYPE(None, c.c_void_p, c.c_void_p, c.c_void_p, c.c_size_t, c.c_uint64, c.c_void_p, c.c_size_t, c.c_void_p)
 ENCRYPT_V = c.CFUNCTYPE(None, c.c_void_p, c.c_void_p, c.POINTER(Iovec), c.c_size_t, c.c_uint64, c.c_void_p, c.c_size_t)
 DECRYPT = c.CFUNCTYPE(c.c_size_t, c.c_void_p, c.c_void_p, c.c_void_p, c.c_size_t, c.c_uint64, c.c_void_p, c.c_size_t)
@@ -38,8 +48,31 @@ class PluginDriver:
         self.ref.ptls_aead_new_direct.argtypes = [c.c_void_p, c.c_int, c.c_void_p, c.c_void_p]
         self.ref.ptls_aead_free.argtypes = [c.c_void_p]
         self.ref.ptls_aead_xor_iv.argtypes = [c.c_void_p, c.c_void_p, c.c_size_t]
+        self.ref.ptls_cipher_new.restype = c.c_void_p
+        self.ref.ptls_cipher_new.argtypes = [c.c_void_p, c.c_int, c.c_void_p]
+        self.ref.ptls_cipher_free.argtypes = [c.c_void_p]
         self.algos = {128: c.addressof(c.c_char.in_dll(hip, "ptls_hip_aes128gcm")),
                       256: c.addressof(c.c_char.in_dll(hip, "ptls_hip_aes256gcm"))}
+        self.ctr_algos = {128: c.addressof(c.c_char.in_dll(hip, "ptls_hip_aes128ctr")),
+                          256: c.addressof(c.c_char.in_dll(hip, "ptls_hip_aes256ctr"))}
+
+    def cipher_new(self, bits, key, is_enc=1):
+        """ptls_cipher_new (lib/picotls.c) on ptls_hip_aes{128,256}ctr"""
+        ctx = self.ref.ptls_cipher_new(self.ctr_algos[bits], is_enc, key)
+        assert ctx, "ptls_cipher_new returned NULL: " + ptls_hip.last_error()
+        return ctx
+
+    def cipher_free(self, ctx):
+        self.ref.ptls_cipher_free(ctx)
+
+    @staticmethod
+    def cipher_encrypt(ctx, iv, data):
+        """ptls_cipher_init + ptls_cipher_encrypt (include/picotls.h inline dispatchers)"""
+        vt = CipherContext.from_address(ctx)
+        CIPHER_INIT(vt.do_init)(ctx, iv)
+        out = c.create_string_buffer(max(len(data), 1))
+        CIPHER_TRANSFORM(vt.do_transform)(ctx, out, data, len(data))
+        return out.raw[:len(data)]
 
     def new(self, bits, key, iv, is_enc=1):
         ctx = self.ref.ptls_aead_new_direct(self.algos[bits], is_enc, key, iv)
@@ -60,6 +93,13 @@ class PluginDriver:
         out = c.create_string_buffer(len(pt) + 16)
         ENCRYPT(self._vt(ctx).do_encrypt)(ctx, out, pt, len(pt), seq, aad, len(aad), None)
         return out.raw
+
+    def encrypt_s(self, ctx, pt, seq, aad, supp_ctx, sample_off):
+        """ptls_aead_encrypt_s with a supplementary (header-protection) block sampled from the output"""
+        out = c.create_string_buffer(len(pt) + 16)
+        supp = Supp(supp_ctx, c.addressof(out) + sample_off)
+        ENCRYPT(self._vt(ctx).do_encrypt)(ctx, out, pt, len(pt), seq, aad, len(aad), c.byref(supp))
+        return out.raw, bytes(supp.output)
 
     def encrypt_v(self, ctx, parts, seq, aad):
         bufs = [c.create_string_buffer(p, max(len(p), 1)) for p in parts]

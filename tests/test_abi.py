@@ -23,7 +23,7 @@ def declared_functions():
 
 def declared_data():
     src = open(HEADER).read()
-    m = re.findall(r"extern\s+ptls_aead_algorithm_t\s+([^;]+);", src)
+    m = re.findall(r"extern\s+ptls_(?:aead|cipher)_algorithm_t\s+([^;]+);", src)
     return sorted(n.strip() for decl in m for n in decl.split(","))
 
 
@@ -80,6 +80,24 @@ def test_algorithm_objects_mirror_fusion():
         assert a.conf == 0x2000000 and a.integ == 0x40000000000000
         assert (a.fixed_iv, a.record_iv, a.bits & 1, a.align_bits) == (0, 0, 0, 0)
         assert a.context_size >= 80 and a.setup
+
+
+def test_ctr_objects_mirror_fusion():
+    """ptls_hip_aes{128,256}ctr vs ptls_fusion_aes{128,256}ctr (lib/fusion.c:1219-1230), and the AEAD
+    objects advertise them as ctr_cipher like fusion's do"""
+    L = ptls_hip.lib()
+
+    class Cipher(ctypes.Structure):  # include/picotls.h:408-415
+        _fields_ = [("name", ctypes.c_char_p), ("key_size", ctypes.c_size_t), ("block_size", ctypes.c_size_t),
+                    ("iv_size", ctypes.c_size_t), ("context_size", ctypes.c_size_t), ("setup", ctypes.c_void_p)]
+
+    for name, ks, label, aead in (("ptls_hip_aes128ctr", 16, b"AES128-CTR", "ptls_hip_aes128gcm"),
+                                  ("ptls_hip_aes256ctr", 32, b"AES256-CTR", "ptls_hip_aes256gcm")):
+        c = Cipher.in_dll(L, name)
+        assert (c.name, c.key_size, c.block_size, c.iv_size) == (label, ks, 1, 16)
+        assert c.context_size >= 32 and c.setup
+        ctr_field = ctypes.c_void_p.from_address(ctypes.addressof(ctypes.c_char.in_dll(L, aead)) + 24).value
+        assert ctr_field == ctypes.addressof(c)
 
 
 def _gpu_present():

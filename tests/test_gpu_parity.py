@@ -304,6 +304,129 @@ def test_plugin_through_reference_picotls(engine, oracle, golden):
             drv.free(ctx)
 
 
+def _supp_array(rows):
+    arr = np.zeros(len(rows), dtype=ptls_hip.SUPP_DTYPE)
+    for i, (sample_off, mask_off, hp_key, flags) in enumerate(rows):
+        arr[i] = (sample_off, mask_off, hp_key, flags)
+    return torch.from_numpy(arr.view(np.uint8)).cuda()
+
+
+@pytest.mark.parametrize("key_len", [16, 32])
+def test_seal_batch_quic_header_protection(engine, oracle, key_len):
+    """QUIC header protection fused into the seal launch (fusion's supp,
+    lib/fusion.c:424-428, :636-650).  Packets of 20-1500 B with 16-40 B headers as AAD, 3 AEAD keys,
+    2 header-protection keys, samples anywhere in ciphertext || tag (incl. covering the tag), some
+    records without HP.  Ciphertext == oracle, mask == AES-ECB(hp key, sample of the output)."""
+    rng = np.random.default_rng(key_len)
+    hp_keys = [rng.integers(0, 256, key_len, dtype=np.uint8).tobytes() for _ in range(2)]
+    recs = []
+    for i in range(600):
+        L = int(rng.integers(20, 1500))
+        key, iv = oracle.gen_key(i * 3 // 600, key_len)
+        recs.append((key, iv, 10_000 + i, oracle.stream(900 + i, int(rng.integers(16, 41))), oracle.stream(3000 + i, L)))
+    hb = HostBatch(engine, recs)
+    hp = ptls_hip.KeySet(engine, key_len, 2)
+    hp.set(0, b"".join(hp_keys), None)
+    rows, expect = [], []
+    for j, (r, rec) in enumerate(zip(recs, hb.recs)):
+        L = len(r[4])
+        off = int(rng.integers(0, L + 1)) if j % 5 else L  # j % 5 == 0: sample == the tag
+        enabled = j % 7 != 3
+        rows.append((int(rec["out_off"]) + off, 16 * j, j % 2, ptls_hip.SUPP_ENABLE if enabled else 0))
+        expect.append((off, j % 2, enabled))
+    d_supp = _supp_array(rows)
+    d_in = torch.from_numpy(hb._input([r[4] for r in recs])).cuda()
+    d_aad = torch.from_numpy(np.concatenate([hb.aad, np.zeros(16, np.uint8)])).cuda()
+    d_out = torch.zeros(hb.out_total + 32, dtype=torch.uint8, device="cuda")
+    d_mask = torch.zeros(16 * len(recs), dtype=torch.uint8, device="cuda")
+    hb.batch.seal_supp(hb.keyset, hp, d_supp, d_in, d_aad, d_out, d_mask)
+    torch.cuda.synchronize()
+    out, mask = d_out.cpu().numpy(), d_mask.cpu().numpy()
+    for j, (r, rec, (off, k, enabled)) in enumerate(zip(recs, hb.recs, expect)):
+        sealed = out[rec["out_off"]: rec["out_off"] + rec["len"] + 16].tobytes()
+        assert sealed == oracle.seal(*r), j
+        m = mask[16 * j: 16 * j + 16].tobytes()
+        assert m == (oracle.aes_ecb(hp_keys[k], sealed[off: off + 16]) if enabled else bytes(16)), j
+    hp.close()
+    hb.close()
+
+
+def test_supp_kats_gcm_test_vectors(engine, golden):
+    """t/fusion.c gcm_test_vectors (:289-343): supp = AES-ECB(01 x 16, output[2:18]) in the same launch"""
+    tv = golden["kats"]["gcm_test_vectors"]
+    recs = [(bytes(16), bytes(12), 0, bytes(v["aadlen"]), bytes(v["ptlen"])) for v in tv]
+    hb = HostBatch(engine, recs)
+    hp = ptls_hip.KeySet(engine, 16, 1)
+    hp.set(0, b"\x01" * 16, None)
+    d_supp = _supp_array([(int(rec["out_off"]) + 2, 16 * j, 0, ptls_hip.SUPP_ENABLE) for j, rec in enumerate(hb.recs)])
+    d_in = torch.from_numpy(hb._input([r[4] for r in recs])).cuda()
+    d_aad = torch.from_numpy(np.concatenate([hb.aad, np.zeros(16, np.uint8)])).cuda()
+    d_out = torch.zeros(hb.out_total + 32, dtype=torch.uint8, device="cuda")
+    d_mask = torch.zeros(16 * len(recs), dtype=torch.uint8, device="cuda")
+    hb.batch.seal_supp(hb.keyset, hp, d_supp, d_in, d_aad, d_out, d_mask)
+    torch.cuda.synchronize()
+    out, mask = d_out.cpu().numpy(), d_mask.cpu().numpy()
+    for j, (v, rec) in enumerate(zip(tv, hb.recs)):
+        assert out[rec["out_off"] + v["ptlen"]: rec["out_off"] + v["ptlen"] + 16].tobytes().hex() == v["tag"]
+        assert mask[16 * j: 16 * j + 16].tobytes().hex() == v["supp"], v
+    hp.close()
+    hb.close()
+
+
+@pytest.mark.parametrize("key_len", [16, 32])
+def test_aesecb_batch_receive_side(engine, oracle, key_len):
+    """receive side of header protection: masks from samples of received ciphertext, many hp keys"""
+    rng = np.random.default_rng(100 + key_len)
+    nkeys, n = 37, 5000
+    keys = rng.integers(0, 256, (nkeys, key_len), dtype=np.uint8)
+    hp = ptls_hip.KeySet(engine, key_len, nkeys)
+    hp.set(0, keys.tobytes(), None)
+    src = rng.integers(0, 256, 70_000, dtype=np.uint8)
+    rows = [(int(rng.integers(0, len(src) - 16)), 16 * j, int(rng.integers(0, nkeys)), ptls_hip.SUPP_ENABLE)
+            for j in range(n)]
+    d_mask = torch.zeros(16 * n, dtype=torch.uint8, device="cuda")
+    engine.aesecb(hp, _supp_array(rows), torch.from_numpy(src).cuda(), d_mask)
+    torch.cuda.synchronize()
+    mask = d_mask.cpu().numpy()
+    for j, (so, mo, k, _) in enumerate(rows):
+        assert mask[mo: mo + 16].tobytes() == oracle.aes_ecb(keys[k].tobytes(), src[so: so + 16].tobytes()), j
+    hp.close()
+
+
+def test_plugin_ctr_cipher_and_fused_supp(engine, oracle):
+    """ptls_hip_aes{128,256}ctr through the reference's ptls_cipher_new (lib/picotls.c), and
+    ptls_aead_encrypt_s with it as supp: output and supp block equal lib/fusion.c's (ref_seal_supp uses
+    ptls_fusion_aes*ctr the same way, t/fusion.c:321-331)"""
+    from oracle_lib import Ref
+    if not Ref.available:
+        pytest.skip("oracle/_ref not built")
+    import plugin_driver
+    drv = plugin_driver.PluginDriver()
+    ref = Ref()
+    rng = np.random.default_rng(8)
+    for bits in (128, 256):
+        hp_key = rng.integers(0, 256, bits // 8, dtype=np.uint8).tobytes()
+        cctx = drv.cipher_new(bits, hp_key)
+        for _ in range(5):
+            iv = rng.integers(0, 256, 16, dtype=np.uint8).tobytes()
+            ks = oracle.aes_ecb(hp_key, iv)
+            assert drv.cipher_encrypt(cctx, iv, bytes(16)) == ks
+            data = rng.integers(0, 256, 5, dtype=np.uint8).tobytes()  # a QUIC header mask use: 5 bytes
+            assert drv.cipher_encrypt(cctx, iv, data) == bytes(a ^ b for a, b in zip(data, ks))
+        key = rng.integers(0, 256, bits // 8, dtype=np.uint8).tobytes()
+        iv = rng.integers(0, 256, 12, dtype=np.uint8).tobytes()
+        actx = drv.new(bits, key, iv)
+        for L in (20, 100, 1200):
+            text = rng.integers(0, 256, L, dtype=np.uint8).tobytes()
+            aad = rng.integers(0, 256, 20, dtype=np.uint8).tobytes()
+            for off in (0, 3, L):  # L: the sample is the tag
+                out, supp = drv.encrypt_s(actx, text, 77, aad, cctx, off)
+                ref_out, ref_supp = ref.seal_supp(key, iv, 77, aad, text, hp_key, off)
+                assert out == ref_out and supp == ref_supp, (bits, L, off)
+        drv.free(actx)
+        drv.cipher_free(cctx)
+
+
 @pytest.mark.parametrize("slice_kib", [64, 1024])
 def test_host_pipeline_seal_open(engine, oracle, slice_kib):
     """host-resident path: records in pinned host memory, sliced, H2D -> kernel -> D2H over 3 streams;
