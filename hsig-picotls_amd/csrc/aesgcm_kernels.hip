@@ -474,6 +474,24 @@ __device__ void build_ghash_tables(uint8_t *lds, const uint32_t *__restrict__ ba
 
 /* ---------------- global-memory block access ---------------- */
 
+/* A whole 16-byte block at any byte address: gfx9+ global memory instructions handle unaligned
+ * addresses (the ROCm default unaligned access mode), so an align(1) vector type still compiles to ONE
+ * global_load/store_dwordx4.  Only whole blocks (all 16 bytes inside the record) go through these. */
+struct __attribute__((packed, aligned(1))) U4u {
+    uint32_t x, y, z, w;
+};
+
+__device__ __forceinline__ V4 load_full(const uint8_t *p)
+{
+    const U4u v = *reinterpret_cast<const U4u *>(p);
+    return V4{v.x, v.y, v.z, v.w};
+}
+
+__device__ __forceinline__ void store_full(uint8_t *p, V4 v)
+{
+    *reinterpret_cast<U4u *>(p) = U4u{v.w0, v.w1, v.w2, v.w3};
+}
+
 /* 128-bit shifts by one byte (raw byte order: w0 holds bytes 0..3) */
 __device__ __forceinline__ V4 shr8(V4 v)
 {
@@ -514,18 +532,17 @@ template <bool ALIGNED>
 __device__ __forceinline__ V4 load_block(const uint8_t *p, int n)
 {
     if (ALIGNED) {
-        const uint4 v = *reinterpret_cast<const uint4 *>(p);
-        const V4 r = V4{v.x, v.y, v.z, v.w};
+        const V4 r = load_full(p);
         return n == 16 ? r : mask_block(r, n);
     }
-    return load_bytes(p, n);
+    return n == 16 ? load_full(p) : load_bytes(p, n);
 }
 
 template <bool ALIGNED>
 __device__ __forceinline__ void store_block(uint8_t *p, int n, V4 v)
 {
-    if (ALIGNED && n == 16) {
-        *reinterpret_cast<uint4 *>(p) = make_uint4(v.w0, v.w1, v.w2, v.w3);
+    if (n == 16) {
+        store_full(p, v);
         return;
     }
     store_bytes(p, n, v);
@@ -678,7 +695,7 @@ __global__ void __launch_bounds__(WGT)
             const int my_mlo = na > i0 ? (na - i0 + G - 1) >> LOG2G : 0;
             /* full blocks only, and (for the counter-mode shortcut) block counters c + 2 < 2^16 */
             const int lastc = min(nf, 65534) - 1; /* last data block index allowed in the pure stretch */
-            const int my_mhi = (ALIGNED && valid && na + lastc - i0 >= 0) ? ((na + lastc - i0) >> LOG2G) + 1 : 0;
+            const int my_mhi = (valid && na + lastc - i0 >= 0) ? ((na + lastc - i0) >> LOG2G) + 1 : 0;
             const int pm0 = wave_max(my_mlo);
             const int pm_hi = -wave_max(-my_mhi);
             const int npure = pm_hi > pm0 ? (pm_hi - pm0) / KP : 0;
@@ -699,7 +716,7 @@ __global__ void __launch_bounds__(WGT)
                  * named buffers instead of a copy keep the compiler from waiting on the fresh loads. */
 #pragma unroll
                 for (int b = 0; b < KP; ++b)
-                    bufA[b] = load_block<true>(src + 16 * b * G, 16);
+                    bufA[b] = load_full(src + 16 * b * G);
                 /* one branch-free iteration; `hash_pending` is a literal at every call site */
                 auto pure_iter = [&](int it, bool hash_pending, V4(&d)[KP], V4(&dn)[KP]) {
                     const size_t o = (size_t)(it * KP * G) * 16;
@@ -708,7 +725,7 @@ __global__ void __launch_bounds__(WGT)
                     uint32_t cw[KP];
 #pragma unroll
                     for (int b = 0; b < KP; ++b) {
-                        dn[b] = load_block<true>(src + on + 16 * b * G, 16);
+                        dn[b] = load_full(src + on + 16 * b * G);
                         cw[b] = bswap32(cbase + (uint32_t)((it * KP + b) * G));
                         k[b] = V4{n0, n1, n2, cw[b]};
                     }
@@ -728,7 +745,7 @@ __global__ void __launch_bounds__(WGT)
                             y = gh_mul_main(lds, LANE_FRESH, y, d[b]);
 #pragma unroll
                         for (int b = 0; b < KP; ++b)
-                            store_block<true>(dst + o + 16 * b * G, 16, v4xor(d[b], k[b]));
+                            store_full(dst + o + 16 * b * G, v4xor(d[b], k[b]));
                     } else {
                         /* software pipelined: the ciphertext of iteration it is hashed during iteration it + 1 */
                         if (hash_pending) {
@@ -743,7 +760,7 @@ __global__ void __launch_bounds__(WGT)
 #pragma unroll
                         for (int b = 0; b < KP; ++b) {
                             pend[b] = v4xor(d[b], k[b]);
-                            store_block<true>(dst + o + 16 * b * G, 16, pend[b]);
+                            store_full(dst + o + 16 * b * G, pend[b]);
                         }
                     }
                 };
@@ -783,16 +800,12 @@ __global__ void __launch_bounds__(WGT)
             if (valid && q == 0) {
                 const V4 s = gh_mul_nibble(lds, LDS_GTREE, y); /* * H */
                 const V4 tag = v4xor(s, ek0);
-                const bool tag_fast = ALIGNED && (L & 15) == 0;
                 if (OPEN) {
-                    const V4 rt = tag_fast ? load_block<true>(in_p + L, 16) : load_bytes(in_p + L, 16);
+                    const V4 rt = load_full(in_p + L);
                     const bool ok = rt.w0 == tag.w0 && rt.w1 == tag.w1 && rt.w2 == tag.w2 && rt.w3 == tag.w3;
                     result[rec_i] = ok ? (uint64_t)L : ~(uint64_t)0;
                 } else {
-                    if (tag_fast)
-                        store_block<true>(out_p + L, 16, tag);
-                    else
-                        store_bytes(out_p + L, 16, tag);
+                    store_full(out_p + L, tag);
                 }
             }
             if (!OPEN && supp != nullptr) {
@@ -805,9 +818,9 @@ __global__ void __launch_bounds__(WGT)
                 if (valid && r == 0) {
                     const ptls_hip_supp_t sp = supp[rec_i];
                     if (sp.flags & PTLS_HIP_SUPP_ENABLE) {
-                        const V4 sample = load_bytes(out + sp.sample_off, 16);
+                        const V4 sample = load_full(out + sp.sample_off);
                         const V4 m = aes_encrypt<ROUNDS>(lds, lb_aes, hp_slots[sp.hp_key].rk, sample);
-                        store_bytes(mask + sp.mask_off, 16, m);
+                        store_full(mask + sp.mask_off, m);
                     }
                 }
             }
@@ -829,8 +842,8 @@ __global__ void __launch_bounds__(256) aesecb_batch_kernel(const ptls_hip_supp_t
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
         const ptls_hip_supp_t sp = supp[i];
         if (sp.flags & PTLS_HIP_SUPP_ENABLE) {
-            const V4 m = aes_encrypt<ROUNDS>(lds, lb_aes, hp_slots[sp.hp_key].rk, load_bytes(src + sp.sample_off, 16));
-            store_bytes(mask + sp.mask_off, 16, m);
+            const V4 m = aes_encrypt<ROUNDS>(lds, lb_aes, hp_slots[sp.hp_key].rk, load_full(src + sp.sample_off));
+            store_full(mask + sp.mask_off, m);
         }
     }
 }

@@ -12,11 +12,17 @@ ap.add_argument("--configs", default="c2,c3,c4")
 ap.add_argument("--lanes", default="1,2,4,8")
 ap.add_argument("--wg", default="512,768")
 ap.add_argument("--reps", type=int, default=4)
+ap.add_argument("--pack", type=int, default=0, help="re-lay records out at this byte alignment (1 = packed)")
 args = ap.parse_args()
 eng = ptls_hip.Engine(0)
 for name in args.configs.split(","):
     cfg = bench.CONFIGS[name]
     idx, recs, in_total, out_total, lens = bench.make_workload(cfg, 0)
+    if args.pack:
+        aad_len = 5 if cfg["aad"] == "tls" else 13
+        r2, in_total, out_total, _ = ptls_hip.layout_records(recs["len"], recs["aad_len"], recs["key"], recs["seq"], align=args.pack)
+        r2["aad_off"] = recs["aad_off"]
+        recs = r2
     n = len(recs); sumL = int(lens.sum())
     ks = ptls_hip.KeySet(eng, cfg["key_len"], cfg["keys"]); ks.set(0, *bench.make_keys(cfg))
     b = ptls_hip.Batch(eng, recs)
