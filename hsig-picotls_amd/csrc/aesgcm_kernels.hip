@@ -561,6 +561,14 @@ __device__ __forceinline__ V4 mask_block(V4 v, int n)
     return V4{o[0], o[1], o[2], o[3]};
 }
 
+/* v with byte `pos` (0..15, currently zero) set to b */
+__device__ __forceinline__ V4 put_byte(V4 v, int pos, uint32_t b)
+{
+    const uint32_t x = b << (8 * (pos & 3));
+    const int w = pos >> 2;
+    return V4{v.w0 | (w == 0 ? x : 0u), v.w1 | (w == 1 ? x : 0u), v.w2 | (w == 2 ? x : 0u), v.w3 | (w == 3 ? x : 0u)};
+}
+
 __device__ __forceinline__ int wave_max(int v)
 {
 #pragma unroll
@@ -665,6 +673,9 @@ __global__ void __launch_bounds__(WGT)
             const int my_iters = i0 < N ? ((N - 1 - i0) >> LOG2G) + 1 : 0;
             const int iters = wave_max(my_iters);
 
+            /* seal of a TLS 1.3 record: the last plaintext byte is the content type, not input */
+            const bool tflag = !OPEN && (rec.flags & 1u) != 0 && L > 0;
+            const uint32_t ttype = (rec.flags >> 8) & 0xffu;
             const uint8_t *in_p = in + rec.in_off;
             uint8_t *out_p = out + rec.out_off;
             const uint8_t *aad_p = aad + rec.aad_off;
@@ -677,8 +688,12 @@ __global__ void __launch_bounds__(WGT)
             auto generic_iter_m = [&](int m) {
                 const Elem e0 = elem_of(i0 + m * G, N, na, nc, L);
                 V4 in0 = V4{0, 0, 0, 0};
-                if (e0.is_c)
-                    in0 = load_block<ALIGNED>(in_p + 16 * (size_t)e0.c, e0.nbytes);
+                if (e0.is_c) {
+                    const bool tb = tflag && e0.c == nc - 1; /* the block holding the content-type byte */
+                    in0 = load_block<ALIGNED>(in_p + 16 * (size_t)e0.c, e0.nbytes - (tb ? 1 : 0));
+                    if (tb)
+                        in0 = put_byte(in0, e0.nbytes - 1, ttype);
+                }
                 /* keystream for data block c (counter inc32(J0) + c), E_K(J0) for the length-block lane */
                 V4 ks0[1] = {V4{n0, n1, n2, e0.is_c ? bswap32((uint32_t)e0.c + 2u) : 0x01000000u}};
                 aes_encrypt_n<ROUNDS, 1>(lds, lb_aes, rk, ks0);
@@ -691,7 +706,7 @@ __global__ void __launch_bounds__(WGT)
              * There the body is branch-free and handles KP blocks per iteration, so their AES lookups and the
              * GHASH lookups of the previous iteration's ciphertext can all be in flight together. */
             constexpr int KP = PURE_BLOCKS;
-            const int nf = L >> 4;
+            const int nf = (L - (tflag ? 1 : 0)) >> 4; /* full blocks that are all input bytes */
             const int my_mlo = na > i0 ? (na - i0 + G - 1) >> LOG2G : 0;
             /* full blocks only, and (for the counter-mode shortcut) block counters c + 2 < 2^16 */
             const int lastc = min(nf, 65534) - 1; /* last data block index allowed in the pure stretch */
@@ -825,6 +840,49 @@ __global__ void __launch_bounds__(WGT)
                 }
             }
         }
+    }
+}
+
+/* TLS 1.3 record headers (build_aad, lib/picotls.c:696-703): 17 03 03 BE16(len + 16) at hdr + aad_off of
+ * every record flagged PTLS_HIP_RECORD_TLS13_TYPE; the seal kernel then reads them back as the AAD. */
+__global__ void __launch_bounds__(256) tls13_header_kernel(const ptls_hip_record_t *__restrict__ recs, uint32_t n, uint8_t *hdr)
+{
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        const ptls_hip_record_t r = recs[i];
+        if (r.flags & 1u) {
+            const uint32_t reclen = r.len + 16u;
+            uint8_t *h = hdr + r.aad_off;
+            h[0] = 0x17;
+            h[1] = 0x03;
+            h[2] = 0x03;
+            h[3] = (uint8_t)(reclen >> 8);
+            h[4] = (uint8_t)reclen;
+        }
+    }
+}
+
+/* TLSInnerPlaintext of opened records (handle_input, lib/picotls.c:5877-5883): skip trailing zero padding,
+ * the last non-zero byte is the content type; result = content length | type << 56. */
+__global__ void __launch_bounds__(256) tls13_inner_kernel(const ptls_hip_record_t *__restrict__ recs, uint32_t n,
+                                                          const uint8_t *__restrict__ out, uint64_t *__restrict__ result)
+{
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        if (result[i] == ~(uint64_t)0)
+            continue; /* bad record MAC */
+        const ptls_hip_record_t r = recs[i];
+        const uint8_t *p = out + r.out_off;
+        int64_t k = (int64_t)r.len;
+        uint32_t type = 0;
+        /* 16 bytes at a time while a whole block lies inside the record, then byte by byte */
+        while (k >= 16) {
+            const V4 v = load_full(p + k - 16);
+            if ((v.w0 | v.w1 | v.w2 | v.w3) != 0)
+                break;
+            k -= 16;
+        }
+        while (k > 0 && (type = p[k - 1]) == 0)
+            --k;
+        result[i] = k == 0 ? ~(uint64_t)1 : (uint64_t)(k - 1) | ((uint64_t)type << 56);
     }
 }
 
@@ -1109,6 +1167,18 @@ int launch_fill(const ptls_hip_record_t *recs, uint32_t n, uint8_t *buf, uint64_
 {
     hipLaunchKernelGGL(fill_records_kernel, dim3(grid), dim3(256), 0, static_cast<hipStream_t>(stream), recs, n, buf, seed,
                        index_base, index);
+    return (int)hipGetLastError();
+}
+
+int launch_tls13_headers(const ptls_hip_record_t *recs, uint32_t n, uint8_t *hdr, unsigned grid, void *stream)
+{
+    hipLaunchKernelGGL(tls13_header_kernel, dim3(grid), dim3(256), 0, static_cast<hipStream_t>(stream), recs, n, hdr);
+    return (int)hipGetLastError();
+}
+
+int launch_tls13_inner(const ptls_hip_record_t *recs, uint32_t n, const uint8_t *out, uint64_t *result, unsigned grid, void *stream)
+{
+    hipLaunchKernelGGL(tls13_inner_kernel, dim3(grid), dim3(256), 0, static_cast<hipStream_t>(stream), recs, n, out, result);
     return (int)hipGetLastError();
 }
 

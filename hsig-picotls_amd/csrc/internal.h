@@ -68,6 +68,8 @@ int launch_keysetup(KeySlot *slots, uint32_t *basis, const uint8_t *keys, const 
                     int key_size, const uint32_t *t0, void *stream);
 int launch_aesecb(int rounds, const ptls_hip_supp_t *supp, uint32_t n, const uint8_t *src, uint8_t *mask, const KeySlot *hp_slots,
                   const uint32_t *t0, unsigned grid, void *stream);
+int launch_tls13_headers(const ptls_hip_record_t *recs, uint32_t n, uint8_t *hdr, unsigned grid, void *stream);
+int launch_tls13_inner(const ptls_hip_record_t *recs, uint32_t n, const uint8_t *out, uint64_t *result, unsigned grid, void *stream);
 int launch_fill(const ptls_hip_record_t *recs, uint32_t n, uint8_t *buf, uint64_t seed, uint64_t index_base,
                 const uint64_t *index, unsigned grid, void *stream);
 

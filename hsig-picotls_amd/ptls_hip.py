@@ -19,6 +19,16 @@ assert RECORD_DTYPE.itemsize == 48
 SUPP_DTYPE = np.dtype([("sample_off", "<u8"), ("mask_off", "<u8"), ("hp_key", "<u4"), ("flags", "<u4")])
 assert SUPP_DTYPE.itemsize == 24
 SUPP_ENABLE = 1
+TLS13_MESSAGE_DTYPE = np.dtype([("in_off", "<u8"), ("out_off", "<u8"), ("seq", "<u8"), ("len", "<u4"), ("key", "<u4"),
+                                ("type", "<u4"), ("reserved", "<u4")])
+assert TLS13_MESSAGE_DTYPE.itemsize == 40
+TLS13_BAD_RECORD_MAC = (1 << 64) - 1
+TLS13_NO_CONTENT_TYPE = (1 << 64) - 2
+TLS13_DECODE_ERROR = -50
+
+
+def record_tls13_type(t):
+    return 1 | ((t & 0xFF) << 8)
 
 # every function declared in include/ptls_hip.h: (restype, argtypes)
 _vp, _sz, _i, _u64 = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_uint64
@@ -48,6 +58,12 @@ SIGNATURES = {
     "ptls_hip_aesgcm_seal_batch_supp": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "ptls_hip_aesecb_batch": (_i, [_vp, _vp, _vp, _sz, _vp, _vp, _vp]),
     "ptls_hip_fill_records": (_i, [_vp, _vp, _u64, _u64, _vp, _vp]),
+    "ptls_hip_tls13_wire_size": (_sz, [_sz]),
+    "ptls_hip_tls13_frame": (_sz, [_vp, _sz, _vp, _sz]),
+    "ptls_hip_tls13_seal_batch": (_i, [_vp, _vp, _vp, _vp, _vp]),
+    "ptls_hip_tls13_parse": (_i, [_vp, _sz, _u64, ctypes.c_uint32, _u64, _u64, _vp, _sz, ctypes.POINTER(_sz),
+                                  ctypes.POINTER(_sz)]),
+    "ptls_hip_tls13_open_batch": (_i, [_vp, _vp, _vp, _vp, _vp, _vp]),
     "ptls_hip_pipeline_new": (_vp, [_vp, _sz]),
     "ptls_hip_pipeline_free": (None, [_vp]),
     "ptls_hip_pipeline_seal": (_i, [_vp, _vp, _vp, _sz, _vp, _vp, _vp]),
@@ -205,6 +221,15 @@ class Batch:
         _check(lib().ptls_hip_aesgcm_seal_batch_supp(self.ptr, keyset.ptr, hp_keyset.ptr, _ptr(supp), _ptr(inp), _ptr(aad),
                                                      _ptr(out), _ptr(mask), _stream(stream)), "seal_batch_supp")
 
+    def tls13_seal(self, keyset, inp, out, stream=None):
+        """records from tls13_frame(): writes headers into `out`, then seals with them as AAD"""
+        _check(lib().ptls_hip_tls13_seal_batch(self.ptr, keyset.ptr, _ptr(inp), _ptr(out), _stream(stream)), "tls13_seal_batch")
+
+    def tls13_open(self, keyset, inp, out, result, stream=None):
+        """records from tls13_parse(): result = content length | type << 56, or TLS13_BAD_RECORD_MAC / NO_CONTENT_TYPE"""
+        _check(lib().ptls_hip_tls13_open_batch(self.ptr, keyset.ptr, _ptr(inp), _ptr(out), _ptr(result), _stream(stream)),
+               "tls13_open_batch")
+
     def fill(self, buf, seed, index_base=0, index=None, stream=None):
         """index: optional device tensor (int64/uint64) of per-descriptor generator indices"""
         _check(lib().ptls_hip_fill_records(self.ptr, _ptr(buf), seed, index_base, _ptr(index), _stream(stream)),
@@ -239,6 +264,26 @@ class Pipeline:
         if self.ptr:
             lib().ptls_hip_pipeline_free(self.ptr)
             self.ptr = None
+
+
+def tls13_frame(msgs):
+    """messages (TLS13_MESSAGE_DTYPE) -> record descriptors, picotls's 16384-byte chunking"""
+    msgs = np.ascontiguousarray(msgs, dtype=TLS13_MESSAGE_DTYPE)
+    n = lib().ptls_hip_tls13_frame(msgs.ctypes.data, len(msgs), None, 0)
+    recs = np.zeros(n, dtype=RECORD_DTYPE)
+    assert lib().ptls_hip_tls13_frame(msgs.ctypes.data, len(msgs), recs.ctypes.data, n) == n
+    return recs
+
+
+def tls13_parse(wire, wire_off=0, key=0, seq=0, out_base=0, cap=1 << 20):
+    """(recs, consumed) for the complete application-data records at the start of `wire` (bytes)"""
+    recs = np.zeros(cap, dtype=RECORD_DTYPE)
+    nrecs, consumed = ctypes.c_size_t(), ctypes.c_size_t()
+    rc = lib().ptls_hip_tls13_parse(bytes(wire), len(wire), wire_off, key, seq, out_base, recs.ctypes.data, cap,
+                                    ctypes.byref(nrecs), ctypes.byref(consumed))
+    if rc != 0:
+        raise HipError(f"tls13_parse: {last_error()} (rc={rc})")
+    return recs[: nrecs.value].copy(), consumed.value
 
 
 def layout_records(lens, aad_lens, keys, seqs, align=16, tag_in_input=False):

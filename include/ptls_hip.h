@@ -109,8 +109,11 @@ typedef struct st_ptls_hip_record_t {
     uint32_t len;
     uint32_t aad_len;
     uint32_t key;   /* key slot index */
-    uint32_t flags; /* reserved, must be 0 */
+    uint32_t flags; /* 0, or PTLS_HIP_RECORD_TLS13_TYPE(type) (seal: TLS 1.3 inner content type, see 2c) */
 } ptls_hip_record_t;
+/* seal only: the record's plaintext is the len - 1 input bytes followed by the content-type byte `type`
+ * (TLSInnerPlaintext without padding, RFC 8446 §5.2; picotls's aead_encrypt, lib/picotls.c:705-715) */
+#define PTLS_HIP_RECORD_TLS13_TYPE(type) (1u | ((uint32_t)(uint8_t)(type) << 8))
 
 /* Upload `n` host descriptors and plan the launch (runs of equal key slot, lane-group width from the
  * record lengths).  A batch is reusable for any number of seal/open calls over same-shaped buffers. */
@@ -155,7 +158,54 @@ int ptls_hip_aesecb_batch(ptls_hip_engine_t *engine, ptls_hip_keyset_t *hp_ks, c
                           const void *src, void *mask, void *stream);
 
 /* ------------------------------------------------------------------------------------------ *
- * 2b. host-resident records (records arrive in and leave through host memory: socket buffers)  *
+ * 2b. TLS 1.3 record layer over the batch                      *
+ * ------------------------------------------------------------------------------------------ */
+
+#define PTLS_HIP_TLS13_MAX_PLAINTEXT 16384         /* PTLS_MAX_PLAINTEXT_RECORD_SIZE, lib/picotls.c:42 */
+#define PTLS_HIP_TLS13_MAX_ENCRYPTED (16384 + 256) /* PTLS_MAX_ENCRYPTED_RECORD_SIZE, lib/picotls.c:43 */
+/* wire bytes of one message of `len` payload bytes: ceil(len / 16384) records of 5 + chunk + 1 + 16 */
+size_t ptls_hip_tls13_wire_size(size_t len);
+
+/* Send side.  A message = `len` bytes of one content type for one connection (key slot); like
+ * buffer_push_encrypted_records (lib/picotls.c:747-794) it is cut into records of at most 16384 bytes,
+ * record j carrying seq + j, all written back to back at out + out_off as
+ *     17 03 03 BE16(chunk + 17) || AES-GCM(chunk || type, AAD = that 5-byte header) || tag
+ * (build_aad and aead_encrypt, lib/picotls.c:696-715).  len == 0 produces no record. */
+typedef struct st_ptls_hip_tls13_message_t {
+    uint64_t in_off;  /* payload in the `in` buffer */
+    uint64_t out_off; /* first wire byte in the `out` buffer */
+    uint64_t seq;     /* sequence number of the first record */
+    uint32_t len;
+    uint32_t key;  /* key slot */
+    uint32_t type; /* content type (PTLS_CONTENT_TYPE_APPDATA = 23, handshake 22, alert 21) */
+    uint32_t reserved;
+} ptls_hip_tls13_message_t;
+/* Host-side planning: fills up to `cap` record descriptors (aad_off = header position in `out`) and
+ * returns the number of records the messages need (call with recs == NULL to size the array). */
+size_t ptls_hip_tls13_frame(const ptls_hip_tls13_message_t *msgs, size_t n, ptls_hip_record_t *recs, size_t cap);
+/* Writes the record headers into `out`, then seals every record (AAD read from the headers). */
+int ptls_hip_tls13_seal_batch(ptls_hip_batch_t *batch, ptls_hip_keyset_t *ks, const void *in, void *out, void *stream);
+
+/* Receive side.  Parses complete TLS records from a received byte stream on the host, like
+ * parse_record_header (lib/picotls.c:5020-5031): application-data records (type 23) of at most
+ * 16384 + 256 bytes become descriptors {aad_off = header, in_off = header + 5, len = length - 16,
+ * seq = seq + i, key, out_off = out_base + plaintext position}.  Stops before the first incomplete record
+ * or non-application-data record; *consumed = wire bytes parsed, *nrecs = records produced.
+ * Returns 0, or PTLS_HIP_TLS13_DECODE_ERROR for an oversized record or one shorter than a tag. */
+#define PTLS_HIP_TLS13_DECODE_ERROR (-50) /* -PTLS_ALERT_DECODE_ERROR */
+int ptls_hip_tls13_parse(const void *wire, size_t wire_len, uint64_t wire_off, uint32_t key, uint64_t seq, uint64_t out_base,
+                         ptls_hip_record_t *recs, size_t cap, size_t *nrecs, size_t *consumed);
+/* Opens the records (AAD = their wire headers in `in`), strips the TLSInnerPlaintext padding and reads
+ * the content type, like handle_input (lib/picotls.c:5866-5883).  result[i] = content length |
+ * (uint64_t)type << 56, or PTLS_HIP_TLS13_BAD_RECORD_MAC (authentication failure), or
+ * PTLS_HIP_TLS13_NO_CONTENT_TYPE (all-zero plaintext: PTLS_ALERT_UNEXPECTED_MESSAGE in picotls). */
+#define PTLS_HIP_TLS13_BAD_RECORD_MAC UINT64_MAX
+#define PTLS_HIP_TLS13_NO_CONTENT_TYPE (UINT64_MAX - 1)
+int ptls_hip_tls13_open_batch(ptls_hip_batch_t *batch, ptls_hip_keyset_t *ks, const void *in, void *out, uint64_t *result,
+                              void *stream);
+
+/* ------------------------------------------------------------------------------------------ *
+ * 2c. host-resident records (records arrive in and leave through host memory: socket buffers)  *
  * ------------------------------------------------------------------------------------------ */
 
 /* A pipeline owns three device staging slots of `slice_bytes` each and three streams.  seal/open

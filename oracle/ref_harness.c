@@ -153,3 +153,131 @@ double ref_bench(int bits, int do_open, const void *key, const void *iv, void *i
     pthread_barrier_destroy(&bar);
     return mx;
 }
+
+/* ---------------------------------------------------------------------------------------------- *
+ * TLS 1.3 record layer of the reference: a post-handshake ptls_t  *
+ * made by ptls_import (lib/picotls.c:5334-5432) from traffic secrets, then ptls_send /            *
+ * ptls_receive (:6121-6145, :6061-6097).  The AEAD is minicrypto's, or any ptls_aead_algorithm_t  *
+ * the caller passes (the HIP engine's, for the drop-in test); the hash is minicrypto's SHA-256/384 *
+ * (lib/cifra/aes128.c, aes256.c), compiled unmodified.                                            *
+ * ---------------------------------------------------------------------------------------------- */
+#include "picotls/minicrypto.h"
+
+struct ref_tls13 {
+    ptls_context_t ctx;
+    struct st_ptls_cipher_suite_t suite; /* ptls_cipher_suite_t is the const-qualified typedef */
+    ptls_cipher_suite_t *suites[2];
+    ptls_t *tls;
+};
+
+static void ref_random_bytes(void *buf, size_t len)
+{
+    memset(buf, 0x5a, len); /* client_random only; irrelevant to the record layer */
+}
+
+static void put16(uint8_t **p, uint16_t v)
+{
+    (*p)[0] = (uint8_t)(v >> 8);
+    (*p)[1] = (uint8_t)v;
+    *p += 2;
+}
+
+static void put64(uint8_t **p, uint64_t v)
+{
+    for (int i = 0; i < 8; ++i)
+        (*p)[i] = (uint8_t)(v >> (56 - 8 * i));
+    *p += 8;
+}
+
+/* bits 128 -> TLS_AES_128_GCM_SHA256, 256 -> TLS_AES_256_GCM_SHA384.  aead NULL -> minicrypto's AES-GCM
+ * (lib/cifra/aes{128,256}.c): fusion's own do_encrypt_v is an assert stub (lib/fusion.c:1145-1149), so
+ * ptls_send cannot run on it -- the gap SURVEY.md §8(f) rank 1 names. */
+void *ref_tls13_import(int bits, const void *aead, int is_server, const void *enc_secret, uint64_t enc_seq, const void *dec_secret,
+                       uint64_t dec_seq)
+{
+    struct ref_tls13 *r = calloc(1, sizeof(*r));
+    ptls_hash_algorithm_t *hash = bits == 256 ? &ptls_minicrypto_sha384 : &ptls_minicrypto_sha256;
+    r->suite.id = bits == 256 ? PTLS_CIPHER_SUITE_AES_256_GCM_SHA384 : PTLS_CIPHER_SUITE_AES_128_GCM_SHA256;
+    r->suite.aead = aead != NULL ? (ptls_aead_algorithm_t *)aead
+                                 : (bits == 256 ? &ptls_minicrypto_aes256gcm : &ptls_minicrypto_aes128gcm);
+    r->suite.hash = hash;
+    r->suite.name = "ref";
+    r->suites[0] = &r->suite;
+    r->ctx.random_bytes = ref_random_bytes;
+    r->ctx.get_time = &ptls_get_time;
+    r->ctx.cipher_suites = r->suites;
+    /* export_tls_params layout (lib/picotls.c:5171-5191) with the TLS 1.3 block of ptls_export (:5265-5272) */
+    uint8_t params[512], *p = params + 2;
+    const size_t ds = hash->digest_size;
+    *p++ = (uint8_t)is_server;
+    *p++ = 0; /* session_reused */
+    put16(&p, PTLS_PROTOCOL_VERSION_TLS13);
+    put16(&p, r->suite.id);
+    memset(p, 0x11, PTLS_HELLO_RANDOM_SIZE);
+    p += PTLS_HELLO_RANDOM_SIZE;
+    put16(&p, 0); /* server name */
+    put16(&p, 0); /* negotiated protocol */
+    put16(&p, (uint16_t)(2 * (ds + 8)));
+    memcpy(p, enc_secret, ds);
+    p += ds;
+    put64(&p, enc_seq);
+    memcpy(p, dec_secret, ds);
+    p += ds;
+    put64(&p, dec_seq);
+    put16(&p, 0); /* extensions */
+    uint8_t *q = params;
+    put16(&q, (uint16_t)(p - params - 2));
+    if (ptls_import(&r->ctx, &r->tls, ptls_iovec_init(params, p - params)) != 0) {
+        free(r);
+        return NULL;
+    }
+    return r;
+}
+
+void ref_tls13_free(void *h)
+{
+    struct ref_tls13 *r = h;
+    ptls_free(r->tls);
+    free(r);
+}
+
+/* ptls_send of `len` application bytes; returns the wire bytes copied to out (or -1) */
+long ref_tls13_send(void *h, const void *in, size_t len, void *out, size_t cap)
+{
+    struct ref_tls13 *r = h;
+    ptls_buffer_t buf;
+    ptls_buffer_init(&buf, "", 0);
+    long n = -1;
+    if (ptls_send(r->tls, &buf, in, len) == 0 && buf.off <= cap) {
+        memcpy(out, buf.base, buf.off);
+        n = (long)buf.off;
+    }
+    ptls_buffer_dispose(&buf);
+    return n;
+}
+
+/* ptls_receive: returns picotls's error code; *consumed = wire bytes used, *outlen = plaintext bytes */
+int ref_tls13_receive(void *h, const void *in, size_t inlen, size_t *consumed, void *out, size_t cap, size_t *outlen)
+{
+    struct ref_tls13 *r = h;
+    ptls_buffer_t buf;
+    ptls_buffer_init(&buf, "", 0);
+    size_t n = inlen;
+    int ret = ptls_receive(r->tls, &buf, in, &n);
+    *consumed = n;
+    *outlen = buf.off;
+    if (buf.off <= cap)
+        memcpy(out, buf.base, buf.off);
+    ptls_buffer_dispose(&buf);
+    return ret;
+}
+
+/* the record-protection key and IV picotls derives from a traffic secret (ptls_aead_new ->
+ * get_traffic_keys, lib/picotls.c:6434-6456): HKDF-Expand-Label(secret, "key" / "iv", "", len) */
+int ref_hkdf_expand_label(int bits, void *out, size_t outlen, const void *secret, const char *label, const void *hashvalue,
+                          size_t hashlen)
+{
+    ptls_hash_algorithm_t *hash = bits == 256 ? &ptls_minicrypto_sha384 : &ptls_minicrypto_sha256;
+    return ptls_hkdf_expand_label(hash, out, outlen, ptls_iovec_init(secret, hash->digest_size), label,
+                                  ptls_iovec_init(hashvalue, hashlen), NULL);
+}

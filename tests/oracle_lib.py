@@ -160,3 +160,66 @@ class Ref:
         out = _c.create_string_buffer(max(len(ct), 16))
         n = self.lib.ref_open(len(key) * 8, _buf(key), _buf(iv), seq, _buf(aad), len(aad), _buf(ct), len(ct), out)
         return (None if n == SIZE_MAX else n), out.raw[: max(len(ct) - 16, 0)]
+
+
+def tls13_wire(oracle, key, iv, seq, ctype, payload):
+    """Restatement of picotls's TLS 1.3 send path (buffer_push_encrypted_records + aead_encrypt + build_aad,
+    lib/picotls.c:696-715, :747-794): 16384-byte chunks, header 17 03 03 BE16(chunk + 17) as the AAD,
+    plaintext chunk || content type, one sequence number per record.  Checked against ptls_send itself."""
+    out = []
+    for j, pos in enumerate(range(0, len(payload), 16384)):
+        chunk = payload[pos:pos + 16384]
+        hdr = bytes([0x17, 0x03, 0x03]) + (len(chunk) + 17).to_bytes(2, "big")
+        out.append(hdr + oracle.seal(key, iv, seq + j, hdr, chunk + bytes([ctype])))
+    return b"".join(out)
+
+
+class RefTLS:
+    """A post-handshake TLS 1.3 connection of the REFERENCE (ptls_import from traffic secrets, then its own
+    ptls_send / ptls_receive record layer, lib/picotls.c:5334-5432, :6061-6145).  `aead` = address of a
+    ptls_aead_algorithm_t (None = minicrypto's AES-GCM: fusion's do_encrypt_v is a stub, lib/fusion.c:1145)."""
+
+    def __init__(self, bits, enc_secret, dec_secret, enc_seq=0, dec_seq=0, aead=None, is_server=1):
+        L = self.lib = _c.CDLL(REF_SO)
+        L.ref_tls13_import.restype = _c.c_void_p
+        L.ref_tls13_import.argtypes = [_c.c_int, _c.c_void_p, _c.c_int, _u8p, _c.c_uint64, _u8p, _c.c_uint64]
+        L.ref_tls13_free.argtypes = [_c.c_void_p]
+        L.ref_tls13_send.restype = _c.c_long
+        L.ref_tls13_send.argtypes = [_c.c_void_p, _u8p, _c.c_size_t, _u8p, _c.c_size_t]
+        L.ref_tls13_receive.restype = _c.c_int
+        L.ref_tls13_receive.argtypes = [_c.c_void_p, _u8p, _c.c_size_t, _c.POINTER(_c.c_size_t), _u8p, _c.c_size_t,
+                                        _c.POINTER(_c.c_size_t)]
+        self.h = L.ref_tls13_import(bits, aead, is_server, _buf(enc_secret), enc_seq, _buf(dec_secret), dec_seq)
+        assert self.h, "ptls_import failed"
+
+    def send(self, payload):
+        cap = len(payload) + 64 * (len(payload) // 16384 + 2)
+        out = _c.create_string_buffer(cap)
+        n = self.lib.ref_tls13_send(self.h, _buf(payload), len(payload), out, cap)
+        assert n >= 0
+        return out.raw[:n]
+
+    def receive(self, wire):
+        """(ret, consumed, plaintext) of ONE ptls_receive call"""
+        out = _c.create_string_buffer(len(wire) + 16)
+        consumed, outlen = _c.c_size_t(), _c.c_size_t()
+        ret = self.lib.ref_tls13_receive(self.h, _buf(wire), len(wire), _c.byref(consumed), out, len(wire) + 16,
+                                         _c.byref(outlen))
+        return ret, consumed.value, out.raw[:outlen.value]
+
+    def close(self):
+        if self.h:
+            self.lib.ref_tls13_free(self.h)
+            self.h = None
+
+
+def ref_traffic_keys(bits, secret):
+    """(key, iv) picotls derives from a TLS 1.3 traffic secret: HKDF-Expand-Label "key" / "iv" (lib/picotls.c:6434-6456)"""
+    L = _c.CDLL(REF_SO)
+    L.ref_hkdf_expand_label.restype = _c.c_int
+    L.ref_hkdf_expand_label.argtypes = [_c.c_int, _u8p, _c.c_size_t, _u8p, _c.c_char_p, _u8p, _c.c_size_t]
+    key = _c.create_string_buffer(bits // 8)
+    iv = _c.create_string_buffer(12)
+    assert L.ref_hkdf_expand_label(bits, key, bits // 8, _buf(secret), b"key", None, 0) == 0
+    assert L.ref_hkdf_expand_label(bits, iv, 12, _buf(secret), b"iv", None, 0) == 0
+    return key.raw, iv.raw
