@@ -285,6 +285,58 @@ extern "C" int ptls_hip_keyset_set(ptls_hip_keyset_t *ks, size_t first, size_t c
     return rc;
 }
 
+/* TLS 1.3 traffic secrets -> key slots, optionally after the key-update step (keyschedule.hip) */
+static int keyset_from_secrets(ptls_hip_keyset_t *ks, size_t first, size_t count, void *secrets, size_t hash_size, void *stream,
+                               bool update)
+{
+    if (ks == nullptr || secrets == nullptr || first + count > ks->nslots || !(hash_size == 32 || hash_size == 48) ||
+        count > 0xffffffffu)
+        return fail(PTLS_HIP_EINVAL, "keyset_%s_secrets: bad arguments", update ? "update" : "set");
+    if (count == 0)
+        return 0;
+    DeviceGuard g(ks->eng->device);
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    const size_t sbytes = count * hash_size, kbytes = count * ks->key_size, ibytes = count * 12;
+    uint8_t *d = nullptr;
+    HIP_TRY(hipMalloc(&d, 2 * sbytes + kbytes + ibytes), PTLS_HIP_ENOMEM);
+    uint8_t *d_sec = d, *d_next = d + sbytes, *d_keys = d + 2 * sbytes, *d_ivs = d + 2 * sbytes + kbytes;
+    std::vector<uint8_t> h_ivs(ibytes);
+    int rc = 0;
+    if (hipMemcpyAsync(d_sec, secrets, sbytes, hipMemcpyHostToDevice, s) != hipSuccess) {
+        rc = fail(PTLS_HIP_ENODEV, "keyset secrets: upload failed");
+    } else if (int e = launch_derive_traffic_keys(d_sec, update ? d_next : nullptr, (uint32_t)count, (int)hash_size,
+                                                  (int)ks->key_size, update ? 1 : 0, d_keys, d_ivs, stream)) {
+        rc = fail(PTLS_HIP_ELAUNCH, "keyset secrets: derive launch failed: %s", hipGetErrorString((hipError_t)e));
+    } else if (int e2 = launch_keysetup(ks->d_slots, ks->d_basis, d_keys, d_ivs, (uint32_t)first, (uint32_t)count,
+                                        (int)ks->key_size, ks->eng->d_t0, stream)) {
+        rc = fail(PTLS_HIP_ELAUNCH, "keyset secrets: key setup launch failed: %s", hipGetErrorString((hipError_t)e2));
+    } else if (hipMemcpyAsync(h_ivs.data(), d_ivs, ibytes, hipMemcpyDeviceToHost, s) != hipSuccess ||
+               (update && hipMemcpyAsync(secrets, d_next, sbytes, hipMemcpyDeviceToHost, s) != hipSuccess) ||
+               hipStreamSynchronize(s) != hipSuccess) {
+        rc = fail(PTLS_HIP_ENODEV, "keyset secrets: derivation failed");
+    }
+    /* secrets and raw keys do not stay in device memory outside the expanded slots */
+    (void)hipMemsetAsync(d, 0, 2 * sbytes + kbytes + ibytes, s);
+    (void)hipStreamSynchronize(s);
+    (void)hipFree(d);
+    if (rc == 0)
+        std::memcpy(&ks->ivs[first * 12], h_ivs.data(), ibytes);
+    std::fill(h_ivs.begin(), h_ivs.end(), 0);
+    return rc;
+}
+
+extern "C" int ptls_hip_keyset_set_secrets(ptls_hip_keyset_t *ks, size_t first, size_t count, const void *secrets, size_t hash_size,
+                                           void *stream)
+{
+    return keyset_from_secrets(ks, first, count, const_cast<void *>(secrets), hash_size, stream, false);
+}
+
+extern "C" int ptls_hip_keyset_update_secrets(ptls_hip_keyset_t *ks, size_t first, size_t count, void *secrets, size_t hash_size,
+                                              void *stream)
+{
+    return keyset_from_secrets(ks, first, count, secrets, hash_size, stream, true);
+}
+
 extern "C" int ptls_hip_keyset_get_iv(ptls_hip_keyset_t *ks, size_t slot, void *iv)
 {
     if (ks == nullptr || slot >= ks->nslots)

@@ -70,6 +70,8 @@ int launch_aesecb(int rounds, const ptls_hip_supp_t *supp, uint32_t n, const uin
                   const uint32_t *t0, unsigned grid, void *stream);
 int launch_tls13_headers(const ptls_hip_record_t *recs, uint32_t n, uint8_t *hdr, unsigned grid, void *stream);
 int launch_tls13_inner(const ptls_hip_record_t *recs, uint32_t n, const uint8_t *out, uint64_t *result, unsigned grid, void *stream);
+int launch_derive_traffic_keys(const uint8_t *secrets_in, uint8_t *secrets_out, uint32_t count, int hash_size, int key_size,
+                               int update, uint8_t *keys, uint8_t *ivs, void *stream);
 int launch_fill(const ptls_hip_record_t *recs, uint32_t n, uint8_t *buf, uint64_t seed, uint64_t index_base,
                 const uint64_t *index, unsigned grid, void *stream);
 

@@ -44,6 +44,8 @@ SIGNATURES = {
     "ptls_hip_keyset_size": (_sz, [_vp]),
     "ptls_hip_keyset_set": (_i, [_vp, _sz, _sz, _vp, _vp, _vp]),
     "ptls_hip_keyset_get_iv": (_i, [_vp, _sz, _vp]),
+    "ptls_hip_keyset_set_secrets": (_i, [_vp, _sz, _sz, _vp, _sz, _vp]),
+    "ptls_hip_keyset_update_secrets": (_i, [_vp, _sz, _sz, _vp, _sz, _vp]),
     "ptls_hip_keyset_set_iv": (_i, [_vp, _sz, _vp, _vp]),
     "ptls_hip_keyset_xor_iv": (_i, [_vp, _sz, _vp, _sz, _vp]),
     "ptls_hip_batch_new": (_vp, [_vp, _vp, _sz, _vp]),
@@ -165,6 +167,20 @@ class KeySet:
             ivs = bytes(ivs)
             assert len(ivs) == count * 12
         _check(lib().ptls_hip_keyset_set(self.ptr, first, count, keys, ivs, _stream(stream)), "keyset_set")
+
+    def set_secrets(self, first, secrets, hash_size, stream=None):
+        """slots [first, first + n) keyed from n TLS 1.3 traffic secrets (HKDF-Expand-Label "key"/"iv" on the GPU)"""
+        secrets = bytes(secrets)
+        n = len(secrets) // hash_size
+        _check(lib().ptls_hip_keyset_set_secrets(self.ptr, first, n, secrets, hash_size, _stream(stream)), "keyset_set_secrets")
+
+    def update_secrets(self, first, secrets, hash_size, stream=None):
+        """TLS 1.3 key update of n connections; returns the next secrets"""
+        buf = ctypes.create_string_buffer(bytes(secrets), len(secrets))
+        n = len(secrets) // hash_size
+        _check(lib().ptls_hip_keyset_update_secrets(self.ptr, first, n, buf, hash_size, _stream(stream)),
+               "keyset_update_secrets")
+        return buf.raw
 
     def get_iv(self, slot):
         buf = ctypes.create_string_buffer(12)

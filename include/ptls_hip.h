@@ -91,6 +91,18 @@ int ptls_hip_keyset_get_iv(ptls_hip_keyset_t *ks, size_t slot, void *iv);
 int ptls_hip_keyset_set_iv(ptls_hip_keyset_t *ks, size_t slot, const void *iv, void *stream);
 int ptls_hip_keyset_xor_iv(ptls_hip_keyset_t *ks, size_t slot, const void *bytes, size_t len, void *stream);
 
+/* Many-connection key management, on the device.  `secrets` = count TLS 1.3
+ * traffic secrets of hash_size bytes (32: SHA-256 suites, 48: SHA-384) in host memory.
+ * set_secrets: slot i gets the record key / IV picotls derives from secret i when it creates the
+ *   connection's AEAD (HKDF-Expand-Label "key" / "iv", get_traffic_keys, lib/picotls.c:1603-1622).
+ * update_secrets: the TLS 1.3 key update (update_traffic_key, lib/picotls.c:4980-4996): every secret
+ *   becomes HKDF-Expand-Label(secret, "traffic upd", "", hash_size) -- written back to `secrets` -- and the
+ *   slots are re-keyed from the new secrets.  Both run one device thread per connection. */
+int ptls_hip_keyset_set_secrets(ptls_hip_keyset_t *ks, size_t first, size_t count, const void *secrets, size_t hash_size,
+                                void *stream);
+int ptls_hip_keyset_update_secrets(ptls_hip_keyset_t *ks, size_t first, size_t count, void *secrets, size_t hash_size,
+                                   void *stream);
+
 /* Record descriptor (48 bytes).  Offsets are byte offsets into the buffers passed to seal/open.
  *   seal: reads len bytes at in+in_off, writes len bytes of ciphertext and the 16-byte tag at
  *         out+out_off (len + 16 bytes), like ptls_aead_encrypt (include/picotls.h:1993).

@@ -213,6 +213,16 @@ class RefTLS:
             self.h = None
 
 
+def ref_hkdf_expand_label(bits, secret, label, outlen):
+    """the reference's ptls_hkdf_expand_label with minicrypto SHA-256 (bits 128) / SHA-384 (bits 256), empty context"""
+    L = _c.CDLL(REF_SO)
+    L.ref_hkdf_expand_label.restype = _c.c_int
+    L.ref_hkdf_expand_label.argtypes = [_c.c_int, _u8p, _c.c_size_t, _u8p, _c.c_char_p, _u8p, _c.c_size_t]
+    out = _c.create_string_buffer(outlen)
+    assert L.ref_hkdf_expand_label(bits, out, outlen, _buf(secret), label, None, 0) == 0
+    return out.raw
+
+
 def ref_traffic_keys(bits, secret):
     """(key, iv) picotls derives from a TLS 1.3 traffic secret: HKDF-Expand-Label "key" / "iv" (lib/picotls.c:6434-6456)"""
     L = _c.CDLL(REF_SO)

@@ -174,3 +174,73 @@ def test_reference_record_layer_on_hip_aead(engine, bits):
     assert ret == 20
     for o in (on_hip, on_ref, peer_hip):
         o.close()
+
+
+@needs_ref
+@pytest.mark.parametrize("bits", [128, 256])
+def test_keyset_from_traffic_secrets(engine, oracle, bits):
+    """§8(f) rank 4: 3000 connections keyed on the GPU from TLS 1.3 traffic secrets (SHA-256 / SHA-384
+    HKDF-Expand-Label "key" / "iv"), then one record each sealed in a batch: == oracle seal with the keys
+    the reference's ptls_hkdf_expand_label derives; the static IVs read back equal the reference's"""
+    from oracle_lib import ref_traffic_keys
+    n, hs = 3000, 48 if bits == 256 else 32
+    rng = np.random.default_rng(bits + 5)
+    secrets = rng.integers(0, 256, n * hs, dtype=np.uint8).tobytes()
+    ks = ptls_hip.KeySet(engine, bits // 8, n)
+    ks.set_secrets(0, secrets, hs)
+    lens = [int(rng.integers(0, 300)) for _ in range(n)]
+    recs, in_total, out_total, _ = ptls_hip.layout_records(lens, [0] * n, np.arange(n), np.arange(n) * 3)
+    payloads = [rng.integers(0, 256, L, dtype=np.uint8).tobytes() for L in lens]
+    h_in = np.zeros(in_total + 16, np.uint8)
+    for r, p in zip(recs, payloads):
+        h_in[r["in_off"]: r["in_off"] + len(p)] = np.frombuffer(p, np.uint8)
+    b = ptls_hip.Batch(engine, recs)
+    d_out = torch.zeros(out_total + 16, dtype=torch.uint8, device="cuda")
+    b.seal(ks, torch.from_numpy(h_in).cuda(), torch.zeros(16, dtype=torch.uint8, device="cuda"), d_out)
+    torch.cuda.synchronize()
+    out = d_out.cpu().numpy()
+    for i in range(0, n, 7):
+        key, iv = ref_traffic_keys(bits, secrets[i * hs:(i + 1) * hs])
+        assert ks.get_iv(i) == iv
+        r = recs[i]
+        assert out[r["out_off"]: r["out_off"] + r["len"] + 16].tobytes() == oracle.seal(key, iv, 3 * i, b"", payloads[i]), i
+    b.close()
+    ks.close()
+
+
+@needs_ref
+@pytest.mark.parametrize("bits", [128, 256])
+def test_key_update_matches_ptls_send(engine, oracle, bits):
+    """the TLS 1.3 key update on the GPU (update_traffic_key, lib/picotls.c:4980-4996) for many connections:
+    next secrets == the reference's HKDF-Expand-Label(secret, "traffic upd"), and a connection at seq 2^24
+    -- where the reference's own ptls_send performs the update (lib/picotls.c:6129-6141) -- sends its next
+    application record exactly as the GPU-updated slot seals it"""
+    from oracle_lib import ref_hkdf_expand_label
+    n, hs = 512, 48 if bits == 256 else 32
+    rng = np.random.default_rng(bits + 9)
+    secrets = rng.integers(0, 256, n * hs, dtype=np.uint8).tobytes()
+    ks = ptls_hip.KeySet(engine, bits // 8, n)
+    ks.set_secrets(0, secrets, hs)
+    nxt = ks.update_secrets(0, secrets, hs)
+    for i in range(0, n, 5):
+        assert nxt[i * hs:(i + 1) * hs] == ref_hkdf_expand_label(bits, secrets[i * hs:(i + 1) * hs], b"traffic upd", hs), i
+    # connection 0 through the reference's ptls_send at the key-update threshold
+    peer_secret = rng.integers(0, 256, hs, dtype=np.uint8).tobytes()
+    conn = RefTLS(bits, secrets[:hs], peer_secret, enc_seq=1 << 24)
+    payload = rng.integers(0, 256, 700, dtype=np.uint8).tobytes()
+    wire = conn.send(payload)
+    conn.close()
+    first_len = 5 + int.from_bytes(wire[3:5], "big")  # the KeyUpdate handshake record, old key
+    app = wire[first_len:]
+    recs, in_total, out_total, _ = ptls_hip.layout_records([len(payload) + 1], [5], [0], [0])
+    recs["flags"] = ptls_hip.record_tls13_type(23)
+    hdr = app[:5]
+    d_in = torch.from_numpy(np.frombuffer(payload + bytes(32), np.uint8).copy()).cuda()
+    d_aad = torch.from_numpy(np.frombuffer(hdr + bytes(11), np.uint8).copy()).cuda()
+    d_out = torch.zeros(out_total + 32, dtype=torch.uint8, device="cuda")
+    b = ptls_hip.Batch(engine, recs)
+    b.seal(ks, d_in, d_aad, d_out)  # slot 0 now holds the updated key, seq restarts at 0
+    torch.cuda.synchronize()
+    assert d_out.cpu().numpy()[: len(payload) + 17].tobytes() == app[5:]
+    b.close()
+    ks.close()
