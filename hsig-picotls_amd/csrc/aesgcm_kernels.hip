@@ -55,6 +55,12 @@ constexpr uint32_t LDS_BYTES = LDS_GTREE + 3 * LDS_TREE_STRIDE; /* 152 KiB of th
 #ifndef GHASH_HALF_BARRIER
 #define GHASH_HALF_BARRIER 0
 #endif
+#ifndef PHASED
+#define PHASED 1 /* round-phased full-block loop (ctr_ghash_phased); 0 = the compiler-scheduled one */
+#endif
+#if PHASED && !CTR_SHORTCUT
+#error "PHASED needs CTR_SHORTCUT"
+#endif
 #ifndef PURE_BLOCKS
 #define PURE_BLOCKS 2 /* data blocks per lane per iteration of the branch-free loop */
 #endif
@@ -289,6 +295,160 @@ __device__ __forceinline__ void aes_ctr_n(const uint8_t *lds, uint32_t lb, const
         s[b] = t[b];
 }
 
+/* ---------------- phased full-block iteration (PHASED=1) ----------------
+ * The compiler, left alone, consumes each T-table lookup a few instructions after issuing it
+ * (lgkmcnt(0..4) waits), so a wave keeps only a handful of LDS reads in flight and the LDS array idles
+ * while the 12 waves of a CU wait on latency.  Here every AES round is one "phase": all lookups of the
+ * round for the KP blocks of the lane (+ a quarter of one GHASH multiply) are issued first, then a
+ * scheduling barrier, then all the XORs: 32-36 reads in flight per wave at every round boundary. */
+struct RoundLoads {
+    uint32_t L[16];
+};
+
+/* the 16 lookups of a full round (column c uses bytes j of words c + j), raw T0 / T2 entries */
+__device__ __forceinline__ void round_issue(const uint8_t *lds, uint32_t lb, const V4 &s, RoundLoads &r)
+{
+    const uint32_t w[4] = {s.w0, s.w1, s.w2, s.w3};
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        r.L[4 * c + 0] = lds32(lds, aes_addr<0>(w[c], lb));
+        r.L[4 * c + 1] = lds32(lds, aes_addr<1>(w[(c + 1) & 3], lb));
+        r.L[4 * c + 2] = lds32(lds, 128 + aes_addr<2>(w[(c + 2) & 3], lb));
+        r.L[4 * c + 3] = lds32(lds, 128 + aes_addr<3>(w[(c + 3) & 3], lb));
+    }
+}
+
+__device__ __forceinline__ V4 round_finish(const RoundLoads &r, const uint32_t *__restrict__ k)
+{
+    uint32_t t[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+        t[c] = xor3(r.L[4 * c + 0], r.L[4 * c + 2], rotl8(r.L[4 * c + 1] ^ r.L[4 * c + 3])) ^ k[c];
+    return V4{t[0], t[1], t[2], t[3]};
+}
+
+/* final round: S-box bytes from T2[.].b0, T0[.].b1, T0[.].b2, T2[.].b3 (as aes_col_last) */
+__device__ __forceinline__ void last_issue(const uint8_t *lds, uint32_t lb, const V4 &s, RoundLoads &r)
+{
+    const uint32_t w[4] = {s.w0, s.w1, s.w2, s.w3};
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        r.L[4 * c + 0] = lds32(lds, 128 + aes_addr<0>(w[c], lb));
+        r.L[4 * c + 1] = lds32(lds, aes_addr<1>(w[(c + 1) & 3], lb));
+        r.L[4 * c + 2] = lds32(lds, aes_addr<2>(w[(c + 2) & 3], lb));
+        r.L[4 * c + 3] = lds32(lds, 128 + aes_addr<3>(w[(c + 3) & 3], lb));
+    }
+}
+
+__device__ __forceinline__ V4 last_finish(const RoundLoads &r, const uint32_t *__restrict__ k)
+{
+    uint32_t t[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        const uint32_t lo = __builtin_amdgcn_perm(r.L[4 * c + 1], r.L[4 * c + 0], 0x0c0c0500u);
+        const uint32_t hi = __builtin_amdgcn_perm(r.L[4 * c + 3], r.L[4 * c + 2], 0x07020c0cu);
+        t[c] = xor3(lo, hi, k[c]);
+    }
+    return V4{t[0], t[1], t[2], t[3]};
+}
+
+/* forward declarations of the GHASH pieces (defined below) */
+struct GhLane;
+__device__ __forceinline__ V4 gh_rot(const GhLane &g, V4 y);
+template <int T0, int NT>
+__device__ __forceinline__ void gh_issue(const uint8_t *lds, const GhLane &g, const V4 &xr, V4 (&G)[8]);
+
+/* Keystream of KP counter blocks (counter-mode shortcut for rounds 1-2, as aes_ctr_n) and, when HASH,
+ * y <- (...(y * P ^ hx[0]) * P ^ ...) ^ hx[KP-1]: multiply j spread over phases 4j+1 .. 4j+4. */
+template <int ROUNDS, int KP, bool HASH>
+__device__ __forceinline__ void ctr_ghash_phased(const uint8_t *lds, uint32_t lb, const uint32_t *__restrict__ rk, const CtrConst &cc,
+                                                 const uint32_t (&cw)[KP], V4 (&ks)[KP], V4 &y, const V4 (&hx)[KP], const GhLane &g)
+{
+    /* phases per GHASH multiply (16 lookups each): as many as the rounds allow, a power of two */
+    constexpr int MPR = ROUNDS / KP;
+    constexpr int MP = MPR >= 8 ? 8 : MPR >= 4 ? 4 : MPR >= 2 ? 2 : 1;
+    constexpr int NT = 16 / MP; /* GHASH lookups per phase */
+    static_assert(MP * KP <= ROUNDS, "GHASH multiplies must fit in the AES phases");
+    V4 s[KP];
+    uint32_t t0[KP], t1[KP];
+    V4 acc = V4{0, 0, 0, 0}, xr = V4{0, 0, 0, 0};
+#pragma unroll
+    for (int p = 1; p <= ROUNDS; ++p) {
+        const bool gh = HASH && p <= MP * KP;
+        const int j = (p - 1) / MP, q = (p - 1) % MP;
+        RoundLoads R[KP];
+        uint32_t M[KP][8];
+        V4 G[8];
+        /* ---- issue ---- */
+        if (gh && q == 0) {
+            xr = gh_rot(g, y);
+            acc = hx[j];
+        }
+#pragma unroll
+        for (int b = 0; b < KP; ++b) {
+            if (p == 1) {
+                const uint32_t x3 = cw[b] ^ cc.r03;
+                M[b][0] = lT2<3>(lds, x3, lb);
+                M[b][1] = lT2<2>(lds, x3, lb);
+            } else if (p == 2) {
+                M[b][0] = lT0<0>(lds, t0[b], lb);
+                M[b][1] = lT0<1>(lds, t1[b], lb);
+                M[b][2] = lT0<0>(lds, t1[b], lb);
+                M[b][3] = lT2<3>(lds, t0[b], lb);
+                M[b][4] = lT2<2>(lds, t0[b], lb);
+                M[b][5] = lT2<3>(lds, t1[b], lb);
+                M[b][6] = lT0<1>(lds, t0[b], lb);
+                M[b][7] = lT2<2>(lds, t1[b], lb);
+            } else if (p < ROUNDS) {
+                round_issue(lds, lb, s[b], R[b]);
+            } else {
+                last_issue(lds, lb, s[b], R[b]);
+            }
+        }
+        if (gh) {
+            /* q is a constant once the phase loop is unrolled: the switch folds to one call */
+            switch (q) {
+            case 0: gh_issue<(0 * NT) & 15, NT>(lds, g, xr, G); break;
+            case 1: gh_issue<(1 * NT) & 15, NT>(lds, g, xr, G); break;
+            case 2: gh_issue<(2 * NT) & 15, NT>(lds, g, xr, G); break;
+            case 3: gh_issue<(3 * NT) & 15, NT>(lds, g, xr, G); break;
+            case 4: gh_issue<(4 * NT) & 15, NT>(lds, g, xr, G); break;
+            case 5: gh_issue<(5 * NT) & 15, NT>(lds, g, xr, G); break;
+            case 6: gh_issue<(6 * NT) & 15, NT>(lds, g, xr, G); break;
+            default: gh_issue<(7 * NT) & 15, NT>(lds, g, xr, G); break;
+            }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        /* ---- finish ---- */
+#pragma unroll
+        for (int b = 0; b < KP; ++b) {
+            if (p == 1) {
+                t0[b] = cc.k10 ^ rotl8(M[b][0]);
+                t1[b] = cc.k11 ^ M[b][1];
+            } else if (p == 2) {
+                s[b].w0 = xor3(cc.k20, M[b][0], rotl8(M[b][1]));
+                s[b].w1 = xor3(cc.k21, M[b][2], rotl8(M[b][3]));
+                s[b].w2 = xor3(cc.k22, M[b][4], rotl8(M[b][5]));
+                s[b].w3 = xor3(cc.k23, rotl8(M[b][6]), M[b][7]);
+            } else if (p < ROUNDS) {
+                s[b] = round_finish(R[b], rk + 4 * p);
+            } else {
+                ks[b] = last_finish(R[b], rk + 4 * p);
+            }
+        }
+        if (gh) {
+#pragma unroll
+            for (int i = 0; i + 1 < NT; i += 2)
+                acc = v4xor3(acc, G[i], G[i + 1]);
+            if (NT & 1)
+                acc = v4xor(acc, G[NT - 1]);
+            if (q == MP - 1)
+                y = acc;
+        }
+        __builtin_amdgcn_sched_barrier(0);
+    }
+}
+
 /* K independent blocks, round-interleaved */
 template <int ROUNDS, int K>
 __device__ __forceinline__ void aes_encrypt_n(const uint8_t *lds, uint32_t lb, const uint32_t *__restrict__ rk, V4 (&s)[K])
@@ -400,6 +560,28 @@ __device__ __forceinline__ V4 gh_mul_main(const uint8_t *lds, const GhLane &g, V
     acc = v4xor3(acc, gh_term<12>(lds, x3, g.lb3), gh_term<13>(lds, x3, g.lb3));
     acc = v4xor3(acc, gh_term<14>(lds, x3, g.lb3), gh_term<15>(lds, x3, g.lb3));
     return acc;
+}
+
+/* gh_mul_main in pieces for the phased loop: the lane rotation of y, then the 4 lookups of word Q */
+__device__ __forceinline__ V4 gh_rot(const GhLane &g, V4 y)
+{
+    const uint32_t s0 = g.rot1 ? y.w1 : y.w0, s1 = g.rot1 ? y.w2 : y.w1, s2 = g.rot1 ? y.w3 : y.w2, s3 = g.rot1 ? y.w0 : y.w3;
+    const uint32_t r0 = g.rot2 ? s2 : s0, r1 = g.rot2 ? s3 : s1, r2 = g.rot2 ? s0 : s2, r3 = g.rot2 ? s1 : s3;
+    return V4{__builtin_amdgcn_alignbit(r1, r0, g.shift), __builtin_amdgcn_alignbit(r2, r1, g.shift),
+              __builtin_amdgcn_alignbit(r3, r2, g.shift), __builtin_amdgcn_alignbit(r0, r3, g.shift)};
+}
+
+template <int T0, int NT>
+__device__ __forceinline__ void gh_issue(const uint8_t *lds, const GhLane &g, const V4 &xr, V4 (&G)[8])
+{
+#pragma unroll
+    for (int i = 0; i < NT; ++i) {
+        const int t = T0 + i, q = t >> 2;
+        const uint32_t xw = q == 0 ? xr.w0 : q == 1 ? xr.w1 : q == 2 ? xr.w2 : xr.w3;
+        const uint32_t lbw = q == 0 ? g.lb0 : q == 1 ? g.lb1 : q == 2 ? g.lb2 : g.lb3;
+        const uint32_t addr = __builtin_amdgcn_perm(xw, lbw, 0x0c0c0000u | ((4u + (t & 3)) << 8) | (t & 3));
+        G[i] = lds128(lds, LDS_GMAIN + addr);
+    }
 }
 
 /* y * P with a nibble table [p = 8w + j][v] (used only in the per-record reduction tree).  One word
@@ -746,6 +928,25 @@ __global__ void __launch_bounds__(WGT)
                     }
 #if PREFETCH_BARRIER
                     __builtin_amdgcn_sched_barrier(0); /* keep the prefetch at the top of the iteration */
+#endif
+#if PHASED
+                    if (OPEN) {
+                        ctr_ghash_phased<ROUNDS, KP, true>(lds, lb_aes, rk, cc, cw, k, y, d, gl);
+#pragma unroll
+                        for (int b = 0; b < KP; ++b)
+                            store_full(dst + o + 16 * b * G, v4xor(d[b], k[b]));
+                    } else {
+                        if (hash_pending)
+                            ctr_ghash_phased<ROUNDS, KP, true>(lds, lb_aes, rk, cc, cw, k, y, pend, gl);
+                        else
+                            ctr_ghash_phased<ROUNDS, KP, false>(lds, lb_aes, rk, cc, cw, k, y, pend, gl);
+#pragma unroll
+                        for (int b = 0; b < KP; ++b) {
+                            pend[b] = v4xor(d[b], k[b]);
+                            store_full(dst + o + 16 * b * G, pend[b]);
+                        }
+                    }
+                    return;
 #endif
 #if ABLATE_AES /* timing-only diagnostic build: keystream = counter block */
 #elif CTR_SHORTCUT

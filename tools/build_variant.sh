@@ -7,5 +7,6 @@ name=$1; out=variants/libptls_hip_${name}.so
 mkdir -p variants/build_${name}
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC $EXTRA -I../include -Icsrc -c csrc/aesgcm_kernels.hip -o variants/build_${name}/k.o
 g++ -std=c++17 -O2 -fPIC -D__HIP_PLATFORM_AMD__ $EXTRA -I/opt/rocm/include -I../include -Icsrc -c csrc/engine.cpp -o variants/build_${name}/e.o
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $out variants/build_${name}/k.o variants/build_${name}/e.o -L/opt/rocm/lib -lamdhip64 -Wl,-rpath,/opt/rocm/lib
+[ -f build/keyschedule.o ] || make -s build/keyschedule.o
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $out variants/build_${name}/k.o build/keyschedule.o variants/build_${name}/e.o -L/opt/rocm/lib -lamdhip64 -Wl,-rpath,/opt/rocm/lib
 echo "built $out"
