@@ -1,0 +1,11 @@
+/* batch_g4.hip -- aesgcm_batch_kernel instantiations for 4 lane(s) per record (batch_kernel.h) */
+#include "batch_kernel.h"
+
+namespace ptls_hip {
+
+int launch_batch_g4(int rounds, bool open, int wg, unsigned grid, void *stream, const KernelArgs &a, bool aligned)
+{
+    return launch_batch_g<4>(rounds, open, wg, grid, static_cast<hipStream_t>(stream), a, aligned);
+}
+
+} // namespace ptls_hip

@@ -1,0 +1,1094 @@
+/*
+ * batch_kernel.h -- the gfx950 (MI355X) AES-GCM batch kernel template and its device helpers
+ * (included by batch_g*.hip, one instantiation set per lanes-per-record G, and by aesgcm_kernels.hip).
+ *
+ * What is computed (bit-exact with picotls lib/fusion.c):
+ *   seal  ptls_fusion_aesgcm_encrypt  lib/fusion.c:400-658
+ *   open  ptls_fusion_aesgcm_decrypt  lib/fusion.c:660-844
+ *   nonce calc_counter                lib/fusion.c:1126-1133 (== ptls_aead__build_iv lib/picotls.c:6492)
+ *   setup new_aesgcm + setup_one_ghash_entry  lib/fusion.c:984-1010, :939-966
+ * How: no AES / carry-less instructions exist on CDNA4 and north_star rules out MFMA,
+ * so both halves of GCM are table work in LDS:
+ *   AES   : T-table rounds.  One 256-entry table T0 (and T2 = rotl16(T0)) replicated 32x so that
+ *           lane l always hits bank l%32 -> ds_read_b32 is conflict-free for any data.  The LDS
+ *           address (byte << 8 | lane slot) is produced by ONE v_perm_b32 per lookup.
+ *   GHASH : multiplication by a fixed power P of H is GF(2)-linear, so X*P = XOR over the 16 bytes
+ *           of X of T8[p][X_p] with T8[p][v] = (v at byte p) * P.  The table is laid out row v, slot
+ *           p; lane l looks up byte p = (k + l) % 16 at step k, so the 16 lanes of every ds_read_b128
+ *           lane group touch 16 distinct slots -> conflict-free; X is pre-rotated per lane so the
+ *           byte for step k sits at a fixed position and the address is again one v_perm_b32.
+ *   Record parallelism: G lanes share one record (Horner with stride G inside a lane, then a
+ *           log2(G)-level shuffle tree with nibble tables for H, H^2, H^4), 64/G records per wave,
+ *           8 waves per workgroup, workgroups persist over key-homogeneous chunks of records.
+ */
+#ifndef PTLS_HIP_BATCH_KERNEL_H
+#define PTLS_HIP_BATCH_KERNEL_H
+
+#include <hip/hip_runtime.h>
+#include "internal.h"
+
+namespace ptls_hip {
+
+/* ---------------- LDS map (bytes) ---------------- */
+constexpr uint32_t LDS_GMAIN = 0;            /* 64 KiB: row v (256 B) = 16 positions x 16 B, P = H^G       */
+constexpr uint32_t LDS_AES = 65536;          /* 64 KiB: row v = [T0 x32 lane slots | T2 x32 lane slots]  */
+constexpr uint32_t LDS_GTREE = 131072;       /* up to 4 x 8 KiB nibble tables for H^1, H^2, H^4, H^8: [p(32)][v(16)] */
+constexpr uint32_t LDS_TREE_STRIDE = 8192;
+/* the tree needs max(log2 G, 1) nibble tables: 152 KiB for G <= 8, all 160 KiB of the CU for G = 16 */
+__host__ __device__ constexpr uint32_t lds_bytes(int log2g)
+{
+    return LDS_GTREE + (log2g > 3 ? log2g : 3) * LDS_TREE_STRIDE;
+}
+
+#ifndef PREFETCH_BARRIER
+#define PREFETCH_BARRIER 1
+#endif
+#ifndef CTR_SHORTCUT
+#define CTR_SHORTCUT 1
+#endif
+#ifndef REMAT_LANE
+#define REMAT_LANE 0
+#endif
+#if REMAT_LANE /* measured: no gain over keeping the constants (same-box A/B), default off */
+#define LANE_FRESH gh_lane_fresh()
+#else
+#define LANE_FRESH gl
+#endif
+#ifndef ABLATE_AES
+#define ABLATE_AES 0
+#endif
+#ifndef ABLATE_GHASH
+#define ABLATE_GHASH 0
+#endif
+#ifndef GHASH_HALF_BARRIER
+#define GHASH_HALF_BARRIER 0
+#endif
+#ifndef PHASED
+#define PHASED 1 /* round-phased full-block loop (ctr_ghash_phased); 0 = the compiler-scheduled one */
+#endif
+#if PHASED && !CTR_SHORTCUT
+#error "PHASED needs CTR_SHORTCUT"
+#endif
+#ifndef PURE_BLOCKS
+#define PURE_BLOCKS 2 /* data blocks per lane per iteration of the branch-free loop */
+#endif
+
+struct V4 {
+    uint32_t w0, w1, w2, w3;
+};
+
+__device__ __forceinline__ V4 v4xor(V4 a, V4 b)
+{
+    return V4{a.w0 ^ b.w0, a.w1 ^ b.w1, a.w2 ^ b.w2, a.w3 ^ b.w3};
+}
+
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c)
+{
+    return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96); /* v_bitop3_b32: a ^ b ^ c in one VALU op */
+}
+
+__device__ __forceinline__ V4 v4xor3(V4 a, V4 b, V4 c)
+{
+    return V4{xor3(a.w0, b.w0, c.w0), xor3(a.w1, b.w1, c.w1), xor3(a.w2, b.w2, c.w2), xor3(a.w3, b.w3, c.w3)};
+}
+
+__device__ __forceinline__ uint32_t bswap32(uint32_t x)
+{
+    return __builtin_bswap32(x);
+}
+
+__device__ __forceinline__ uint32_t lds32(const uint8_t *lds, uint32_t addr)
+{
+    return *reinterpret_cast<const uint32_t *>(lds + addr);
+}
+
+__device__ __forceinline__ V4 lds128(const uint8_t *lds, uint32_t addr)
+{
+    const uint4 v = *reinterpret_cast<const uint4 *>(lds + addr);
+    return V4{v.x, v.y, v.z, v.w};
+}
+
+__device__ __forceinline__ void lds128_store(uint8_t *lds, uint32_t addr, V4 v)
+{
+    *reinterpret_cast<uint4 *>(lds + addr) = make_uint4(v.w0, v.w1, v.w2, v.w3);
+}
+
+/* ======================================================================================= *
+ *  AES (FIPS-197) with replicated T-tables in LDS                                          *
+ * ======================================================================================= */
+
+/* LDS byte address of T0[byte k of x] for this lane: LDS_AES | (x.byte[k] << 8) | lane_slot, from ONE
+ * v_perm_b32: byte0 <- lb.byte0 (selector 0), byte1 <- x.byte[k] (selector 4+k), byte2 <- lb.byte2 (= 1,
+ * i.e. the 64 KiB table base, selector 2), byte3 <- 0.  lb = (lane & 31) * 4 | LDS_AES. */
+template <int K>
+__device__ __forceinline__ uint32_t aes_addr(uint32_t x, uint32_t lb)
+{
+    static_assert(LDS_AES == 65536, "the table base is injected as byte 2 of the address");
+    return __builtin_amdgcn_perm(x, lb, 0x0c020000u | ((4u + K) << 8));
+}
+
+__device__ __forceinline__ uint32_t rotl8(uint32_t x)
+{
+    return __builtin_amdgcn_alignbit(x, x, 24);
+}
+
+/* one output column of a full round:
+ * T0[x0.b0] ^ T1[x1.b1] ^ T2[x2.b2] ^ T3[x3.b3] ^ k  with T1 = rotl8(T0), T3 = rotl8(T2) */
+__device__ __forceinline__ uint32_t aes_col(const uint8_t *lds, uint32_t lb, uint32_t x0, uint32_t x1, uint32_t x2, uint32_t x3,
+                                            uint32_t k)
+{
+    const uint32_t a0 = lds32(lds, aes_addr<0>(x0, lb));
+    const uint32_t a1 = lds32(lds, aes_addr<1>(x1, lb));
+    const uint32_t a2 = lds32(lds, 128 + aes_addr<2>(x2, lb));
+    const uint32_t a3 = lds32(lds, 128 + aes_addr<3>(x3, lb));
+    return xor3(a0, a2, rotl8(a1 ^ a3)) ^ k;
+}
+
+/* final round column: S-box bytes picked out of T2[.].b0, T0[.].b1, T0[.].b2, T2[.].b3 */
+__device__ __forceinline__ uint32_t aes_col_last(const uint8_t *lds, uint32_t lb, uint32_t x0, uint32_t x1, uint32_t x2,
+                                                 uint32_t x3, uint32_t k)
+{
+    const uint32_t u0 = lds32(lds, 128 + aes_addr<0>(x0, lb));
+    const uint32_t u1 = lds32(lds, aes_addr<1>(x1, lb));
+    const uint32_t u2 = lds32(lds, aes_addr<2>(x2, lb));
+    const uint32_t u3 = lds32(lds, 128 + aes_addr<3>(x3, lb));
+    const uint32_t lo = __builtin_amdgcn_perm(u1, u0, 0x0c0c0500u); /* u0.b0 -> b0, u1.b1 -> b1 */
+    const uint32_t hi = __builtin_amdgcn_perm(u3, u2, 0x07020c0cu); /* u2.b2 -> b2, u3.b3 -> b3 */
+    return xor3(lo, hi, k); /* lo and hi occupy disjoint bytes: lo ^ hi == lo | hi */
+}
+
+template <int ROUNDS>
+__device__ __forceinline__ V4 aes_encrypt(const uint8_t *lds, uint32_t lb, const uint32_t *__restrict__ rk, V4 s)
+{
+    s.w0 ^= rk[0];
+    s.w1 ^= rk[1];
+    s.w2 ^= rk[2];
+    s.w3 ^= rk[3];
+#pragma unroll
+    for (int r = 1; r < ROUNDS; ++r) {
+        const uint32_t t0 = aes_col(lds, lb, s.w0, s.w1, s.w2, s.w3, rk[4 * r + 0]);
+        const uint32_t t1 = aes_col(lds, lb, s.w1, s.w2, s.w3, s.w0, rk[4 * r + 1]);
+        const uint32_t t2 = aes_col(lds, lb, s.w2, s.w3, s.w0, s.w1, rk[4 * r + 2]);
+        const uint32_t t3 = aes_col(lds, lb, s.w3, s.w0, s.w1, s.w2, rk[4 * r + 3]);
+        s = V4{t0, t1, t2, t3};
+    }
+    const uint32_t t0 = aes_col_last(lds, lb, s.w0, s.w1, s.w2, s.w3, rk[4 * ROUNDS + 0]);
+    const uint32_t t1 = aes_col_last(lds, lb, s.w1, s.w2, s.w3, s.w0, rk[4 * ROUNDS + 1]);
+    const uint32_t t2 = aes_col_last(lds, lb, s.w2, s.w3, s.w0, s.w1, rk[4 * ROUNDS + 2]);
+    const uint32_t t3 = aes_col_last(lds, lb, s.w3, s.w0, s.w1, s.w2, rk[4 * ROUNDS + 3]);
+    return V4{t0, t1, t2, t3};
+}
+
+/* two independent blocks, round-interleaved: twice the LDS requests in flight per wave */
+template <int ROUNDS>
+__device__ __forceinline__ void aes_encrypt2(const uint8_t *lds, uint32_t lb, const uint32_t *__restrict__ rk, V4 &s, V4 &u)
+{
+    s.w0 ^= rk[0];
+    s.w1 ^= rk[1];
+    s.w2 ^= rk[2];
+    s.w3 ^= rk[3];
+    u.w0 ^= rk[0];
+    u.w1 ^= rk[1];
+    u.w2 ^= rk[2];
+    u.w3 ^= rk[3];
+#pragma unroll
+    for (int r = 1; r < ROUNDS; ++r) {
+        const uint32_t k0 = rk[4 * r + 0], k1 = rk[4 * r + 1], k2 = rk[4 * r + 2], k3 = rk[4 * r + 3];
+        const uint32_t t0 = aes_col(lds, lb, s.w0, s.w1, s.w2, s.w3, k0);
+        const uint32_t v0 = aes_col(lds, lb, u.w0, u.w1, u.w2, u.w3, k0);
+        const uint32_t t1 = aes_col(lds, lb, s.w1, s.w2, s.w3, s.w0, k1);
+        const uint32_t v1 = aes_col(lds, lb, u.w1, u.w2, u.w3, u.w0, k1);
+        const uint32_t t2 = aes_col(lds, lb, s.w2, s.w3, s.w0, s.w1, k2);
+        const uint32_t v2 = aes_col(lds, lb, u.w2, u.w3, u.w0, u.w1, k2);
+        const uint32_t t3 = aes_col(lds, lb, s.w3, s.w0, s.w1, s.w2, k3);
+        const uint32_t v3 = aes_col(lds, lb, u.w3, u.w0, u.w1, u.w2, k3);
+        s = V4{t0, t1, t2, t3};
+        u = V4{v0, v1, v2, v3};
+    }
+    const uint32_t k0 = rk[4 * ROUNDS + 0], k1 = rk[4 * ROUNDS + 1], k2 = rk[4 * ROUNDS + 2], k3 = rk[4 * ROUNDS + 3];
+    const uint32_t t0 = aes_col_last(lds, lb, s.w0, s.w1, s.w2, s.w3, k0);
+    const uint32_t v0 = aes_col_last(lds, lb, u.w0, u.w1, u.w2, u.w3, k0);
+    const uint32_t t1 = aes_col_last(lds, lb, s.w1, s.w2, s.w3, s.w0, k1);
+    const uint32_t v1 = aes_col_last(lds, lb, u.w1, u.w2, u.w3, u.w0, k1);
+    const uint32_t t2 = aes_col_last(lds, lb, s.w2, s.w3, s.w0, s.w1, k2);
+    const uint32_t v2 = aes_col_last(lds, lb, u.w2, u.w3, u.w0, u.w1, k2);
+    const uint32_t t3 = aes_col_last(lds, lb, s.w3, s.w0, s.w1, s.w2, k3);
+    const uint32_t v3 = aes_col_last(lds, lb, u.w3, u.w0, u.w1, u.w2, k3);
+    s = V4{t0, t1, t2, t3};
+    u = V4{v0, v1, v2, v3};
+}
+
+/* single table lookups: T0, T1 = rotl8(T0), T2 = rotl16(T0), T3 = rotl8(T2), byte K of x */
+template <int K>
+__device__ __forceinline__ uint32_t lT0(const uint8_t *lds, uint32_t x, uint32_t lb)
+{
+    return lds32(lds, aes_addr<K>(x, lb));
+}
+template <int K>
+__device__ __forceinline__ uint32_t lT2(const uint8_t *lds, uint32_t x, uint32_t lb)
+{
+    return lds32(lds, 128 + aes_addr<K>(x, lb));
+}
+
+/* Counter-mode shortcut (rounds 1-2).  For a record whose block counters stay below 2^16, the counter
+ * word is 00 00 hi lo and everything else of the AES input is fixed per record, so after round 1 only
+ * state columns 0 and 1 vary (they take counter bytes 15 and 14) and after round 2 every column is
+ * (constant ^ two lookups).  CtrConst holds those per-record constants. */
+struct CtrConst {
+    uint32_t k10, k11; /* round-1 columns 0, 1 without their counter-byte term */
+    uint32_t k20, k21, k22, k23; /* round-2 columns without the terms from round-1 columns 0 and 1 */
+    uint32_t r03;      /* round key 0 word 3 (the counter word's whitening) */
+};
+
+__device__ __forceinline__ CtrConst ctr_const(const uint8_t *lds, uint32_t lb, const uint32_t *__restrict__ rk, uint32_t n0,
+                                              uint32_t n1, uint32_t n2)
+{
+    const uint32_t s0 = n0 ^ rk[0], s1 = n1 ^ rk[1], s2 = n2 ^ rk[2], s3 = rk[3]; /* counter bytes 12,13 = 0 */
+    CtrConst c;
+    c.r03 = rk[3];
+    /* round 1: t_c = T0[s_c.b0] ^ T1[s_{c+1}.b1] ^ T2[s_{c+2}.b2] ^ T3[s_{c+3}.b3] ^ rk1_c */
+    c.k10 = lT0<0>(lds, s0, lb) ^ rotl8(lT0<1>(lds, s1, lb)) ^ lT2<2>(lds, s2, lb) ^ rk[4]; /* - T3[s3.b3] */
+    c.k11 = lT0<0>(lds, s1, lb) ^ rotl8(lT0<1>(lds, s2, lb)) ^ rotl8(lT2<3>(lds, s0, lb)) ^ rk[5]; /* - T2[s3.b2] */
+    const uint32_t t2 = lT0<0>(lds, s2, lb) ^ rotl8(lT0<1>(lds, s3, lb)) ^ lT2<2>(lds, s0, lb) ^ rotl8(lT2<3>(lds, s1, lb)) ^ rk[6];
+    const uint32_t t3 = lT0<0>(lds, s3, lb) ^ rotl8(lT0<1>(lds, s0, lb)) ^ lT2<2>(lds, s1, lb) ^ rotl8(lT2<3>(lds, s2, lb)) ^ rk[7];
+    /* round 2 constant parts (terms reading t2, t3) */
+    c.k20 = lT2<2>(lds, t2, lb) ^ rotl8(lT2<3>(lds, t3, lb)) ^ rk[8];
+    c.k21 = rotl8(lT0<1>(lds, t2, lb)) ^ lT2<2>(lds, t3, lb) ^ rk[9];
+    c.k22 = lT0<0>(lds, t2, lb) ^ rotl8(lT0<1>(lds, t3, lb)) ^ rk[10];
+    c.k23 = lT0<0>(lds, t3, lb) ^ rotl8(lT2<3>(lds, t2, lb)) ^ rk[11];
+    return c;
+}
+
+/* AES of K counter blocks (n0, n1, n2, bswap(ctr_b)) with ctr_b < 2^16, using the per-record constants */
+template <int ROUNDS, int K>
+__device__ __forceinline__ void aes_ctr_n(const uint8_t *lds, uint32_t lb, const uint32_t *__restrict__ rk, const CtrConst &cc,
+                                          const uint32_t (&ctrw)[K], V4 (&s)[K])
+{
+#pragma unroll
+    for (int b = 0; b < K; ++b) {
+        const uint32_t x3 = ctrw[b] ^ cc.r03;                                     /* state column 3 after round 0 */
+        const uint32_t t0 = cc.k10 ^ rotl8(lT2<3>(lds, x3, lb));                  /* + T3[x3.b3] */
+        const uint32_t t1 = cc.k11 ^ lT2<2>(lds, x3, lb);                         /* + T2[x3.b2] */
+        s[b].w0 = xor3(cc.k20, lT0<0>(lds, t0, lb), rotl8(lT0<1>(lds, t1, lb)));  /* T0[t0.b0] ^ T1[t1.b1] */
+        s[b].w1 = xor3(cc.k21, lT0<0>(lds, t1, lb), rotl8(lT2<3>(lds, t0, lb)));  /* T0[t1.b0] ^ T3[t0.b3] */
+        s[b].w2 = xor3(cc.k22, lT2<2>(lds, t0, lb), rotl8(lT2<3>(lds, t1, lb)));  /* T2[t0.b2] ^ T3[t1.b3] */
+        s[b].w3 = xor3(cc.k23, rotl8(lT0<1>(lds, t0, lb)), lT2<2>(lds, t1, lb));  /* T1[t0.b1] ^ T2[t1.b2] */
+    }
+#pragma unroll
+    for (int r = 3; r < ROUNDS; ++r) {
+        const uint32_t k0 = rk[4 * r + 0], k1 = rk[4 * r + 1], k2 = rk[4 * r + 2], k3 = rk[4 * r + 3];
+        V4 t[K];
+#pragma unroll
+        for (int b = 0; b < K; ++b) {
+            t[b].w0 = aes_col(lds, lb, s[b].w0, s[b].w1, s[b].w2, s[b].w3, k0);
+            t[b].w1 = aes_col(lds, lb, s[b].w1, s[b].w2, s[b].w3, s[b].w0, k1);
+            t[b].w2 = aes_col(lds, lb, s[b].w2, s[b].w3, s[b].w0, s[b].w1, k2);
+            t[b].w3 = aes_col(lds, lb, s[b].w3, s[b].w0, s[b].w1, s[b].w2, k3);
+        }
+#pragma unroll
+        for (int b = 0; b < K; ++b)
+            s[b] = t[b];
+    }
+    const uint32_t k0 = rk[4 * ROUNDS + 0], k1 = rk[4 * ROUNDS + 1], k2 = rk[4 * ROUNDS + 2], k3 = rk[4 * ROUNDS + 3];
+    V4 t[K];
+#pragma unroll
+    for (int b = 0; b < K; ++b) {
+        t[b].w0 = aes_col_last(lds, lb, s[b].w0, s[b].w1, s[b].w2, s[b].w3, k0);
+        t[b].w1 = aes_col_last(lds, lb, s[b].w1, s[b].w2, s[b].w3, s[b].w0, k1);
+        t[b].w2 = aes_col_last(lds, lb, s[b].w2, s[b].w3, s[b].w0, s[b].w1, k2);
+        t[b].w3 = aes_col_last(lds, lb, s[b].w3, s[b].w0, s[b].w1, s[b].w2, k3);
+    }
+#pragma unroll
+    for (int b = 0; b < K; ++b)
+        s[b] = t[b];
+}
+
+/* ---------------- phased full-block iteration (PHASED=1) ----------------
+ * The compiler, left alone, consumes each T-table lookup a few instructions after issuing it
+ * (lgkmcnt(0..4) waits), so a wave keeps only a handful of LDS reads in flight and the LDS array idles
+ * while the 12 waves of a CU wait on latency.  Here every AES round is one "phase": all lookups of the
+ * round for the KP blocks of the lane (+ a quarter of one GHASH multiply) are issued first, then a
+ * scheduling barrier, then all the XORs: 32-36 reads in flight per wave at every round boundary. */
+struct RoundLoads {
+    uint32_t L[16];
+};
+
+/* the 16 lookups of a full round (column c uses bytes j of words c + j), raw T0 / T2 entries */
+__device__ __forceinline__ void round_issue(const uint8_t *lds, uint32_t lb, const V4 &s, RoundLoads &r)
+{
+    const uint32_t w[4] = {s.w0, s.w1, s.w2, s.w3};
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        r.L[4 * c + 0] = lds32(lds, aes_addr<0>(w[c], lb));
+        r.L[4 * c + 1] = lds32(lds, aes_addr<1>(w[(c + 1) & 3], lb));
+        r.L[4 * c + 2] = lds32(lds, 128 + aes_addr<2>(w[(c + 2) & 3], lb));
+        r.L[4 * c + 3] = lds32(lds, 128 + aes_addr<3>(w[(c + 3) & 3], lb));
+    }
+}
+
+__device__ __forceinline__ V4 round_finish(const RoundLoads &r, const uint32_t *__restrict__ k)
+{
+    uint32_t t[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+        t[c] = xor3(r.L[4 * c + 0], r.L[4 * c + 2], rotl8(r.L[4 * c + 1] ^ r.L[4 * c + 3])) ^ k[c];
+    return V4{t[0], t[1], t[2], t[3]};
+}
+
+/* final round: S-box bytes from T2[.].b0, T0[.].b1, T0[.].b2, T2[.].b3 (as aes_col_last) */
+__device__ __forceinline__ void last_issue(const uint8_t *lds, uint32_t lb, const V4 &s, RoundLoads &r)
+{
+    const uint32_t w[4] = {s.w0, s.w1, s.w2, s.w3};
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        r.L[4 * c + 0] = lds32(lds, 128 + aes_addr<0>(w[c], lb));
+        r.L[4 * c + 1] = lds32(lds, aes_addr<1>(w[(c + 1) & 3], lb));
+        r.L[4 * c + 2] = lds32(lds, aes_addr<2>(w[(c + 2) & 3], lb));
+        r.L[4 * c + 3] = lds32(lds, 128 + aes_addr<3>(w[(c + 3) & 3], lb));
+    }
+}
+
+__device__ __forceinline__ V4 last_finish(const RoundLoads &r, const uint32_t *__restrict__ k)
+{
+    uint32_t t[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        const uint32_t lo = __builtin_amdgcn_perm(r.L[4 * c + 1], r.L[4 * c + 0], 0x0c0c0500u);
+        const uint32_t hi = __builtin_amdgcn_perm(r.L[4 * c + 3], r.L[4 * c + 2], 0x07020c0cu);
+        t[c] = xor3(lo, hi, k[c]);
+    }
+    return V4{t[0], t[1], t[2], t[3]};
+}
+
+/* forward declarations of the GHASH pieces (defined below) */
+struct GhLane;
+__device__ __forceinline__ V4 gh_rot(const GhLane &g, V4 y);
+template <int T0, int NT>
+__device__ __forceinline__ void gh_issue(const uint8_t *lds, const GhLane &g, const V4 &xr, V4 (&G)[8]);
+
+/* Keystream of KP counter blocks (counter-mode shortcut for rounds 1-2, as aes_ctr_n) and, when HASH,
+ * y <- (...(y * P ^ hx[0]) * P ^ ...) ^ hx[KP-1]: multiply j spread over phases 4j+1 .. 4j+4. */
+template <int ROUNDS, int KP, bool HASH>
+__device__ __forceinline__ void ctr_ghash_phased(const uint8_t *lds, uint32_t lb, const uint32_t *__restrict__ rk, const CtrConst &cc,
+                                                 const uint32_t (&cw)[KP], V4 (&ks)[KP], V4 &y, const V4 (&hx)[KP], const GhLane &g)
+{
+    /* phases per GHASH multiply (16 lookups each): as many as the rounds allow, a power of two */
+    constexpr int MPR = ROUNDS / KP;
+    constexpr int MP = MPR >= 8 ? 8 : MPR >= 4 ? 4 : MPR >= 2 ? 2 : 1;
+    constexpr int NT = 16 / MP; /* GHASH lookups per phase */
+    static_assert(MP * KP <= ROUNDS, "GHASH multiplies must fit in the AES phases");
+    V4 s[KP];
+    uint32_t t0[KP], t1[KP];
+    V4 acc = V4{0, 0, 0, 0}, xr = V4{0, 0, 0, 0};
+#pragma unroll
+    for (int p = 1; p <= ROUNDS; ++p) {
+        const bool gh = HASH && p <= MP * KP;
+        const int j = (p - 1) / MP, q = (p - 1) % MP;
+        RoundLoads R[KP];
+        uint32_t M[KP][8];
+        V4 G[8];
+        /* ---- issue ---- */
+        if (gh && q == 0) {
+            xr = gh_rot(g, y);
+            acc = hx[j];
+        }
+#pragma unroll
+        for (int b = 0; b < KP; ++b) {
+            if (p == 1) {
+                const uint32_t x3 = cw[b] ^ cc.r03;
+                M[b][0] = lT2<3>(lds, x3, lb);
+                M[b][1] = lT2<2>(lds, x3, lb);
+            } else if (p == 2) {
+                M[b][0] = lT0<0>(lds, t0[b], lb);
+                M[b][1] = lT0<1>(lds, t1[b], lb);
+                M[b][2] = lT0<0>(lds, t1[b], lb);
+                M[b][3] = lT2<3>(lds, t0[b], lb);
+                M[b][4] = lT2<2>(lds, t0[b], lb);
+                M[b][5] = lT2<3>(lds, t1[b], lb);
+                M[b][6] = lT0<1>(lds, t0[b], lb);
+                M[b][7] = lT2<2>(lds, t1[b], lb);
+            } else if (p < ROUNDS) {
+                round_issue(lds, lb, s[b], R[b]);
+            } else {
+                last_issue(lds, lb, s[b], R[b]);
+            }
+        }
+        if (gh) {
+            /* q is a constant once the phase loop is unrolled: the switch folds to one call */
+            switch (q) {
+            case 0: gh_issue<(0 * NT) & 15, NT>(lds, g, xr, G); break;
+            case 1: gh_issue<(1 * NT) & 15, NT>(lds, g, xr, G); break;
+            case 2: gh_issue<(2 * NT) & 15, NT>(lds, g, xr, G); break;
+            case 3: gh_issue<(3 * NT) & 15, NT>(lds, g, xr, G); break;
+            case 4: gh_issue<(4 * NT) & 15, NT>(lds, g, xr, G); break;
+            case 5: gh_issue<(5 * NT) & 15, NT>(lds, g, xr, G); break;
+            case 6: gh_issue<(6 * NT) & 15, NT>(lds, g, xr, G); break;
+            default: gh_issue<(7 * NT) & 15, NT>(lds, g, xr, G); break;
+            }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        /* ---- finish ---- */
+#pragma unroll
+        for (int b = 0; b < KP; ++b) {
+            if (p == 1) {
+                t0[b] = cc.k10 ^ rotl8(M[b][0]);
+                t1[b] = cc.k11 ^ M[b][1];
+            } else if (p == 2) {
+                s[b].w0 = xor3(cc.k20, M[b][0], rotl8(M[b][1]));
+                s[b].w1 = xor3(cc.k21, M[b][2], rotl8(M[b][3]));
+                s[b].w2 = xor3(cc.k22, M[b][4], rotl8(M[b][5]));
+                s[b].w3 = xor3(cc.k23, rotl8(M[b][6]), M[b][7]);
+            } else if (p < ROUNDS) {
+                s[b] = round_finish(R[b], rk + 4 * p);
+            } else {
+                ks[b] = last_finish(R[b], rk + 4 * p);
+            }
+        }
+        if (gh) {
+#pragma unroll
+            for (int i = 0; i + 1 < NT; i += 2)
+                acc = v4xor3(acc, G[i], G[i + 1]);
+            if (NT & 1)
+                acc = v4xor(acc, G[NT - 1]);
+            if (q == MP - 1)
+                y = acc;
+        }
+        __builtin_amdgcn_sched_barrier(0);
+    }
+}
+
+/* K independent blocks, round-interleaved */
+template <int ROUNDS, int K>
+__device__ __forceinline__ void aes_encrypt_n(const uint8_t *lds, uint32_t lb, const uint32_t *__restrict__ rk, V4 (&s)[K])
+{
+#pragma unroll
+    for (int b = 0; b < K; ++b) {
+        s[b].w0 ^= rk[0];
+        s[b].w1 ^= rk[1];
+        s[b].w2 ^= rk[2];
+        s[b].w3 ^= rk[3];
+    }
+#pragma unroll
+    for (int r = 1; r < ROUNDS; ++r) {
+        const uint32_t k0 = rk[4 * r + 0], k1 = rk[4 * r + 1], k2 = rk[4 * r + 2], k3 = rk[4 * r + 3];
+        V4 t[K];
+#pragma unroll
+        for (int b = 0; b < K; ++b) {
+            t[b].w0 = aes_col(lds, lb, s[b].w0, s[b].w1, s[b].w2, s[b].w3, k0);
+            t[b].w1 = aes_col(lds, lb, s[b].w1, s[b].w2, s[b].w3, s[b].w0, k1);
+            t[b].w2 = aes_col(lds, lb, s[b].w2, s[b].w3, s[b].w0, s[b].w1, k2);
+            t[b].w3 = aes_col(lds, lb, s[b].w3, s[b].w0, s[b].w1, s[b].w2, k3);
+        }
+#pragma unroll
+        for (int b = 0; b < K; ++b)
+            s[b] = t[b];
+    }
+    const uint32_t k0 = rk[4 * ROUNDS + 0], k1 = rk[4 * ROUNDS + 1], k2 = rk[4 * ROUNDS + 2], k3 = rk[4 * ROUNDS + 3];
+    V4 t[K];
+#pragma unroll
+    for (int b = 0; b < K; ++b) {
+        t[b].w0 = aes_col_last(lds, lb, s[b].w0, s[b].w1, s[b].w2, s[b].w3, k0);
+        t[b].w1 = aes_col_last(lds, lb, s[b].w1, s[b].w2, s[b].w3, s[b].w0, k1);
+        t[b].w2 = aes_col_last(lds, lb, s[b].w2, s[b].w3, s[b].w0, s[b].w1, k2);
+        t[b].w3 = aes_col_last(lds, lb, s[b].w3, s[b].w0, s[b].w1, s[b].w2, k3);
+    }
+#pragma unroll
+    for (int b = 0; b < K; ++b)
+        s[b] = t[b];
+}
+
+/* ======================================================================================= *
+ *  GHASH multiply by table                                                                 *
+ * ======================================================================================= */
+
+struct GhLane {
+    uint32_t lb0, lb1, lb2, lb3; /* byte m of lbI = ((4I + m + lane) & 15) * 16 : slot of step 4I+m */
+    uint32_t shift;              /* 8 * (lane & 3) */
+    bool rot1, rot2;             /* word rotation by (lane >> 2) & 3 */
+};
+
+__device__ __forceinline__ GhLane gh_lane_from(uint32_t lane)
+{
+    GhLane g;
+    /* byte m of lbI = ((lane + 4I + m) & 15) * 16: all four bytes at once (no carries: values < 256) */
+    const uint32_t base = lane * 0x01010101u + 0x03020100u;
+    g.lb0 = ((base + 0x00000000u) & 0x0f0f0f0fu) << 4;
+    g.lb1 = ((base + 0x04040404u) & 0x0f0f0f0fu) << 4;
+    g.lb2 = ((base + 0x08080808u) & 0x0f0f0f0fu) << 4;
+    g.lb3 = ((base + 0x0c0c0c0cu) & 0x0f0f0f0fu) << 4;
+    g.shift = 8u * (lane & 3);
+    g.rot1 = ((lane >> 2) & 1) != 0;
+    g.rot2 = ((lane >> 3) & 1) != 0;
+    return g;
+}
+
+__device__ __forceinline__ GhLane gh_lane_init(int lane)
+{
+    return gh_lane_from((uint32_t)lane);
+}
+
+/* Lane id through an opaque asm statement: the compiler can neither hoist nor keep the derived lane
+ * constants alive across the hot loop, so they are rematerialised (a few VALU) instead of being
+ * spilled to scratch, whose reload waits would also drain this wave's in-flight stores (vmcnt is
+ * in-order). */
+__device__ __forceinline__ GhLane gh_lane_fresh()
+{
+    uint32_t lane;
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lane));
+    return gh_lane_from(lane);
+}
+
+template <int K>
+__device__ __forceinline__ V4 gh_term(const uint8_t *lds, uint32_t xw, uint32_t lbw)
+{
+    /* address = (xrot.byte[K] << 8) | slot(K):  byte0 <- lbw.byte[K%4], byte1 <- xw.byte[K%4] */
+    const uint32_t addr = __builtin_amdgcn_perm(xw, lbw, 0x0c0c0000u | ((4u + (K & 3)) << 8) | (K & 3));
+    return lds128(lds, LDS_GMAIN + addr);
+}
+
+/* returns y * P ^ x, P = the power held in the main table */
+__device__ __forceinline__ V4 gh_mul_main(const uint8_t *lds, const GhLane &g, V4 y, V4 x)
+{
+    /* rotate y right by (lane & 15) bytes: xr.byte[k] = y.byte[(k + lane) & 15] */
+    const uint32_t s0 = g.rot1 ? y.w1 : y.w0, s1 = g.rot1 ? y.w2 : y.w1, s2 = g.rot1 ? y.w3 : y.w2, s3 = g.rot1 ? y.w0 : y.w3;
+    const uint32_t r0 = g.rot2 ? s2 : s0, r1 = g.rot2 ? s3 : s1, r2 = g.rot2 ? s0 : s2, r3 = g.rot2 ? s1 : s3;
+    const uint32_t x0 = __builtin_amdgcn_alignbit(r1, r0, g.shift);
+    const uint32_t x1 = __builtin_amdgcn_alignbit(r2, r1, g.shift);
+    const uint32_t x2 = __builtin_amdgcn_alignbit(r3, r2, g.shift);
+    const uint32_t x3 = __builtin_amdgcn_alignbit(r0, r3, g.shift);
+    V4 acc = v4xor3(x, gh_term<0>(lds, x0, g.lb0), gh_term<1>(lds, x0, g.lb0));
+    acc = v4xor3(acc, gh_term<2>(lds, x0, g.lb0), gh_term<3>(lds, x0, g.lb0));
+    acc = v4xor3(acc, gh_term<4>(lds, x1, g.lb1), gh_term<5>(lds, x1, g.lb1));
+    acc = v4xor3(acc, gh_term<6>(lds, x1, g.lb1), gh_term<7>(lds, x1, g.lb1));
+#if GHASH_HALF_BARRIER
+    __builtin_amdgcn_sched_barrier(0);
+#endif
+    acc = v4xor3(acc, gh_term<8>(lds, x2, g.lb2), gh_term<9>(lds, x2, g.lb2));
+    acc = v4xor3(acc, gh_term<10>(lds, x2, g.lb2), gh_term<11>(lds, x2, g.lb2));
+    acc = v4xor3(acc, gh_term<12>(lds, x3, g.lb3), gh_term<13>(lds, x3, g.lb3));
+    acc = v4xor3(acc, gh_term<14>(lds, x3, g.lb3), gh_term<15>(lds, x3, g.lb3));
+    return acc;
+}
+
+/* gh_mul_main in pieces for the phased loop: the lane rotation of y, then the 4 lookups of word Q */
+__device__ __forceinline__ V4 gh_rot(const GhLane &g, V4 y)
+{
+    const uint32_t s0 = g.rot1 ? y.w1 : y.w0, s1 = g.rot1 ? y.w2 : y.w1, s2 = g.rot1 ? y.w3 : y.w2, s3 = g.rot1 ? y.w0 : y.w3;
+    const uint32_t r0 = g.rot2 ? s2 : s0, r1 = g.rot2 ? s3 : s1, r2 = g.rot2 ? s0 : s2, r3 = g.rot2 ? s1 : s3;
+    return V4{__builtin_amdgcn_alignbit(r1, r0, g.shift), __builtin_amdgcn_alignbit(r2, r1, g.shift),
+              __builtin_amdgcn_alignbit(r3, r2, g.shift), __builtin_amdgcn_alignbit(r0, r3, g.shift)};
+}
+
+template <int T0, int NT>
+__device__ __forceinline__ void gh_issue(const uint8_t *lds, const GhLane &g, const V4 &xr, V4 (&G)[8])
+{
+#pragma unroll
+    for (int i = 0; i < NT; ++i) {
+        const int t = T0 + i, q = t >> 2;
+        const uint32_t xw = q == 0 ? xr.w0 : q == 1 ? xr.w1 : q == 2 ? xr.w2 : xr.w3;
+        const uint32_t lbw = q == 0 ? g.lb0 : q == 1 ? g.lb1 : q == 2 ? g.lb2 : g.lb3;
+        const uint32_t addr = __builtin_amdgcn_perm(xw, lbw, 0x0c0c0000u | ((4u + (t & 3)) << 8) | (t & 3));
+        G[i] = lds128(lds, LDS_GMAIN + addr);
+    }
+}
+
+/* y * P with a nibble table [p = 8w + j][v] (used only in the per-record reduction tree).  One word
+ * (8 lookups) at a time: sched barriers keep the compiler from hoisting all 32 ds_read_b128 (128 VGPRs). */
+__device__ __forceinline__ V4 gh_mul_nibble(const uint8_t *lds, uint32_t table, V4 y)
+{
+    V4 acc = V4{0, 0, 0, 0};
+    const uint32_t w[4] = {y.w0, y.w1, y.w2, y.w3};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        V4 t[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+            t[j] = lds128(lds, table + (uint32_t)(8 * i + j) * 256u + ((w[i] >> (4 * j)) & 15u) * 16u);
+        acc = v4xor3(acc, t[0], t[1]);
+        acc = v4xor3(acc, t[2], t[3]);
+        acc = v4xor3(acc, t[4], t[5]);
+        acc = v4xor3(acc, t[6], t[7]);
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    return acc;
+}
+
+/* ---------------- table construction in LDS ---------------- */
+
+__device__ __forceinline__ V4 ld_basis(const uint32_t *b, int e)
+{
+    const uint4 v = reinterpret_cast<const uint4 *>(b)[e];
+    return V4{v.x, v.y, v.z, v.w};
+}
+
+/* AES tables: row v = [T0[v] x 32 | rotl16(T0[v]) x 32] */
+__device__ void build_aes_tables(uint8_t *lds, const uint32_t *__restrict__ t0)
+{
+    for (int e = threadIdx.x; e < 256 * 32; e += blockDim.x) {
+        const int v = e >> 5, s = e & 31; /* row v, lane slot s */
+        const uint32_t t = t0[v];
+        *reinterpret_cast<uint32_t *>(lds + LDS_AES + v * 256 + s * 4) = t;
+        *reinterpret_cast<uint32_t *>(lds + LDS_AES + v * 256 + 128 + s * 4) = (t << 16) | (t >> 16);
+    }
+}
+
+/* GHASH tables of one key slot.  basis = uint4[NPOW][128], basis[t][e] = H^(2^t) * x^e (GCM bit
+ * index e: byte e/8, bit 7 - e%8).  Raw byte p, bit t  <->  e = 8p + 7 - t. */
+__device__ void build_ghash_tables(uint8_t *lds, const uint32_t *__restrict__ basis, int log2g)
+{
+    const uint32_t *bm = basis + log2g * 128 * 4;
+    for (int e = threadIdx.x; e < 16 * 256; e += blockDim.x) {
+        const int p = e >> 8, v = e & 255;
+        V4 acc = V4{0, 0, 0, 0};
+#pragma unroll
+        for (int t = 0; t < 8; ++t)
+            if ((v >> t) & 1)
+                acc = v4xor(acc, ld_basis(bm, 8 * p + 7 - t));
+        lds128_store(lds, LDS_GMAIN + v * 256 + p * 16, acc);
+    }
+    const int ntree = log2g > 1 ? log2g : 1; /* H^(2^d) for the tree levels d < log2 G; d = 0 (H) always */
+    for (int e = threadIdx.x; e < ntree * 512; e += blockDim.x) {
+        const int d = e >> 9, p = (e >> 4) & 31, v = e & 15;
+        const int w = p >> 3, j = p & 7;
+        const uint32_t *bt = basis + d * 128 * 4;
+        V4 acc = V4{0, 0, 0, 0};
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            if ((v >> t) & 1) {
+                const int u = 4 * j + t; /* bit u of little-endian word w = raw byte 4w + u/8, bit u%8 */
+                acc = v4xor(acc, ld_basis(bt, 8 * (4 * w + (u >> 3)) + 7 - (u & 7)));
+            }
+        }
+        lds128_store(lds, LDS_GTREE + d * LDS_TREE_STRIDE + p * 256 + v * 16, acc);
+    }
+}
+
+/* ---------------- global-memory block access ---------------- */
+
+/* A whole 16-byte block at any byte address: gfx9+ global memory instructions handle unaligned
+ * addresses (the ROCm default unaligned access mode), so an align(1) vector type still compiles to ONE
+ * global_load/store_dwordx4.  Only whole blocks (all 16 bytes inside the record) go through these. */
+struct __attribute__((packed, aligned(1))) U4u {
+    uint32_t x, y, z, w;
+};
+
+__device__ __forceinline__ V4 load_full(const uint8_t *p)
+{
+    const U4u v = *reinterpret_cast<const U4u *>(p);
+    return V4{v.x, v.y, v.z, v.w};
+}
+
+__device__ __forceinline__ void store_full(uint8_t *p, V4 v)
+{
+    *reinterpret_cast<U4u *>(p) = U4u{v.w0, v.w1, v.w2, v.w3};
+}
+
+/* 128-bit shifts by one byte (raw byte order: w0 holds bytes 0..3) */
+__device__ __forceinline__ V4 shr8(V4 v)
+{
+    return V4{__builtin_amdgcn_alignbit(v.w1, v.w0, 8), __builtin_amdgcn_alignbit(v.w2, v.w1, 8),
+              __builtin_amdgcn_alignbit(v.w3, v.w2, 8), v.w3 >> 8};
+}
+
+__device__ __forceinline__ V4 shl8_in(V4 v, uint8_t b)
+{
+    return V4{(v.w0 << 8) | b, __builtin_amdgcn_alignbit(v.w1, v.w0, 24), __builtin_amdgcn_alignbit(v.w2, v.w1, 24),
+              __builtin_amdgcn_alignbit(v.w3, v.w2, 24)};
+}
+
+/* exact byte-granular access (n in 0..16): compact loops, used for unaligned layouts and partial stores */
+__device__ __forceinline__ V4 load_bytes(const uint8_t *p, int n)
+{
+    V4 v = V4{0, 0, 0, 0};
+#pragma unroll 1
+    for (int k = n - 1; k >= 0; --k)
+        v = shl8_in(v, p[k]);
+    return v;
+}
+
+__device__ __forceinline__ void store_bytes(uint8_t *p, int n, V4 v)
+{
+#pragma unroll 1
+    for (int k = 0; k < n; ++k) {
+        p[k] = (uint8_t)v.w0;
+        v = shr8(v);
+    }
+}
+
+__device__ __forceinline__ V4 mask_block(V4 v, int n);
+
+/* ALIGNED: p is 16-byte aligned, so the 16-byte chunk holding a partial block never crosses a page;
+ * load it whole and keep the first n bytes.  Otherwise read exactly n bytes. */
+template <bool ALIGNED>
+__device__ __forceinline__ V4 load_block(const uint8_t *p, int n)
+{
+    if (ALIGNED) {
+        const V4 r = load_full(p);
+        return n == 16 ? r : mask_block(r, n);
+    }
+    return n == 16 ? load_full(p) : load_bytes(p, n);
+}
+
+template <bool ALIGNED>
+__device__ __forceinline__ void store_block(uint8_t *p, int n, V4 v)
+{
+    if (n == 16) {
+        store_full(p, v);
+        return;
+    }
+    store_bytes(p, n, v);
+}
+
+__device__ __forceinline__ V4 mask_block(V4 v, int n)
+{
+    /* keep the first n (0..16) bytes */
+    const uint32_t w[4] = {v.w0, v.w1, v.w2, v.w3};
+    uint32_t o[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int keep = n - 4 * i;
+        o[i] = keep >= 4 ? w[i] : (keep <= 0 ? 0u : (w[i] & ((1u << (8 * keep)) - 1u)));
+    }
+    return V4{o[0], o[1], o[2], o[3]};
+}
+
+/* v with byte `pos` (0..15, currently zero) set to b */
+__device__ __forceinline__ V4 put_byte(V4 v, int pos, uint32_t b)
+{
+    const uint32_t x = b << (8 * (pos & 3));
+    const int w = pos >> 2;
+    return V4{v.w0 | (w == 0 ? x : 0u), v.w1 | (w == 1 ? x : 0u), v.w2 | (w == 2 ? x : 0u), v.w3 | (w == 3 ? x : 0u)};
+}
+
+__device__ __forceinline__ int wave_max(int v)
+{
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1)
+        v = max(v, __shfl_xor(v, o, 64));
+    return v;
+}
+
+/* ======================================================================================= *
+ *  batch seal / open                                                                       *
+ * ======================================================================================= */
+
+/* one GHASH element of a lane: which of AAD / ciphertext / length block it is */
+struct Elem {
+    bool active, is_aad, is_c, is_len;
+    int i, c, nbytes;
+};
+
+__device__ __forceinline__ Elem elem_of(int i, int N, int na, int nc, int L)
+{
+    Elem e;
+    e.i = i;
+    e.active = i < N;
+    e.is_aad = i < na;
+    e.is_c = !e.is_aad && i < na + nc;
+    e.is_len = e.active && i == N - 1;
+    e.c = i - na;
+    e.nbytes = e.is_c ? min(16, L - 16 * e.c) : 0;
+    return e;
+}
+
+template <bool OPEN, bool ALIGNED>
+__device__ __forceinline__ V4 finish_elem(const Elem &e, V4 in_blk, V4 ks, const uint8_t *aad_p, int A, int L, uint8_t *out_p,
+                                          V4 &ek0)
+{
+    V4 x = V4{0, 0, 0, 0};
+    if (e.is_aad) {
+        x = load_block<ALIGNED>(aad_p + 16 * e.i, min(16, A - 16 * e.i));
+    } else if (e.is_c) {
+        const V4 o = v4xor(in_blk, ks);
+        if (OPEN) {
+            store_block<ALIGNED>(out_p + 16 * (size_t)e.c, e.nbytes, o);
+            x = in_blk;
+        } else {
+            x = mask_block(o, e.nbytes);
+            store_block<ALIGNED>(out_p + 16 * (size_t)e.c, e.nbytes, x);
+        }
+    } else if (e.is_len) { /* [len(A)]64 || [len(C)]64 in bits, big-endian (lib/fusion.c:468) */
+        x = V4{0, bswap32((uint32_t)A << 3), 0, bswap32((uint32_t)L << 3)};
+        ek0 = ks;
+    }
+    return x;
+}
+
+/* Pointers are separate __restrict__ kernel parameters (not a struct) so the compiler can prove that
+ * the key slots, tables and descriptors are never written by the kernel and read them through the
+ * scalar unit (s_load into SGPRs) instead of per-lane vector loads.  in/out may alias (in place). */
+template <int G, int ROUNDS, bool OPEN, bool ALIGNED, int WGT>
+__global__ void __launch_bounds__(WGT)
+    aesgcm_batch_kernel(const ptls_hip_record_t *__restrict__ recs, const uint32_t *__restrict__ order,
+                        const Chunk *__restrict__ chunks, uint32_t nchunks,
+                        const uint8_t *in, const uint8_t *__restrict__ aad, uint8_t *out, uint64_t *__restrict__ result,
+                        const KeySlot *__restrict__ slots, const uint32_t *__restrict__ basis, const uint32_t *__restrict__ t0,
+                        const ptls_hip_supp_t *__restrict__ supp, const KeySlot *__restrict__ hp_slots, uint8_t *mask)
+{
+    constexpr int LOG2G = G == 1 ? 0 : G == 2 ? 1 : G == 4 ? 2 : G == 8 ? 3 : 4;
+    __shared__ __attribute__((aligned(16))) uint8_t lds[lds_bytes(LOG2G)];
+    constexpr int R = 64 / G; /* records per wave task */
+
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    const uint32_t lb_aes = (uint32_t)(lane & 31) * 4u | LDS_AES;
+    const GhLane gl = gh_lane_init(lane);
+    const int r = lane & (G - 1);
+    const int grp = lane >> LOG2G;
+
+    build_aes_tables(lds, t0);
+    uint32_t cur_key = 0xffffffffu;
+
+    for (uint32_t ci = blockIdx.x; ci < nchunks; ci += gridDim.x) {
+        const Chunk ch = chunks[ci];
+        if (ch.key != cur_key) {
+            __syncthreads();
+            build_ghash_tables(lds, basis + (size_t)ch.key * (NPOW * 128 * 4), LOG2G);
+            __syncthreads();
+            cur_key = ch.key;
+        }
+        const KeySlot *__restrict__ slot = slots + ch.key;
+        const uint32_t *__restrict__ rk = slot->rk;
+        const int ntasks = (int)((ch.count + R - 1) / R);
+
+        /* snake order over the chunk's tasks (records sorted by decreasing length): the waves that drew the
+         * longest tasks in one pass draw the shortest ones in the next */
+        constexpr int NW = WGT / 64;
+        for (int pass = 0;; ++pass) {
+            const int t = pass * NW + ((pass & 1) ? NW - 1 - wave : wave);
+            if (t >= ntasks)
+                break;
+            const uint32_t ridx = (uint32_t)t * R + grp;
+            const bool valid = ridx < ch.count;
+            const uint32_t rec_i = order[ch.first + (valid ? ridx : 0)];
+            const ptls_hip_record_t rec = recs[rec_i];
+            const int L = valid ? (int)rec.len : 0;
+            const int A = valid ? (int)rec.aad_len : 0;
+            const int na = (A + 15) >> 4, nc = (L + 15) >> 4;
+            const int N = valid ? na + nc + 1 : 0;
+            const int i0 = (r + na) & (G - 1);
+            const int my_iters = i0 < N ? ((N - 1 - i0) >> LOG2G) + 1 : 0;
+            const int iters = wave_max(my_iters);
+
+            /* seal of a TLS 1.3 record: the last plaintext byte is the content type, not input */
+            const bool tflag = !OPEN && (rec.flags & 1u) != 0 && L > 0;
+            const uint32_t ttype = (rec.flags >> 8) & 0xffu;
+            const uint8_t *in_p = in + rec.in_off;
+            uint8_t *out_p = out + rec.out_off;
+            const uint8_t *aad_p = aad + rec.aad_off;
+            const uint32_t n0 = slot->iv[0], n1 = slot->iv[1] ^ bswap32((uint32_t)(rec.seq >> 32)),
+                           n2 = slot->iv[2] ^ bswap32((uint32_t)rec.seq);
+
+            V4 y = V4{0, 0, 0, 0}, ek0 = V4{0, 0, 0, 0};
+            /* Iterations handle two Horner elements (i and i + G) of a lane; their AES blocks are independent
+             * and run interleaved.  y = y * P ^ x is exact from y = 0 (0 * P = 0), so no first-element case. */
+            auto generic_iter_m = [&](int m) {
+                const Elem e0 = elem_of(i0 + m * G, N, na, nc, L);
+                V4 in0 = V4{0, 0, 0, 0};
+                if (e0.is_c) {
+                    const bool tb = tflag && e0.c == nc - 1; /* the block holding the content-type byte */
+                    in0 = load_block<ALIGNED>(in_p + 16 * (size_t)e0.c, e0.nbytes - (tb ? 1 : 0));
+                    if (tb)
+                        in0 = put_byte(in0, e0.nbytes - 1, ttype);
+                }
+                /* keystream for data block c (counter inc32(J0) + c), E_K(J0) for the length-block lane */
+                V4 ks0[1] = {V4{n0, n1, n2, e0.is_c ? bswap32((uint32_t)e0.c + 2u) : 0x01000000u}};
+                aes_encrypt_n<ROUNDS, 1>(lds, lb_aes, rk, ks0);
+                const V4 x0 = finish_elem<OPEN, ALIGNED>(e0, in0, ks0[0], aad_p, A, L, out_p, ek0);
+                if (e0.active)
+                    y = gh_mul_main(lds, gl, y, x0);
+            };
+
+            /* "pure" stretch: elements m in [pm0, pm1) of every lane of the wave are full, aligned data blocks.
+             * There the body is branch-free and handles KP blocks per iteration, so their AES lookups and the
+             * GHASH lookups of the previous iteration's ciphertext can all be in flight together. */
+            constexpr int KP = PURE_BLOCKS;
+            const int nf = (L - (tflag ? 1 : 0)) >> 4; /* full blocks that are all input bytes */
+            const int my_mlo = na > i0 ? (na - i0 + G - 1) >> LOG2G : 0;
+            /* full blocks only, and (for the counter-mode shortcut) block counters c + 2 < 2^16 */
+            const int lastc = min(nf, 65534) - 1; /* last data block index allowed in the pure stretch */
+            const int my_mhi = (valid && na + lastc - i0 >= 0) ? ((na + lastc - i0) >> LOG2G) + 1 : 0;
+            const int pm0 = wave_max(my_mlo);
+            const int pm_hi = -wave_max(-my_mhi);
+            const int npure = pm_hi > pm0 ? (pm_hi - pm0) / KP : 0;
+            const int pm1 = pm0 + npure * KP;
+
+            for (int j = 0; j < (npure ? pm0 : iters); ++j)
+                generic_iter_m(j);
+            if (npure) {
+                const uint8_t *src = in_p + 16 * (size_t)(i0 - na + pm0 * G);
+                uint8_t *dst = out_p + 16 * (size_t)(i0 - na + pm0 * G);
+                const uint32_t cbase = (uint32_t)(i0 - na + pm0 * G) + 2u;
+#if CTR_SHORTCUT
+                const CtrConst cc = ctr_const(lds, lb_aes, rk, n0, n1, n2);
+#endif
+                V4 pend[KP], bufA[KP], bufB[KP];
+                /* ping-pong prefetch: iteration `it` consumes the buffer loaded one iteration earlier and refills
+                 * the other one for it + 1 (clamped to the last iteration so the body stays branch-free).  Two
+                 * named buffers instead of a copy keep the compiler from waiting on the fresh loads. */
+#pragma unroll
+                for (int b = 0; b < KP; ++b)
+                    bufA[b] = load_full(src + 16 * b * G);
+                /* one branch-free iteration; `hash_pending` is a literal at every call site */
+                auto pure_iter = [&](int it, bool hash_pending, V4(&d)[KP], V4(&dn)[KP]) {
+                    const size_t o = (size_t)(it * KP * G) * 16;
+                    const size_t on = (size_t)(min(it + 1, npure - 1) * KP * G) * 16;
+                    V4 k[KP];
+                    uint32_t cw[KP];
+#pragma unroll
+                    for (int b = 0; b < KP; ++b) {
+                        dn[b] = load_full(src + on + 16 * b * G);
+                        cw[b] = bswap32(cbase + (uint32_t)((it * KP + b) * G));
+                        k[b] = V4{n0, n1, n2, cw[b]};
+                    }
+#if PREFETCH_BARRIER
+                    __builtin_amdgcn_sched_barrier(0); /* keep the prefetch at the top of the iteration */
+#endif
+#if PHASED
+                    if (OPEN) {
+                        ctr_ghash_phased<ROUNDS, KP, true>(lds, lb_aes, rk, cc, cw, k, y, d, gl);
+#pragma unroll
+                        for (int b = 0; b < KP; ++b)
+                            store_full(dst + o + 16 * b * G, v4xor(d[b], k[b]));
+                    } else {
+                        if (hash_pending)
+                            ctr_ghash_phased<ROUNDS, KP, true>(lds, lb_aes, rk, cc, cw, k, y, pend, gl);
+                        else
+                            ctr_ghash_phased<ROUNDS, KP, false>(lds, lb_aes, rk, cc, cw, k, y, pend, gl);
+#pragma unroll
+                        for (int b = 0; b < KP; ++b) {
+                            pend[b] = v4xor(d[b], k[b]);
+                            store_full(dst + o + 16 * b * G, pend[b]);
+                        }
+                    }
+                    return;
+#endif
+#if ABLATE_AES /* timing-only diagnostic build: keystream = counter block */
+#elif CTR_SHORTCUT
+                    aes_ctr_n<ROUNDS, KP>(lds, lb_aes, rk, cc, cw, k);
+#else
+                    aes_encrypt_n<ROUNDS, KP>(lds, lb_aes, rk, k);
+#endif
+                    if (OPEN) {
+                        /* the input is the ciphertext: hash it in the same iteration */
+#pragma unroll
+                        for (int b = 0; b < KP; ++b)
+                            y = gh_mul_main(lds, LANE_FRESH, y, d[b]);
+#pragma unroll
+                        for (int b = 0; b < KP; ++b)
+                            store_full(dst + o + 16 * b * G, v4xor(d[b], k[b]));
+                    } else {
+                        /* software pipelined: the ciphertext of iteration it is hashed during iteration it + 1 */
+                        if (hash_pending) {
+#pragma unroll
+                            for (int b = 0; b < KP; ++b)
+#if ABLATE_GHASH /* timing-only diagnostic build */
+                                y = v4xor(y, pend[b]);
+#else
+                                y = gh_mul_main(lds, LANE_FRESH, y, pend[b]);
+#endif
+                        }
+#pragma unroll
+                        for (int b = 0; b < KP; ++b) {
+                            pend[b] = v4xor(d[b], k[b]);
+                            store_full(dst + o + 16 * b * G, pend[b]);
+                        }
+                    }
+                };
+                pure_iter(0, false, bufA, bufB);
+                int it = 1;
+                for (; it + 1 < npure; it += 2) {
+                    pure_iter(it, true, bufB, bufA);
+                    pure_iter(it + 1, true, bufA, bufB);
+                }
+                if (it < npure)
+                    pure_iter(it, true, bufB, bufA);
+                if (!OPEN) {
+#pragma unroll
+                    for (int b = 0; b < KP; ++b)
+                        y = gh_mul_main(lds, gl, y, pend[b]);
+                }
+                for (int j = pm1; j < iters; ++j)
+                    generic_iter_m(j);
+            }
+
+            /* combine the G partial sums of each record: position q = distance of a lane's last element
+             * from the end of the GHASH input; sum_q y_q * H^(q+1) by a shuffle tree */
+            const int q = (nc - r) & (G - 1);
+#pragma unroll
+            for (int lvl = 0; lvl < LOG2G; ++lvl) {
+                const int d = 1 << lvl;
+                const int src = (lane & ~(G - 1)) | ((r - d) & (G - 1));
+                V4 v;
+                v.w0 = __shfl(y.w0, src, 64);
+                v.w1 = __shfl(y.w1, src, 64);
+                v.w2 = __shfl(y.w2, src, 64);
+                v.w3 = __shfl(y.w3, src, 64);
+                const V4 w = gh_mul_nibble(lds, LDS_GTREE + lvl * LDS_TREE_STRIDE, v);
+                if ((q & (2 * d - 1)) == 0)
+                    y = v4xor(y, w);
+            }
+            if (valid && q == 0) {
+                const V4 s = gh_mul_nibble(lds, LDS_GTREE, y); /* * H */
+                const V4 tag = v4xor(s, ek0);
+                if (OPEN) {
+                    const V4 rt = load_full(in_p + L);
+                    const bool ok = rt.w0 == tag.w0 && rt.w1 == tag.w1 && rt.w2 == tag.w2 && rt.w3 == tag.w3;
+                    result[rec_i] = ok ? (uint64_t)L : ~(uint64_t)0;
+                } else {
+                    store_full(out_p + L, tag);
+                }
+            }
+            if (!OPEN && supp != nullptr) {
+                /* QUIC header protection (fusion's supp, lib/fusion.c:636-650): AES-ECB(hp key, 16 output bytes)
+                 * computed after the record, because the sample may cover the tag.  The sample was written by
+                 * other lanes of this wave: the agent-scope release/acquire pair completes their stores and
+                 * invalidates this CU's L1 before the read. */
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                if (valid && r == 0) {
+                    const ptls_hip_supp_t sp = supp[rec_i];
+                    if (sp.flags & PTLS_HIP_SUPP_ENABLE) {
+                        const V4 sample = load_full(out + sp.sample_off);
+                        const V4 m = aes_encrypt<ROUNDS>(lds, lb_aes, hp_slots[sp.hp_key].rk, sample);
+                        store_full(mask + sp.mask_off, m);
+                    }
+                }
+            }
+        }
+    }
+}
+
+template <int G, int R, bool O, int W>
+static hipError_t launch_one(unsigned grid, hipStream_t s, const KernelArgs &a, bool aligned)
+{
+    if (aligned)
+        hipLaunchKernelGGL((aesgcm_batch_kernel<G, R, O, true, W>), dim3(grid), dim3(W), 0, s, a.recs, a.order, a.chunks,
+                           a.nchunks, a.in, a.aad, a.out, a.result, a.slots, a.basis, a.t0, a.supp, a.hp_slots, a.mask);
+    else
+        hipLaunchKernelGGL((aesgcm_batch_kernel<G, R, O, false, W>), dim3(grid), dim3(W), 0, s, a.recs, a.order, a.chunks,
+                           a.nchunks, a.in, a.aad, a.out, a.result, a.slots, a.basis, a.t0, a.supp, a.hp_slots, a.mask);
+    return hipGetLastError();
+}
+
+template <int G, int R, bool O>
+static hipError_t launch_w(int wg, unsigned grid, hipStream_t s, const KernelArgs &a, bool aligned)
+{
+    return wg == 512 ? launch_one<G, R, O, 512>(grid, s, a, aligned) : launch_one<G, R, O, WG_ALT>(grid, s, a, aligned);
+}
+
+/* every (rounds, open, workgroup, alignment) variant of lanes-per-record G */
+template <int G>
+static int launch_batch_g(int rounds, bool open, int wg, unsigned grid, hipStream_t s, const KernelArgs &a, bool al)
+{
+    hipError_t e;
+    if (rounds == 10)
+        e = open ? launch_w<G, 10, true>(wg, grid, s, a, al) : launch_w<G, 10, false>(wg, grid, s, a, al);
+    else
+        e = open ? launch_w<G, 14, true>(wg, grid, s, a, al) : launch_w<G, 14, false>(wg, grid, s, a, al);
+    return (int)e;
+}
+
+} // namespace ptls_hip
+
+#endif

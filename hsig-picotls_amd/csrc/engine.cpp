@@ -373,16 +373,27 @@ extern "C" int ptls_hip_keyset_xor_iv(ptls_hip_keyset_t *ks, size_t slot, const 
 /* ---------------------------------------------------------------------------------------------- */
 
 /* lanes per record from the mean GHASH length N = ceil(A/16) + ceil(L/16) + 1: keep >= ~16 Horner
- * steps per lane so the log2(G) reduction tree stays a small fraction of the work */
+ * steps per lane so the log2(G) reduction tree stays a small fraction of the work.  Many keys with few
+ * records each (a server's connections): a workgroup works on one key at a time (its GHASH tables fill
+ * the LDS), so with 8 lanes a 64-record key run gives only 8 wave tasks to 12 waves; 16 lanes per
+ * record doubles the tasks per key run (measured on the 64K-key BASELINE shape). */
 static int choose_lanes(const std::vector<ptls_hip_record_t> &recs)
 {
     if (recs.empty())
         return 1;
     double sum = 0;
-    for (const auto &r : recs)
-        sum += (double)((r.aad_len + 15) / 16 + (r.len + 15) / 16 + 1);
+    size_t runs = 1;
+    for (size_t i = 0; i < recs.size(); ++i) {
+        sum += (double)((recs[i].aad_len + 15) / 16 + (recs[i].len + 15) / 16 + 1);
+        if (i != 0 && recs[i].key != recs[i - 1].key)
+            ++runs;
+    }
     const double mean = sum / (double)recs.size();
-    return mean >= 128 ? 8 : mean >= 48 ? 4 : mean >= 16 ? 2 : 1;
+    const double per_run = (double)recs.size() / (double)runs;
+    const int g = mean >= 128 ? 8 : mean >= 48 ? 4 : mean >= 16 ? 2 : 1;
+    if (g == 8 && mean >= 256 && per_run < (double)(WG_ALT / 64) * (64 / 8))
+        return 16;
+    return g;
 }
 
 static int plan_wg(const std::vector<Chunk> &ch, int lanes)
@@ -500,8 +511,8 @@ extern "C" size_t ptls_hip_batch_count(ptls_hip_batch_t *b)
 
 extern "C" int ptls_hip_batch_set_lanes(ptls_hip_batch_t *b, int lanes)
 {
-    if (b == nullptr || !(lanes == 0 || lanes == 1 || lanes == 2 || lanes == 4 || lanes == 8))
-        return fail(PTLS_HIP_EINVAL, "batch_set_lanes: lanes must be 0, 1, 2, 4 or 8");
+    if (b == nullptr || !(lanes == 0 || lanes == 1 || lanes == 2 || lanes == 4 || lanes == 8 || lanes == 16))
+        return fail(PTLS_HIP_EINVAL, "batch_set_lanes: lanes must be 0, 1, 2, 4, 8 or 16");
     DeviceGuard g(b->eng->device);
     const int want = lanes == 0 ? b->auto_lanes : lanes;
     if (want == b->lanes)

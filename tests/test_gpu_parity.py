@@ -25,7 +25,7 @@ from make_golden import CONFIGS, config_record, sweep_inputs  # noqa: E402
 from oracle_lib import tls_aad  # noqa: E402
 
 UINT64_MAX = (1 << 64) - 1
-LANES = (1, 2, 4, 8)
+LANES = (1, 2, 4, 8, 16)
 
 
 def kat_records(golden):
@@ -160,7 +160,7 @@ def test_unaligned_layout(engine, oracle, align):
 
 
 @pytest.mark.parametrize("wg", [512, 768])
-@pytest.mark.parametrize("lanes", [2, 4, 8])
+@pytest.mark.parametrize("lanes", [2, 4, 8, 16])
 def test_key_runs_mixed_lengths(engine, oracle, wg, lanes):
     """BASELINE configs[3] shape in miniature: AES-256, several keys with runs of 150-400 records of
     random 0..6000-byte lengths (the planner reorders each key chunk by length), every workgroup size"""
