@@ -69,6 +69,9 @@ __host__ __device__ constexpr uint32_t lds_bytes(int log2g)
 #if PHASED && !CTR_SHORTCUT
 #error "PHASED needs CTR_SHORTCUT"
 #endif
+#ifndef SKEWED
+#define SKEWED 1 /* ctr_ghash_skewed for KP = 2 (the two blocks half a round apart) */
+#endif
 #ifndef PURE_BLOCKS
 #define PURE_BLOCKS 2 /* data blocks per lane per iteration of the branch-free loop */
 #endif
@@ -455,6 +458,97 @@ __device__ __forceinline__ void ctr_ghash_phased(const uint8_t *lds, uint32_t lb
         }
         __builtin_amdgcn_sched_barrier(0);
     }
+}
+
+/* SKEWED=1 variant of ctr_ghash_phased for KP = 2: the lane's two blocks run half a round apart, so a
+ * wave always has one block's lookups in flight while it XORs the other's.  Segment s issues a quarter
+ * GHASH multiply (s < 8) and round s/2+1 of block s&1, then finishes round (s-1)/2+1 of block (s-1)&1
+ * and folds in the quarter multiply (waits skip the lookups this segment just issued for the AES). */
+template <int ROUNDS, bool HASH>
+__device__ __forceinline__ void ctr_ghash_skewed(const uint8_t *lds, uint32_t lb, const uint32_t *__restrict__ rk, const CtrConst &cc,
+                                                 const uint32_t (&cw)[2], V4 (&ks)[2], V4 &y, const V4 (&hx)[2], const GhLane &g)
+{
+    V4 s[2];
+    uint32_t t0[2], t1[2];
+    RoundLoads R[2];
+    uint32_t M[2][8];
+    V4 G[8];
+    V4 acc = V4{0, 0, 0, 0}, xr = V4{0, 0, 0, 0};
+#pragma unroll
+    for (int seg = 0; seg <= 2 * ROUNDS; ++seg) {
+        const int gj = seg >> 2, gq = seg & 3;
+        const bool gh = HASH && gj < 2;
+        /* ---- issue: GHASH quarter first, then the AES lookups (so the fold below need not wait for them) ---- */
+        if (gh) {
+            if (gq == 0) {
+                xr = gh_rot(g, y);
+                acc = hx[gj];
+            }
+            switch (gq) {
+            case 0: gh_issue<0, 4>(lds, g, xr, G); break;
+            case 1: gh_issue<4, 4>(lds, g, xr, G); break;
+            case 2: gh_issue<8, 4>(lds, g, xr, G); break;
+            default: gh_issue<12, 4>(lds, g, xr, G); break;
+            }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        if (seg < 2 * ROUNDS) {
+            const int b = seg & 1, r = (seg >> 1) + 1;
+            if (r == 1) {
+                const uint32_t x3 = cw[b] ^ cc.r03;
+                M[b][0] = lT2<3>(lds, x3, lb);
+                M[b][1] = lT2<2>(lds, x3, lb);
+            } else if (r == 2) {
+                M[b][0] = lT0<0>(lds, t0[b], lb);
+                M[b][1] = lT0<1>(lds, t1[b], lb);
+                M[b][2] = lT0<0>(lds, t1[b], lb);
+                M[b][3] = lT2<3>(lds, t0[b], lb);
+                M[b][4] = lT2<2>(lds, t0[b], lb);
+                M[b][5] = lT2<3>(lds, t1[b], lb);
+                M[b][6] = lT0<1>(lds, t0[b], lb);
+                M[b][7] = lT2<2>(lds, t1[b], lb);
+            } else if (r < ROUNDS) {
+                round_issue(lds, lb, s[b], R[b]);
+            } else {
+                last_issue(lds, lb, s[b], R[b]);
+            }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        /* ---- finish ---- */
+        if (seg >= 1) {
+            const int b = (seg - 1) & 1, r = ((seg - 1) >> 1) + 1;
+            if (r == 1) {
+                t0[b] = cc.k10 ^ rotl8(M[b][0]);
+                t1[b] = cc.k11 ^ M[b][1];
+            } else if (r == 2) {
+                s[b].w0 = xor3(cc.k20, M[b][0], rotl8(M[b][1]));
+                s[b].w1 = xor3(cc.k21, M[b][2], rotl8(M[b][3]));
+                s[b].w2 = xor3(cc.k22, M[b][4], rotl8(M[b][5]));
+                s[b].w3 = xor3(cc.k23, rotl8(M[b][6]), M[b][7]);
+            } else if (r < ROUNDS) {
+                s[b] = round_finish(R[b], rk + 4 * r);
+            } else {
+                ks[b] = last_finish(R[b], rk + 4 * r);
+            }
+        }
+        if (gh) {
+            acc = v4xor3(acc, G[0], G[1]);
+            acc = v4xor3(acc, G[2], G[3]);
+            if (gq == 3)
+                y = acc;
+        }
+        __builtin_amdgcn_sched_barrier(0);
+    }
+}
+
+template <int ROUNDS, int KP, bool HASH>
+__device__ __forceinline__ void ctr_ghash(const uint8_t *lds, uint32_t lb, const uint32_t *__restrict__ rk, const CtrConst &cc,
+                                          const uint32_t (&cw)[KP], V4 (&ks)[KP], V4 &y, const V4 (&hx)[KP], const GhLane &g)
+{
+    if constexpr (SKEWED && KP == 2)
+        ctr_ghash_skewed<ROUNDS, HASH>(lds, lb, rk, cc, cw, ks, y, hx, g);
+    else
+        ctr_ghash_phased<ROUNDS, KP, HASH>(lds, lb, rk, cc, cw, ks, y, hx, g);
 }
 
 /* K independent blocks, round-interleaved */
@@ -882,6 +976,43 @@ __global__ void __launch_bounds__(WGT)
             V4 y = V4{0, 0, 0, 0}, ek0 = V4{0, 0, 0, 0};
             /* Iterations handle two Horner elements (i and i + G) of a lane; their AES blocks are independent
              * and run interleaved.  y = y * P ^ x is exact from y = 0 (0 * P = 0), so no first-element case. */
+            /* counter-mode shortcut constants of this lane's record (rounds 1-2 of every block with counter < 2^16) */
+            const CtrConst cc = ctr_const(lds, lb_aes, rk, n0, n1, n2);
+
+            /* elements m and m + 1 of the lane (AAD, partial or full data, length block), their two AES blocks
+             * interleaved; the counter-mode shortcut unless some lane of the wave has a counter >= 2^16 */
+            auto generic_pair = [&](int m) {
+                Elem e[2];
+                V4 in[2], ks[2];
+                uint32_t cw[2];
+                int big = 0;
+#pragma unroll
+                for (int b = 0; b < 2; ++b) {
+                    e[b] = elem_of(i0 + (m + b) * G, N, na, nc, L);
+                    in[b] = V4{0, 0, 0, 0};
+                    if (e[b].is_c) {
+                        const bool tb = tflag && e[b].c == nc - 1; /* the block holding the content-type byte */
+                        in[b] = load_block<ALIGNED>(in_p + 16 * (size_t)e[b].c, e[b].nbytes - (tb ? 1 : 0));
+                        if (tb)
+                            in[b] = put_byte(in[b], e[b].nbytes - 1, ttype);
+                    }
+                    /* keystream for data block c (counter inc32(J0) + c), E_K(J0) for the length-block lane */
+                    cw[b] = e[b].is_c ? bswap32((uint32_t)e[b].c + 2u) : 0x01000000u;
+                    ks[b] = V4{n0, n1, n2, cw[b]};
+                    big |= (e[b].is_c && e[b].c >= 65534) ? 1 : 0;
+                }
+                if (wave_max(big))
+                    aes_encrypt_n<ROUNDS, 2>(lds, lb_aes, rk, ks);
+                else
+                    aes_ctr_n<ROUNDS, 2>(lds, lb_aes, rk, cc, cw, ks);
+#pragma unroll
+                for (int b = 0; b < 2; ++b) {
+                    const V4 x = finish_elem<OPEN, ALIGNED>(e[b], in[b], ks[b], aad_p, A, L, out_p, ek0);
+                    if (e[b].active)
+                        y = gh_mul_main(lds, gl, y, x);
+                }
+            };
+
             auto generic_iter_m = [&](int m) {
                 const Elem e0 = elem_of(i0 + m * G, N, na, nc, L);
                 V4 in0 = V4{0, 0, 0, 0};
@@ -913,15 +1044,18 @@ __global__ void __launch_bounds__(WGT)
             const int npure = pm_hi > pm0 ? (pm_hi - pm0) / KP : 0;
             const int pm1 = pm0 + npure * KP;
 
-            for (int j = 0; j < (npure ? pm0 : iters); ++j)
-                generic_iter_m(j);
+            {
+                const int pre = npure ? pm0 : iters;
+                int j = 0;
+                for (; j + 1 < pre; j += 2)
+                    generic_pair(j);
+                if (j < pre)
+                    generic_iter_m(j);
+            }
             if (npure) {
                 const uint8_t *src = in_p + 16 * (size_t)(i0 - na + pm0 * G);
                 uint8_t *dst = out_p + 16 * (size_t)(i0 - na + pm0 * G);
                 const uint32_t cbase = (uint32_t)(i0 - na + pm0 * G) + 2u;
-#if CTR_SHORTCUT
-                const CtrConst cc = ctr_const(lds, lb_aes, rk, n0, n1, n2);
-#endif
                 V4 pend[KP], bufA[KP], bufB[KP];
                 /* ping-pong prefetch: iteration `it` consumes the buffer loaded one iteration earlier and refills
                  * the other one for it + 1 (clamped to the last iteration so the body stays branch-free).  Two
@@ -946,15 +1080,15 @@ __global__ void __launch_bounds__(WGT)
 #endif
 #if PHASED
                     if (OPEN) {
-                        ctr_ghash_phased<ROUNDS, KP, true>(lds, lb_aes, rk, cc, cw, k, y, d, gl);
+                        ctr_ghash<ROUNDS, KP, true>(lds, lb_aes, rk, cc, cw, k, y, d, gl);
 #pragma unroll
                         for (int b = 0; b < KP; ++b)
                             store_full(dst + o + 16 * b * G, v4xor(d[b], k[b]));
                     } else {
                         if (hash_pending)
-                            ctr_ghash_phased<ROUNDS, KP, true>(lds, lb_aes, rk, cc, cw, k, y, pend, gl);
+                            ctr_ghash<ROUNDS, KP, true>(lds, lb_aes, rk, cc, cw, k, y, pend, gl);
                         else
-                            ctr_ghash_phased<ROUNDS, KP, false>(lds, lb_aes, rk, cc, cw, k, y, pend, gl);
+                            ctr_ghash<ROUNDS, KP, false>(lds, lb_aes, rk, cc, cw, k, y, pend, gl);
 #pragma unroll
                         for (int b = 0; b < KP; ++b) {
                             pend[b] = v4xor(d[b], k[b]);
@@ -1008,7 +1142,10 @@ __global__ void __launch_bounds__(WGT)
                     for (int b = 0; b < KP; ++b)
                         y = gh_mul_main(lds, gl, y, pend[b]);
                 }
-                for (int j = pm1; j < iters; ++j)
+                int j = pm1;
+                for (; j + 1 < iters; j += 2)
+                    generic_pair(j); /* an element past the record is inactive: no store, no hash */
+                if (j < iters)
                     generic_iter_m(j);
             }
 
