@@ -76,7 +76,7 @@ __host__ __device__ constexpr uint32_t lds_bytes(int log2g)
 #define PFPRIO 0 /* priority for the prefetch loads too: measured no gain */
 #endif
 #ifndef SKEWED
-#define SKEWED 1 /* ctr_ghash_skewed for KP = 2 (the two blocks half a round apart) */
+#define SKEWED 1 /* ctr_ghash_skewed (the lane's KP blocks 1/KP of a round apart) */
 #endif
 #ifndef PURE_BLOCKS
 #define PURE_BLOCKS 2 /* data blocks per lane per iteration of the branch-free loop */
@@ -466,24 +466,26 @@ __device__ __forceinline__ void ctr_ghash_phased(const uint8_t *lds, uint32_t lb
     }
 }
 
-/* SKEWED=1 variant of ctr_ghash_phased for KP = 2: the lane's two blocks run half a round apart, so a
- * wave always has one block's lookups in flight while it XORs the other's.  Segment s issues a quarter
- * GHASH multiply (s < 8) and round s/2+1 of block s&1, then finishes round (s-1)/2+1 of block (s-1)&1
- * and folds in the quarter multiply (waits skip the lookups this segment just issued for the AES). */
-template <int ROUNDS, bool HASH>
+/* SKEWED=1 variant of ctr_ghash_phased: the lane's KP blocks run 1/KP of a round apart, so a wave always
+ * has lookups in flight while it XORs.  Segment s issues a quarter GHASH multiply (s < 4 KP) and round
+ * s/KP+1 of block s%KP, then finishes the round that block (s-KP+1)%KP issued KP-1 segments earlier and
+ * folds in the quarter multiply (its lookups go out first, so the fold does not wait for the AES ones). */
+template <int ROUNDS, int KP, bool HASH>
 __device__ __forceinline__ void ctr_ghash_skewed(const uint8_t *lds, uint32_t lb, const uint32_t *__restrict__ rk, const CtrConst &cc,
-                                                 const uint32_t (&cw)[2], V4 (&ks)[2], V4 &y, const V4 (&hx)[2], const GhLane &g)
+                                                 const uint32_t (&cw)[KP], V4 (&ks)[KP], V4 &y, const V4 (&hx)[KP], const GhLane &g)
 {
-    V4 s[2];
-    uint32_t t0[2], t1[2];
-    RoundLoads R[2];
-    uint32_t M[2][8];
+    static_assert(4 * KP <= KP * ROUNDS, "GHASH quarters must fit in the segments");
+    V4 s[KP];
+    uint32_t t0[KP], t1[KP];
+    RoundLoads R[KP];
+    uint32_t M[KP][8];
     V4 G[8];
     V4 acc = V4{0, 0, 0, 0}, xr = V4{0, 0, 0, 0};
+    constexpr int NSEG = KP * ROUNDS + KP - 1;
 #pragma unroll
-    for (int seg = 0; seg <= 2 * ROUNDS; ++seg) {
+    for (int seg = 0; seg < NSEG; ++seg) {
         const int gj = seg >> 2, gq = seg & 3;
-        const bool gh = HASH && gj < 2;
+        const bool gh = HASH && gj < KP;
 #if SETPRIO
         __builtin_amdgcn_s_setprio(SETPRIO); /* a wave about to issue lookups goes first */
 #endif
@@ -501,8 +503,8 @@ __device__ __forceinline__ void ctr_ghash_skewed(const uint8_t *lds, uint32_t lb
             }
         }
         __builtin_amdgcn_sched_barrier(0);
-        if (seg < 2 * ROUNDS) {
-            const int b = seg & 1, r = (seg >> 1) + 1;
+        if (seg < KP * ROUNDS) {
+            const int b = seg % KP, r = seg / KP + 1;
             if (r == 1) {
                 const uint32_t x3 = cw[b] ^ cc.r03;
                 M[b][0] = lT2<3>(lds, x3, lb);
@@ -527,8 +529,9 @@ __device__ __forceinline__ void ctr_ghash_skewed(const uint8_t *lds, uint32_t lb
         __builtin_amdgcn_s_setprio(0);
 #endif
         /* ---- finish ---- */
-        if (seg >= 1) {
-            const int b = (seg - 1) & 1, r = ((seg - 1) >> 1) + 1;
+        if (seg >= KP - 1) {
+            const int fs = seg - (KP - 1); /* the segment that issued the lookups finished here */
+            const int b = fs % KP, r = fs / KP + 1;
             if (r == 1) {
                 t0[b] = cc.k10 ^ rotl8(M[b][0]);
                 t1[b] = cc.k11 ^ M[b][1];
@@ -557,8 +560,8 @@ template <int ROUNDS, int KP, bool HASH>
 __device__ __forceinline__ void ctr_ghash(const uint8_t *lds, uint32_t lb, const uint32_t *__restrict__ rk, const CtrConst &cc,
                                           const uint32_t (&cw)[KP], V4 (&ks)[KP], V4 &y, const V4 (&hx)[KP], const GhLane &g)
 {
-    if constexpr (SKEWED && KP == 2)
-        ctr_ghash_skewed<ROUNDS, HASH>(lds, lb, rk, cc, cw, ks, y, hx, g);
+    if constexpr (SKEWED)
+        ctr_ghash_skewed<ROUNDS, KP, HASH>(lds, lb, rk, cc, cw, ks, y, hx, g);
     else
         ctr_ghash_phased<ROUNDS, KP, HASH>(lds, lb, rk, cc, cw, ks, y, hx, g);
 }
