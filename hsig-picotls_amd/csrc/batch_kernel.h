@@ -977,7 +977,6 @@ __global__ void __launch_bounds__(WGT)
             const int N = valid ? na + nc + 1 : 0;
             const int i0 = (r + na) & (G - 1);
             const int my_iters = i0 < N ? ((N - 1 - i0) >> LOG2G) + 1 : 0;
-            const int iters = wave_max(my_iters);
 
             /* seal of a TLS 1.3 record: the last plaintext byte is the content type, not input */
             const bool tflag = !OPEN && (rec.flags & 1u) != 0 && L > 0;
@@ -1054,18 +1053,21 @@ __global__ void __launch_bounds__(WGT)
             /* full blocks only, and (for the counter-mode shortcut) block counters c + 2 < 2^16 */
             const int lastc = min(nf, 65534) - 1; /* last data block index allowed in the pure stretch */
             const int my_mhi = (valid && na + lastc - i0 >= 0) ? ((na + lastc - i0) >> LOG2G) + 1 : 0;
-            const int pm0 = wave_max(my_mlo);
-            const int pm_hi = -wave_max(-my_mhi);
-            const int npure = pm_hi > pm0 ? (pm_hi - pm0) / KP : 0;
-            const int pm1 = pm0 + npure * KP;
+            /* Each lane starts the stretch at its own first data element (after its AAD elements), so the
+             * lanes without AAD do not spend a generic step on data block 0; the stretch length is the
+             * shortest lane's. */
+            const int pm0 = my_mlo;
+            const int npure = -wave_max(-max(my_mhi - pm0, 0)) / KP;
+            const int pm1 = pm0 + npure * KP; /* per lane: first element after the stretch */
 
-            {
-                const int pre = npure ? pm0 : iters;
-                int j = 0;
-                for (; j + 1 < pre; j += 2)
-                    generic_pair(j);
-                if (j < pre)
-                    generic_iter_m(j);
+            /* AAD elements: GHASH only (no keystream); y = 0 * P ^ x = x for the first one */
+            const int naad = wave_max(my_mlo);
+            for (int j = 0; j < naad; ++j) {
+                if (j < my_mlo) {
+                    const Elem e = elem_of(i0 + j * G, N, na, nc, L);
+                    const V4 x = load_block<ALIGNED>(aad_p + 16 * e.i, min(16, A - 16 * e.i));
+                    y = j == 0 ? x : gh_mul_main(lds, gl, y, x);
+                }
             }
             if (npure) {
                 const uint8_t *src = in_p + 16 * (size_t)(i0 - na + pm0 * G);
@@ -1160,11 +1162,16 @@ __global__ void __launch_bounds__(WGT)
                     for (int b = 0; b < KP; ++b)
                         y = gh_mul_main(lds, gl, y, pend[b]);
                 }
-                int j = pm1;
-                for (; j + 1 < iters; j += 2)
-                    generic_pair(j); /* an element past the record is inactive: no store, no hash */
-                if (j < iters)
-                    generic_iter_m(j);
+            }
+            /* the rest of each lane's elements from its own position (full blocks past the shortest lane's
+             * stretch, the partial block, the length block); an element past the record is inactive */
+            {
+                const int rest = wave_max(max(my_iters - pm1, 0));
+                int j = 0;
+                for (; j + 1 < rest; j += 2)
+                    generic_pair(pm1 + j);
+                if (j < rest)
+                    generic_iter_m(pm1 + j);
             }
 
             /* combine the G partial sums of each record: position q = distance of a lane's last element
