@@ -434,7 +434,7 @@ def main():
     ceil = lds_issue_ceiling(cfg["key_len"])
     ceil["frac"] = round(result["seal_gibps"] / world / ceil["seal_gibps"], 4)
     result["roofline"]["lds_issue_ceiling"] = ceil
-    if not args.no_e2e:
+    if not args.no_e2e and world == 1:  # PCIe path is per GPU; at N > 1 the ranks would share the host links
         result["host_e2e"] = host_e2e(args, cfg, eng, ks, recs, lens, d_pt, d_aad, aad_len)
     tfile = os.path.join(ROOT, "profiles", f"traffic_{args.config}.json")
     if os.path.exists(tfile):
