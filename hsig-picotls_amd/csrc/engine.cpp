@@ -846,9 +846,17 @@ struct Span {
     uint64_t lo, hi;
 };
 
+/* what a pipeline slice runs: plain seal / open (AAD in its own buffer), or the TLS 1.3 record layer
+ * (seal: the 5-byte headers are written into the output and read back as the AAD, like
+ * ptls_hip_tls13_seal_batch; open: the AAD is the header in the received input, and the inner plaintext
+ * is parsed after the open, like ptls_hip_tls13_open_batch) */
+enum PipeMode { PIPE_SEAL, PIPE_OPEN, PIPE_TLS13_SEAL, PIPE_TLS13_OPEN };
+
 static int pipeline_run(ptls_hip_pipeline_t *p, ptls_hip_keyset_t *ks, const ptls_hip_record_t *recs, size_t n, const void *h_in,
-                        const void *h_aad, void *h_out, uint64_t *h_result, bool open)
+                        const void *h_aad, void *h_out, uint64_t *h_result, PipeMode mode)
 {
+    const bool open = mode == PIPE_OPEN || mode == PIPE_TLS13_OPEN;
+    const bool aad_in_out = mode == PIPE_TLS13_SEAL, aad_in_in = mode == PIPE_TLS13_OPEN;
     if (p == nullptr || ks == nullptr || ks->eng != p->eng || (n != 0 && (recs == nullptr || h_in == nullptr || h_out == nullptr)) ||
         (open && h_result == nullptr))
         return fail(PTLS_HIP_EINVAL, "pipeline seal/open: bad arguments");
@@ -870,6 +878,13 @@ static int pipeline_run(ptls_hip_pipeline_t *p, ptls_hip_keyset_t *ks, const ptl
             Span ni{std::min(in.lo, r.in_off), std::max(in.hi, r.in_off + r.len + tag_in)};
             Span no{std::min(out.lo, r.out_off), std::max(out.hi, r.out_off + r.len + tag_out)};
             Span na{std::min(ad.lo, r.aad_off), std::max(ad.hi, r.aad_off + r.aad_len)};
+            if (aad_in_out) { /* the header is part of the output span */
+                no = Span{std::min(no.lo, r.aad_off), std::max(no.hi, r.aad_off + r.aad_len)};
+                na = Span{UINT64_MAX, 0};
+            } else if (aad_in_in) { /* the header is part of the input span */
+                ni = Span{std::min(ni.lo, r.aad_off), std::max(ni.hi, r.aad_off + r.aad_len)};
+                na = Span{UINT64_MAX, 0};
+            }
             if (j > i && (ni.hi - ni.lo > p->slice_bytes || no.hi - no.lo > p->slice_bytes || na.hi - na.lo > p->slice_bytes / 4))
                 break;
             in = ni;
@@ -877,8 +892,10 @@ static int pipeline_run(ptls_hip_pipeline_t *p, ptls_hip_keyset_t *ks, const ptl
             ad = na;
             ++j;
         }
-        if (in.hi - in.lo > p->slice_bytes || out.hi - out.lo > p->slice_bytes || ad.hi - ad.lo > p->slice_bytes / 4)
+        if (in.hi - in.lo > p->slice_bytes || out.hi - out.lo > p->slice_bytes || (ad.hi > ad.lo && ad.hi - ad.lo > p->slice_bytes / 4))
             return fail(PTLS_HIP_EINVAL, "pipeline: record %zu does not fit a %zu-byte slice", i, p->slice_bytes);
+        if (ad.hi <= ad.lo)
+            ad = Span{0, 0};
         PipeSlot &s = p->slot[k % NSLOT];
         if (s.busy)
             HIP_TRY(hipEventSynchronize(s.done), PTLS_HIP_ENODEV);
@@ -889,7 +906,7 @@ static int pipeline_run(ptls_hip_pipeline_t *p, ptls_hip_keyset_t *ks, const ptl
             s.h_recs[t] = recs[i + t];
             s.h_recs[t].in_off -= in_base;
             s.h_recs[t].out_off -= out_base;
-            s.h_recs[t].aad_off -= aad_base;
+            s.h_recs[t].aad_off -= aad_in_out ? out_base : aad_in_in ? in_base : aad_base;
         }
         int lanes;
         {
@@ -909,13 +926,19 @@ static int pipeline_run(ptls_hip_pipeline_t *p, ptls_hip_keyset_t *ks, const ptl
         if (ad.hi > ad.lo)
             HIP_TRY(hipMemcpyAsync(s.d_aad + (ad.lo - aad_base), haad + ad.lo, ad.hi - ad.lo, hipMemcpyHostToDevice, s.stream),
                     PTLS_HIP_ENODEV);
+        const unsigned egrid = (unsigned)std::min<size_t>((cnt + 255) / 256, (size_t)p->eng->ncu * 4);
+        if (aad_in_out) {
+            const int eh = launch_tls13_headers(s.d_recs, (uint32_t)cnt, s.d_out, egrid, s.stream);
+            if (eh != 0)
+                return fail(PTLS_HIP_ELAUNCH, "pipeline: header kernel launch failed: %s", hipGetErrorString((hipError_t)eh));
+        }
         KernelArgs a{};
         a.recs = s.d_recs;
         a.order = s.d_order;
         a.chunks = s.d_chunks;
         a.nchunks = (uint32_t)ch.size();
         a.in = s.d_in;
-        a.aad = s.d_aad;
+        a.aad = aad_in_out ? s.d_out : aad_in_in ? s.d_in : s.d_aad;
         a.out = s.d_out;
         a.result = s.d_result;
         a.slots = ks->d_slots;
@@ -925,6 +948,11 @@ static int pipeline_run(ptls_hip_pipeline_t *p, ptls_hip_keyset_t *ks, const ptl
         const int e = launch_batch(lanes, rounds, open, plan_wg(ch, lanes), grid, s.stream, a, aligned);
         if (e != 0)
             return fail(PTLS_HIP_ELAUNCH, "pipeline: kernel launch failed: %s", hipGetErrorString((hipError_t)e));
+        if (mode == PIPE_TLS13_OPEN) {
+            const int ei = launch_tls13_inner(s.d_recs, (uint32_t)cnt, s.d_out, s.d_result, egrid, s.stream);
+            if (ei != 0)
+                return fail(PTLS_HIP_ELAUNCH, "pipeline: inner-plaintext kernel launch failed: %s", hipGetErrorString((hipError_t)ei));
+        }
         HIP_TRY(hipMemcpyAsync(hout + out.lo, s.d_out + (out.lo - out_base), out.hi - out.lo, hipMemcpyDeviceToHost, s.stream),
                 PTLS_HIP_ENODEV);
         if (open) {
@@ -948,13 +976,25 @@ static int pipeline_run(ptls_hip_pipeline_t *p, ptls_hip_keyset_t *ks, const ptl
 extern "C" int ptls_hip_pipeline_seal(ptls_hip_pipeline_t *p, ptls_hip_keyset_t *ks, const ptls_hip_record_t *recs, size_t n,
                                       const void *h_in, const void *h_aad, void *h_out)
 {
-    return pipeline_run(p, ks, recs, n, h_in, h_aad, h_out, nullptr, false);
+    return pipeline_run(p, ks, recs, n, h_in, h_aad, h_out, nullptr, PIPE_SEAL);
+}
+
+extern "C" int ptls_hip_pipeline_tls13_seal(ptls_hip_pipeline_t *p, ptls_hip_keyset_t *ks, const ptls_hip_record_t *recs, size_t n,
+                                            const void *h_in, void *h_wire)
+{
+    return pipeline_run(p, ks, recs, n, h_in, nullptr, h_wire, nullptr, PIPE_TLS13_SEAL);
+}
+
+extern "C" int ptls_hip_pipeline_tls13_open(ptls_hip_pipeline_t *p, ptls_hip_keyset_t *ks, const ptls_hip_record_t *recs, size_t n,
+                                            const void *h_wire, void *h_out, uint64_t *h_result)
+{
+    return pipeline_run(p, ks, recs, n, h_wire, nullptr, h_out, h_result, PIPE_TLS13_OPEN);
 }
 
 extern "C" int ptls_hip_pipeline_open(ptls_hip_pipeline_t *p, ptls_hip_keyset_t *ks, const ptls_hip_record_t *recs, size_t n,
                                       const void *h_in, const void *h_aad, void *h_out, uint64_t *h_result)
 {
-    return pipeline_run(p, ks, recs, n, h_in, h_aad, h_out, h_result, true);
+    return pipeline_run(p, ks, recs, n, h_in, h_aad, h_out, h_result, PIPE_OPEN);
 }
 
 /* ---------------------------------------------------------------------------------------------- */

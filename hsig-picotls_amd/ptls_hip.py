@@ -70,6 +70,8 @@ SIGNATURES = {
     "ptls_hip_pipeline_free": (None, [_vp]),
     "ptls_hip_pipeline_seal": (_i, [_vp, _vp, _vp, _sz, _vp, _vp, _vp]),
     "ptls_hip_pipeline_open": (_i, [_vp, _vp, _vp, _sz, _vp, _vp, _vp, _vp]),
+    "ptls_hip_pipeline_tls13_seal": (_i, [_vp, _vp, _vp, _sz, _vp, _vp]),
+    "ptls_hip_pipeline_tls13_open": (_i, [_vp, _vp, _vp, _sz, _vp, _vp, _vp]),
     "ptls_hip_host_register": (_i, [_vp, _sz]),
     "ptls_hip_host_unregister": (_i, [_vp]),
 }
@@ -275,6 +277,18 @@ class Pipeline:
         recs = np.ascontiguousarray(recs, dtype=RECORD_DTYPE)
         _check(lib().ptls_hip_pipeline_open(self.ptr, keyset.ptr, recs.ctypes.data, len(recs), _ptr(h_in), _ptr(h_aad),
                                             _ptr(h_out), _ptr(h_result)), "pipeline_open")
+
+    def tls13_seal(self, keyset, recs, h_in, h_wire):
+        """recs from tls13_frame: messages in h_in -> header + ciphertext + tag of every record in h_wire"""
+        recs = np.ascontiguousarray(recs, dtype=RECORD_DTYPE)
+        _check(lib().ptls_hip_pipeline_tls13_seal(self.ptr, keyset.ptr, recs.ctypes.data, len(recs), _ptr(h_in), _ptr(h_wire)),
+               "pipeline_tls13_seal")
+
+    def tls13_open(self, keyset, recs, h_wire, h_out, h_result):
+        """recs from tls13_parse: received stream h_wire -> inner content in h_out, length | type << 56 in h_result"""
+        recs = np.ascontiguousarray(recs, dtype=RECORD_DTYPE)
+        _check(lib().ptls_hip_pipeline_tls13_open(self.ptr, keyset.ptr, recs.ctypes.data, len(recs), _ptr(h_wire), _ptr(h_out),
+                                                  _ptr(h_result)), "pipeline_tls13_open")
 
     def close(self):
         if self.ptr:

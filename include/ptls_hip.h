@@ -232,6 +232,14 @@ int ptls_hip_pipeline_seal(ptls_hip_pipeline_t *p, ptls_hip_keyset_t *ks, const 
                            const void *h_in, const void *h_aad, void *h_out);
 int ptls_hip_pipeline_open(ptls_hip_pipeline_t *p, ptls_hip_keyset_t *ks, const ptls_hip_record_t *recs, size_t n,
                            const void *h_in, const void *h_aad, void *h_out, uint64_t *h_result);
+/* The TLS 1.3 record layer from and to host memory (socket buffers): `recs` from ptls_hip_tls13_frame
+ * (seal: h_in holds the messages, h_wire receives header + ciphertext + tag of every record) or from
+ * ptls_hip_tls13_parse (open: h_wire is the received stream, h_out receives the inner content, h_result
+ * is as in ptls_hip_tls13_open_batch).  Same slicing and overlap as ptls_hip_pipeline_seal/open. */
+int ptls_hip_pipeline_tls13_seal(ptls_hip_pipeline_t *p, ptls_hip_keyset_t *ks, const ptls_hip_record_t *recs, size_t n,
+                                 const void *h_in, void *h_wire);
+int ptls_hip_pipeline_tls13_open(ptls_hip_pipeline_t *p, ptls_hip_keyset_t *ks, const ptls_hip_record_t *recs, size_t n,
+                                 const void *h_wire, void *h_out, uint64_t *h_result);
 int ptls_hip_host_register(void *ptr, size_t len);
 int ptls_hip_host_unregister(void *ptr);
 

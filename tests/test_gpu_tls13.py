@@ -27,8 +27,9 @@ def conn_secrets(bits, n, seed):
 
 
 @needs_ref
+@pytest.mark.parametrize("path", ["device", "pipeline"])
 @pytest.mark.parametrize("bits", [128, 256])
-def test_tls13_seal_batch_equals_ptls_send(engine, oracle, bits):
+def test_tls13_seal_batch_equals_ptls_send(engine, oracle, bits, path):
     """many connections x messages of 0..40000 bytes and three content types, framed + sealed in one
     batch; every connection's wire bytes == the reference's ptls_send (appdata) or its restatement
     (other content types, same code path with `type`, lib/picotls.c:747-794)"""
@@ -64,24 +65,35 @@ def test_tls13_seal_batch_equals_ptls_send(engine, oracle, bits):
     h_in = np.zeros(in_off + 16, np.uint8)
     for m, p in zip(marr, payloads):
         h_in[m["in_off"]: m["in_off"] + len(p)] = np.frombuffer(p, np.uint8)
-    d_in = torch.from_numpy(h_in).cuda()
-    d_out = torch.zeros(out_off + 3 * len(msgs) + 16, dtype=torch.uint8, device="cuda")
-    b = ptls_hip.Batch(engine, recs)
-    b.tls13_seal(ks, d_in, d_out)
-    torch.cuda.synchronize()
-    out = d_out.cpu().numpy()
+    b = None
+    if path == "device":
+        d_in = torch.from_numpy(h_in).cuda()
+        d_out = torch.zeros(out_off + 3 * len(msgs) + 16, dtype=torch.uint8, device="cuda")
+        b = ptls_hip.Batch(engine, recs)
+        b.tls13_seal(ks, d_in, d_out)
+        torch.cuda.synchronize()
+        out = d_out.cpu().numpy()
+    else:  # host-resident: pinned message buffer -> pinned wire buffer, 64 KiB slices (many slices, 3 streams)
+        p_in = torch.from_numpy(h_in).pin_memory()
+        p_out = torch.zeros(out_off + 3 * len(msgs) + 16, dtype=torch.uint8).pin_memory()
+        pipe = ptls_hip.Pipeline(engine, 64 << 10)
+        pipe.tls13_seal(ks, recs, p_in, p_out)
+        pipe.close()
+        out = p_out.numpy()
     for i, (m, wire) in enumerate(zip(marr, expect)):
         got = out[m["out_off"]: m["out_off"] + len(wire)].tobytes()
         assert got == wire, (i, int(m["len"]), int(m["type"]))
     for r in refs:
         r.close()
-    b.close()
+    if b is not None:
+        b.close()
     ks.close()
 
 
 @needs_ref
+@pytest.mark.parametrize("path", ["device", "pipeline"])
 @pytest.mark.parametrize("bits", [128, 256])
-def test_tls13_open_batch_equals_ptls_receive(engine, oracle, bits):
+def test_tls13_open_batch_equals_ptls_receive(engine, oracle, bits, path):
     """a received byte stream (ptls_send output, plus records with TLSInnerPlaintext padding, an all-zero
     record and a tampered one) is parsed on the host and opened in one batch: content, content type and
     picotls's errors (BAD_RECORD_MAC, UNEXPECTED_MESSAGE) as handle_input decides them (lib/picotls.c:5866-5883)"""
@@ -113,14 +125,26 @@ def test_tls13_open_batch_equals_ptls_receive(engine, oracle, bits):
     assert consumed == len(stream) and len(recs) == len(expect)
     ks = ptls_hip.KeySet(engine, bits // 8, 1)
     ks.set(0, key, iv)
-    b = ptls_hip.Batch(engine, recs)
-    d_in = torch.from_numpy(np.frombuffer(stream + bytes(16), np.uint8).copy()).cuda()
-    d_out = torch.zeros(int(recs["out_off"][-1] + recs["len"][-1]) + 32, dtype=torch.uint8, device="cuda")
-    d_res = torch.zeros(len(recs), dtype=torch.int64, device="cuda")
-    b.tls13_open(ks, d_in, d_out, d_res)
-    torch.cuda.synchronize()
-    out = d_out.cpu().numpy()
-    res = [int(x) & ((1 << 64) - 1) for x in d_res.cpu().numpy()]
+    out_size = int(recs["out_off"][-1] + recs["len"][-1]) + 32
+    b = None
+    if path == "device":
+        b = ptls_hip.Batch(engine, recs)
+        d_in = torch.from_numpy(np.frombuffer(stream + bytes(16), np.uint8).copy()).cuda()
+        d_out = torch.zeros(out_size, dtype=torch.uint8, device="cuda")
+        d_res = torch.zeros(len(recs), dtype=torch.int64, device="cuda")
+        b.tls13_open(ks, d_in, d_out, d_res)
+        torch.cuda.synchronize()
+        out = d_out.cpu().numpy()
+        res = [int(x) & ((1 << 64) - 1) for x in d_res.cpu().numpy()]
+    else:  # host-resident: the received stream in pinned memory, 64 KiB slices
+        p_in = torch.from_numpy(np.frombuffer(stream + bytes(16), np.uint8).copy()).pin_memory()
+        p_out = torch.zeros(out_size, dtype=torch.uint8).pin_memory()
+        p_res = torch.zeros(len(recs), dtype=torch.int64).pin_memory()
+        pipe = ptls_hip.Pipeline(engine, 64 << 10)
+        pipe.tls13_open(ks, recs, p_in, p_out, p_res)
+        pipe.close()
+        out = p_out.numpy()
+        res = [int(x) & ((1 << 64) - 1) for x in p_res.numpy()]
     for r, v, (kind, ctype, content) in zip(recs, res, expect):
         if kind == "badmac":
             assert v == ptls_hip.TLS13_BAD_RECORD_MAC
@@ -139,7 +163,8 @@ def test_tls13_open_batch_equals_ptls_receive(engine, oracle, bits):
         got += pt
     assert got == b"".join(c for k, t, c in expect if k == "ok" and t == 23)[: len(got)]
     for o in (b, ks, sender, receiver):
-        o.close()
+        if o is not None:
+            o.close()
 
 
 @needs_ref
