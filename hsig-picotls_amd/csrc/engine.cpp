@@ -751,15 +751,17 @@ static const int NSLOT = 3;
 struct PipeSlot {
     hipStream_t stream;
     hipEvent_t done;
-    uint8_t *d_in, *d_out, *d_aad;
+    uint8_t *d_in, *d_out, *d_aad, *d_mask;
     ptls_hip_record_t *d_recs;
     Chunk *d_chunks;
     uint32_t *d_order;
     uint64_t *d_result;
-    /* pinned host staging for the slice's descriptors / chunks / record order */
+    ptls_hip_supp_t *d_supp;
+    /* pinned host staging for the slice's descriptors / chunks / record order / header-protection descriptors */
     ptls_hip_record_t *h_recs;
     Chunk *h_chunks;
     uint32_t *h_order;
+    ptls_hip_supp_t *h_supp;
     bool busy;
 };
 
@@ -785,7 +787,9 @@ extern "C" ptls_hip_pipeline_t *ptls_hip_pipeline_new(ptls_hip_engine_t *eng, si
         ok = ok && hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking) == hipSuccess &&
              hipEventCreateWithFlags(&s.done, hipEventDisableTiming) == hipSuccess &&
              hipMalloc(&s.d_in, slice_bytes + 64) == hipSuccess && hipMalloc(&s.d_out, slice_bytes + 64) == hipSuccess &&
-             hipMalloc(&s.d_aad, slice_bytes / 4 + 64) == hipSuccess &&
+             hipMalloc(&s.d_aad, slice_bytes / 4 + 64) == hipSuccess && hipMalloc(&s.d_mask, slice_bytes / 4 + 64) == hipSuccess &&
+             hipMalloc(&s.d_supp, p->max_recs * sizeof(ptls_hip_supp_t)) == hipSuccess &&
+             hipHostMalloc(&s.h_supp, p->max_recs * sizeof(ptls_hip_supp_t), hipHostMallocDefault) == hipSuccess &&
              hipMalloc(&s.d_recs, p->max_recs * sizeof(ptls_hip_record_t)) == hipSuccess &&
              hipMalloc(&s.d_chunks, p->max_recs * sizeof(Chunk)) == hipSuccess &&
              hipMalloc(&s.d_order, p->max_recs * sizeof(uint32_t)) == hipSuccess &&
@@ -814,6 +818,9 @@ extern "C" void ptls_hip_pipeline_free(ptls_hip_pipeline_t *p)
         (void)hipFree(s.d_in);
         (void)hipFree(s.d_out);
         (void)hipFree(s.d_aad);
+        (void)hipFree(s.d_mask);
+        (void)hipFree(s.d_supp);
+        (void)hipHostFree(s.h_supp);
         (void)hipFree(s.d_recs);
         (void)hipFree(s.d_chunks);
         (void)hipFree(s.d_order);
@@ -853,8 +860,14 @@ struct Span {
 enum PipeMode { PIPE_SEAL, PIPE_OPEN, PIPE_TLS13_SEAL, PIPE_TLS13_OPEN };
 
 static int pipeline_run(ptls_hip_pipeline_t *p, ptls_hip_keyset_t *ks, const ptls_hip_record_t *recs, size_t n, const void *h_in,
-                        const void *h_aad, void *h_out, uint64_t *h_result, PipeMode mode)
+                        const void *h_aad, void *h_out, uint64_t *h_result, PipeMode mode, ptls_hip_keyset_t *hp_ks = nullptr,
+                        const ptls_hip_supp_t *supp = nullptr, void *h_mask = nullptr)
 {
+    if (supp != nullptr && (mode != PIPE_SEAL || hp_ks == nullptr || ks == nullptr || hp_ks->eng != ks->eng ||
+                            hp_ks->key_size != ks->key_size || h_mask == nullptr))
+        return fail(PTLS_HIP_EINVAL, "pipeline_seal_supp: the header-protection keyset must be on the same engine with the "
+                                     "AEAD's key size, and h_mask must be given");
+    uint8_t *hmask = static_cast<uint8_t *>(h_mask);
     const bool open = mode == PIPE_OPEN || mode == PIPE_TLS13_OPEN;
     const bool aad_in_out = mode == PIPE_TLS13_SEAL, aad_in_in = mode == PIPE_TLS13_OPEN;
     if (p == nullptr || ks == nullptr || ks->eng != p->eng || (n != 0 && (recs == nullptr || h_in == nullptr || h_out == nullptr)) ||
@@ -896,6 +909,23 @@ static int pipeline_run(ptls_hip_pipeline_t *p, ptls_hip_keyset_t *ks, const ptl
             return fail(PTLS_HIP_EINVAL, "pipeline: record %zu does not fit a %zu-byte slice", i, p->slice_bytes);
         if (ad.hi <= ad.lo)
             ad = Span{0, 0};
+        /* header protection: masks land in their own span; every enabled sample must lie in the slice's output */
+        Span mk{UINT64_MAX, 0};
+        if (supp != nullptr) {
+            for (size_t t = i; t < j; ++t) {
+                const ptls_hip_supp_t &sp = supp[t];
+                if (!(sp.flags & PTLS_HIP_SUPP_ENABLE))
+                    continue;
+                if (sp.sample_off < out.lo || sp.sample_off + 16 > out.hi)
+                    return fail(PTLS_HIP_EINVAL, "pipeline_seal_supp: sample of record %zu is outside the slice's output", t);
+                mk = Span{std::min(mk.lo, sp.mask_off), std::max(mk.hi, sp.mask_off + 16)};
+            }
+            if (mk.hi > mk.lo && mk.hi - mk.lo > p->slice_bytes / 4)
+                return fail(PTLS_HIP_EINVAL, "pipeline_seal_supp: masks of records %zu..%zu span more than %zu bytes", i, j,
+                            p->slice_bytes / 4);
+            if (mk.hi <= mk.lo)
+                mk = Span{0, 0};
+        }
         PipeSlot &s = p->slot[k % NSLOT];
         if (s.busy)
             HIP_TRY(hipEventSynchronize(s.done), PTLS_HIP_ENODEV);
@@ -915,6 +945,23 @@ static int pipeline_run(ptls_hip_pipeline_t *p, ptls_hip_keyset_t *ks, const ptl
         }
         bool aligned;
         build_chunks(s.h_recs, cnt, lanes, ch, order, aligned);
+        const uint64_t mask_base = mk.lo & ~(uint64_t)15;
+        if (supp != nullptr) {
+            for (size_t t = 0; t < cnt; ++t) {
+                s.h_supp[t] = supp[i + t];
+                if (s.h_supp[t].flags & PTLS_HIP_SUPP_ENABLE) {
+                    s.h_supp[t].sample_off -= out_base;
+                    s.h_supp[t].mask_off -= mask_base;
+                }
+            }
+            HIP_TRY(hipMemcpyAsync(s.d_supp, s.h_supp, cnt * sizeof(ptls_hip_supp_t), hipMemcpyHostToDevice, s.stream),
+                    PTLS_HIP_ENODEV);
+            /* the mask span goes in as well (16 B per packet), so mask bytes of packets without header protection
+             * and between masks come back unchanged */
+            if (mk.hi > mk.lo)
+                HIP_TRY(hipMemcpyAsync(s.d_mask + (mk.lo - mask_base), hmask + mk.lo, mk.hi - mk.lo, hipMemcpyHostToDevice, s.stream),
+                        PTLS_HIP_ENODEV);
+        }
         std::memcpy(s.h_chunks, ch.data(), ch.size() * sizeof(Chunk));
         std::memcpy(s.h_order, order.data(), cnt * sizeof(uint32_t));
         HIP_TRY(hipMemcpyAsync(s.d_order, s.h_order, cnt * sizeof(uint32_t), hipMemcpyHostToDevice, s.stream), PTLS_HIP_ENODEV);
@@ -944,6 +991,11 @@ static int pipeline_run(ptls_hip_pipeline_t *p, ptls_hip_keyset_t *ks, const ptl
         a.slots = ks->d_slots;
         a.basis = ks->d_basis;
         a.t0 = p->eng->d_t0;
+        if (supp != nullptr) {
+            a.supp = s.d_supp;
+            a.hp_slots = hp_ks->d_slots;
+            a.mask = s.d_mask;
+        }
         const unsigned grid = std::min<unsigned>((unsigned)ch.size(), (unsigned)p->eng->ncu);
         const int e = launch_batch(lanes, rounds, open, plan_wg(ch, lanes), grid, s.stream, a, aligned);
         if (e != 0)
@@ -955,6 +1007,9 @@ static int pipeline_run(ptls_hip_pipeline_t *p, ptls_hip_keyset_t *ks, const ptl
         }
         HIP_TRY(hipMemcpyAsync(hout + out.lo, s.d_out + (out.lo - out_base), out.hi - out.lo, hipMemcpyDeviceToHost, s.stream),
                 PTLS_HIP_ENODEV);
+        if (supp != nullptr && mk.hi > mk.lo)
+            HIP_TRY(hipMemcpyAsync(hmask + mk.lo, s.d_mask + (mk.lo - mask_base), mk.hi - mk.lo, hipMemcpyDeviceToHost, s.stream),
+                    PTLS_HIP_ENODEV);
         if (open) {
             /* results come back in slice order; the caller's array is indexed like recs */
             HIP_TRY(hipMemcpyAsync(h_result + i, s.d_result, cnt * sizeof(uint64_t), hipMemcpyDeviceToHost, s.stream),
@@ -977,6 +1032,15 @@ extern "C" int ptls_hip_pipeline_seal(ptls_hip_pipeline_t *p, ptls_hip_keyset_t 
                                       const void *h_in, const void *h_aad, void *h_out)
 {
     return pipeline_run(p, ks, recs, n, h_in, h_aad, h_out, nullptr, PIPE_SEAL);
+}
+
+extern "C" int ptls_hip_pipeline_seal_supp(ptls_hip_pipeline_t *p, ptls_hip_keyset_t *ks, ptls_hip_keyset_t *hp_ks,
+                                           const ptls_hip_record_t *recs, const ptls_hip_supp_t *supp, size_t n, const void *h_in,
+                                           const void *h_aad, void *h_out, void *h_mask)
+{
+    if (n != 0 && supp == nullptr)
+        return fail(PTLS_HIP_EINVAL, "pipeline_seal_supp: supp descriptors missing");
+    return pipeline_run(p, ks, recs, n, h_in, h_aad, h_out, nullptr, PIPE_SEAL, hp_ks, supp, h_mask);
 }
 
 extern "C" int ptls_hip_pipeline_tls13_seal(ptls_hip_pipeline_t *p, ptls_hip_keyset_t *ks, const ptls_hip_record_t *recs, size_t n,

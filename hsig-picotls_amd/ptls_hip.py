@@ -71,6 +71,7 @@ SIGNATURES = {
     "ptls_hip_pipeline_seal": (_i, [_vp, _vp, _vp, _sz, _vp, _vp, _vp]),
     "ptls_hip_pipeline_open": (_i, [_vp, _vp, _vp, _sz, _vp, _vp, _vp, _vp]),
     "ptls_hip_pipeline_tls13_seal": (_i, [_vp, _vp, _vp, _sz, _vp, _vp]),
+    "ptls_hip_pipeline_seal_supp": (_i, [_vp, _vp, _vp, _vp, _vp, _sz, _vp, _vp, _vp, _vp]),
     "ptls_hip_pipeline_tls13_open": (_i, [_vp, _vp, _vp, _sz, _vp, _vp, _vp]),
     "ptls_hip_host_register": (_i, [_vp, _sz]),
     "ptls_hip_host_unregister": (_i, [_vp]),
@@ -277,6 +278,14 @@ class Pipeline:
         recs = np.ascontiguousarray(recs, dtype=RECORD_DTYPE)
         _check(lib().ptls_hip_pipeline_open(self.ptr, keyset.ptr, recs.ctypes.data, len(recs), _ptr(h_in), _ptr(h_aad),
                                             _ptr(h_out), _ptr(h_result)), "pipeline_open")
+
+    def seal_supp(self, keyset, hp_keyset, recs, supp, h_in, h_aad, h_out, h_mask):
+        """seal + QUIC header-protection masks; supp = host numpy array (SUPP_DTYPE) indexed like recs"""
+        recs = np.ascontiguousarray(recs, dtype=RECORD_DTYPE)
+        supp = np.ascontiguousarray(supp, dtype=SUPP_DTYPE)
+        _check(lib().ptls_hip_pipeline_seal_supp(self.ptr, keyset.ptr, hp_keyset.ptr, recs.ctypes.data, supp.ctypes.data,
+                                                 len(recs), _ptr(h_in), _ptr(h_aad), _ptr(h_out), _ptr(h_mask)),
+               "pipeline_seal_supp")
 
     def tls13_seal(self, keyset, recs, h_in, h_wire):
         """recs from tls13_frame: messages in h_in -> header + ciphertext + tag of every record in h_wire"""

@@ -224,7 +224,9 @@ int ptls_hip_tls13_open_batch(ptls_hip_batch_t *batch, ptls_hip_keyset_t *ks, co
  * cut the record list into slices whose input / output / AAD byte spans fit a slot and overlap, per
  * slice, H2D copy -> kernel -> D2H copy.  Offsets in `recs` are relative to the host buffers.  The
  * call returns when every output byte (and result) is in host memory.  Host buffers should be
- * pinned (hipHostMalloc'd, or ptls_hip_host_register'ed) for the copies to run asynchronously. */
+ * pinned (hipHostMalloc'd, or ptls_hip_host_register'ed) for the copies to run asynchronously.  Each
+ * slice's output (and mask) span is copied back whole: bytes lying between records inside it are not
+ * preserved (the device-resident batch calls leave them untouched). */
 typedef struct st_ptls_hip_pipeline_t ptls_hip_pipeline_t;
 ptls_hip_pipeline_t *ptls_hip_pipeline_new(ptls_hip_engine_t *engine, size_t slice_bytes);
 void ptls_hip_pipeline_free(ptls_hip_pipeline_t *p);
@@ -232,6 +234,13 @@ int ptls_hip_pipeline_seal(ptls_hip_pipeline_t *p, ptls_hip_keyset_t *ks, const 
                            const void *h_in, const void *h_aad, void *h_out);
 int ptls_hip_pipeline_open(ptls_hip_pipeline_t *p, ptls_hip_keyset_t *ks, const ptls_hip_record_t *recs, size_t n,
                            const void *h_in, const void *h_aad, void *h_out, uint64_t *h_result);
+/* seal + QUIC header-protection masks from and to host memory: `supp` is a HOST array indexed like recs
+ * (offsets relative to h_out / h_mask); every enabled sample must lie inside the output of the records
+ * sealed with it (QUIC: pn_offset + 4 is in the ciphertext).  Masks are written at h_mask + mask_off;
+ * other bytes of h_mask are preserved. */
+int ptls_hip_pipeline_seal_supp(ptls_hip_pipeline_t *p, ptls_hip_keyset_t *ks, ptls_hip_keyset_t *hp_ks,
+                                const ptls_hip_record_t *recs, const ptls_hip_supp_t *supp, size_t n, const void *h_in,
+                                const void *h_aad, void *h_out, void *h_mask);
 /* The TLS 1.3 record layer from and to host memory (socket buffers): `recs` from ptls_hip_tls13_frame
  * (seal: h_in holds the messages, h_wire receives header + ciphertext + tag of every record) or from
  * ptls_hip_tls13_parse (open: h_wire is the received stream, h_out receives the inner content, h_result

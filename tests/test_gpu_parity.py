@@ -311,8 +311,9 @@ def _supp_array(rows):
     return torch.from_numpy(arr.view(np.uint8)).cuda()
 
 
+@pytest.mark.parametrize("path", ["device", "pipeline"])
 @pytest.mark.parametrize("key_len", [16, 32])
-def test_seal_batch_quic_header_protection(engine, oracle, key_len):
+def test_seal_batch_quic_header_protection(engine, oracle, key_len, path):
     """QUIC header protection fused into the seal launch (fusion's supp,
     lib/fusion.c:424-428, :636-650).  Packets of 20-1500 B with 16-40 B headers as AAD, 3 AEAD keys,
     2 header-protection keys, samples anywhere in ciphertext || tag (incl. covering the tag), some
@@ -334,14 +335,28 @@ def test_seal_batch_quic_header_protection(engine, oracle, key_len):
         enabled = j % 7 != 3
         rows.append((int(rec["out_off"]) + off, 16 * j, j % 2, ptls_hip.SUPP_ENABLE if enabled else 0))
         expect.append((off, j % 2, enabled))
-    d_supp = _supp_array(rows)
-    d_in = torch.from_numpy(hb._input([r[4] for r in recs])).cuda()
-    d_aad = torch.from_numpy(np.concatenate([hb.aad, np.zeros(16, np.uint8)])).cuda()
-    d_out = torch.zeros(hb.out_total + 32, dtype=torch.uint8, device="cuda")
-    d_mask = torch.zeros(16 * len(recs), dtype=torch.uint8, device="cuda")
-    hb.batch.seal_supp(hb.keyset, hp, d_supp, d_in, d_aad, d_out, d_mask)
-    torch.cuda.synchronize()
-    out, mask = d_out.cpu().numpy(), d_mask.cpu().numpy()
+    h_in = hb._input([r[4] for r in recs])
+    h_aad = np.concatenate([hb.aad, np.zeros(16, np.uint8)])
+    if path == "device":
+        d_supp = _supp_array(rows)
+        d_in = torch.from_numpy(h_in).cuda()
+        d_aad = torch.from_numpy(h_aad).cuda()
+        d_out = torch.zeros(hb.out_total + 32, dtype=torch.uint8, device="cuda")
+        d_mask = torch.zeros(16 * len(recs), dtype=torch.uint8, device="cuda")
+        hb.batch.seal_supp(hb.keyset, hp, d_supp, d_in, d_aad, d_out, d_mask)
+        torch.cuda.synchronize()
+        out, mask = d_out.cpu().numpy(), d_mask.cpu().numpy()
+    else:  # host-resident: pinned buffers, host supp descriptors, 64 KiB slices
+        supp = np.zeros(len(rows), dtype=ptls_hip.SUPP_DTYPE)
+        for i, row in enumerate(rows):
+            supp[i] = row
+        p_out = torch.zeros(hb.out_total + 32, dtype=torch.uint8).pin_memory()
+        p_mask = torch.zeros(16 * len(recs), dtype=torch.uint8).pin_memory()
+        pipe = ptls_hip.Pipeline(engine, 64 << 10)
+        pipe.seal_supp(hb.keyset, hp, hb.recs, supp, torch.from_numpy(h_in).pin_memory(), torch.from_numpy(h_aad).pin_memory(),
+                       p_out, p_mask)
+        pipe.close()
+        out, mask = p_out.numpy(), p_mask.numpy()
     for j, (r, rec, (off, k, enabled)) in enumerate(zip(recs, hb.recs, expect)):
         sealed = out[rec["out_off"]: rec["out_off"] + rec["len"] + 16].tobytes()
         assert sealed == oracle.seal(*r), j
