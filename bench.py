@@ -442,6 +442,10 @@ def main():
             tr = json.load(f)
         result["roofline"]["traffic"] = tr.get("hbm_bytes_per_seal_launch")
         result["roofline"]["traffic_source"] = os.path.relpath(tfile, ROOT)
+    lfile = os.path.join(ROOT, "profiles", f"lds_{args.config}.json")
+    if os.path.exists(lfile):  # LDS-array occupancy of the same kernel from its PMC pass (the bound that binds)
+        with open(lfile) as f:
+            result["roofline"]["lds_issue_ceiling"]["lds_array_busy_measured"] = json.load(f)["lds_array_busy_frac"]
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(args.config, cfg)
     if rank == 0:

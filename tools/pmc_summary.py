@@ -23,3 +23,13 @@ if "SQ_WAVE_CYCLES" in avg and "SQ_BUSY_CYCLES" in avg:
     print("--- shares of wave-cycles: wait_any %.3f wait_inst_any %.3f active_any %.3f valu %.3f lds %.3f" % (
         avg["SQ_WAIT_ANY"] / wc, avg["SQ_WAIT_INST_ANY"] / wc, avg["SQ_ACTIVE_INST_ANY"] / wc,
         avg["SQ_ACTIVE_INST_VALU"] / wc, avg["SQ_ACTIVE_INST_LDS"] / wc))
+
+# LDS-array occupancy of the seal launch (per CU), for bench.py's roofline block: --json <path>
+if "--json" in sys.argv and "SQ_LDS_IDX_ACTIVE" in avg and "GRBM_GUI_ACTIVE" in avg:
+    import json
+    busy = avg["SQ_LDS_IDX_ACTIVE"] / 256 / (avg["GRBM_GUI_ACTIVE"] / 8)
+    with open(sys.argv[sys.argv.index("--json") + 1], "w") as f:
+        json.dump({"lds_array_busy_frac": round(busy, 4), "lds_idx_active_cycles_per_cu": round(avg["SQ_LDS_IDX_ACTIVE"] / 256),
+                   "kernel_cycles_per_xcd": round(avg["GRBM_GUI_ACTIVE"] / 8),
+                   "source": "rocprofv3 --pmc SQ_LDS_IDX_ACTIVE / GRBM_GUI_ACTIVE, separate pass (tools/pmc_passes.sh), seal launch"},
+                  f, indent=1)
