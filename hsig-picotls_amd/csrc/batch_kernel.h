@@ -40,35 +40,10 @@ __host__ __device__ constexpr uint32_t lds_bytes(int log2g)
     return LDS_GTREE + (log2g > 3 ? log2g : 3) * LDS_TREE_STRIDE;
 }
 
-#ifndef PREFETCH_BARRIER
-#define PREFETCH_BARRIER 1
-#endif
-#ifndef CTR_SHORTCUT
-#define CTR_SHORTCUT 1
-#endif
-#ifndef REMAT_LANE
-#define REMAT_LANE 0
-#endif
-#if REMAT_LANE /* measured: no gain over keeping the constants (same-box A/B), default off */
-#define LANE_FRESH gh_lane_fresh()
-#else
-#define LANE_FRESH gl
-#endif
-#ifndef ABLATE_AES
-#define ABLATE_AES 0
-#endif
-#ifndef ABLATE_GHASH
-#define ABLATE_GHASH 0
-#endif
-#ifndef GHASH_HALF_BARRIER
-#define GHASH_HALF_BARRIER 0
-#endif
-#ifndef PHASED
-#define PHASED 1 /* round-phased full-block loop (ctr_ghash_phased); 0 = the compiler-scheduled one */
-#endif
-#if PHASED && !CTR_SHORTCUT
-#error "PHASED needs CTR_SHORTCUT"
-#endif
+/* Tuning switches (defaults are the measured best):
+ *   SKEWED       full-block loop with the lane's KP blocks 1/KP of a round apart (0: round-phased)
+ *   SETPRIO      wave priority while a wave issues a segment's lookups;  PFPRIO  ... and its prefetch loads
+ *   PURE_BLOCKS  KP, data blocks per lane per full-block iteration */
 #ifndef SETPRIO
 #define SETPRIO 1 /* wave priority while issuing a segment's lookups: c2 +6 % measured */
 #endif
@@ -188,45 +163,6 @@ __device__ __forceinline__ V4 aes_encrypt(const uint8_t *lds, uint32_t lb, const
     return V4{t0, t1, t2, t3};
 }
 
-/* two independent blocks, round-interleaved: twice the LDS requests in flight per wave */
-template <int ROUNDS>
-__device__ __forceinline__ void aes_encrypt2(const uint8_t *lds, uint32_t lb, const uint32_t *__restrict__ rk, V4 &s, V4 &u)
-{
-    s.w0 ^= rk[0];
-    s.w1 ^= rk[1];
-    s.w2 ^= rk[2];
-    s.w3 ^= rk[3];
-    u.w0 ^= rk[0];
-    u.w1 ^= rk[1];
-    u.w2 ^= rk[2];
-    u.w3 ^= rk[3];
-#pragma unroll
-    for (int r = 1; r < ROUNDS; ++r) {
-        const uint32_t k0 = rk[4 * r + 0], k1 = rk[4 * r + 1], k2 = rk[4 * r + 2], k3 = rk[4 * r + 3];
-        const uint32_t t0 = aes_col(lds, lb, s.w0, s.w1, s.w2, s.w3, k0);
-        const uint32_t v0 = aes_col(lds, lb, u.w0, u.w1, u.w2, u.w3, k0);
-        const uint32_t t1 = aes_col(lds, lb, s.w1, s.w2, s.w3, s.w0, k1);
-        const uint32_t v1 = aes_col(lds, lb, u.w1, u.w2, u.w3, u.w0, k1);
-        const uint32_t t2 = aes_col(lds, lb, s.w2, s.w3, s.w0, s.w1, k2);
-        const uint32_t v2 = aes_col(lds, lb, u.w2, u.w3, u.w0, u.w1, k2);
-        const uint32_t t3 = aes_col(lds, lb, s.w3, s.w0, s.w1, s.w2, k3);
-        const uint32_t v3 = aes_col(lds, lb, u.w3, u.w0, u.w1, u.w2, k3);
-        s = V4{t0, t1, t2, t3};
-        u = V4{v0, v1, v2, v3};
-    }
-    const uint32_t k0 = rk[4 * ROUNDS + 0], k1 = rk[4 * ROUNDS + 1], k2 = rk[4 * ROUNDS + 2], k3 = rk[4 * ROUNDS + 3];
-    const uint32_t t0 = aes_col_last(lds, lb, s.w0, s.w1, s.w2, s.w3, k0);
-    const uint32_t v0 = aes_col_last(lds, lb, u.w0, u.w1, u.w2, u.w3, k0);
-    const uint32_t t1 = aes_col_last(lds, lb, s.w1, s.w2, s.w3, s.w0, k1);
-    const uint32_t v1 = aes_col_last(lds, lb, u.w1, u.w2, u.w3, u.w0, k1);
-    const uint32_t t2 = aes_col_last(lds, lb, s.w2, s.w3, s.w0, s.w1, k2);
-    const uint32_t v2 = aes_col_last(lds, lb, u.w2, u.w3, u.w0, u.w1, k2);
-    const uint32_t t3 = aes_col_last(lds, lb, s.w3, s.w0, s.w1, s.w2, k3);
-    const uint32_t v3 = aes_col_last(lds, lb, u.w3, u.w0, u.w1, u.w2, k3);
-    s = V4{t0, t1, t2, t3};
-    u = V4{v0, v1, v2, v3};
-}
-
 /* single table lookups: T0, T1 = rotl8(T0), T2 = rotl16(T0), T3 = rotl8(T2), byte K of x */
 template <int K>
 __device__ __forceinline__ uint32_t lT0(const uint8_t *lds, uint32_t x, uint32_t lb)
@@ -312,7 +248,7 @@ __device__ __forceinline__ void aes_ctr_n(const uint8_t *lds, uint32_t lb, const
         s[b] = t[b];
 }
 
-/* ---------------- phased full-block iteration (PHASED=1) ----------------
+/* ---------------- round-phased full-block iteration ----------------
  * The compiler, left alone, consumes each T-table lookup a few instructions after issuing it
  * (lgkmcnt(0..4) waits), so a wave keeps only a handful of LDS reads in flight and the LDS array idles
  * while the 12 waves of a CU wait on latency.  Here every AES round is one "phase": all lookups of the
@@ -636,17 +572,6 @@ __device__ __forceinline__ GhLane gh_lane_init(int lane)
     return gh_lane_from((uint32_t)lane);
 }
 
-/* Lane id through an opaque asm statement: the compiler can neither hoist nor keep the derived lane
- * constants alive across the hot loop, so they are rematerialised (a few VALU) instead of being
- * spilled to scratch, whose reload waits would also drain this wave's in-flight stores (vmcnt is
- * in-order). */
-__device__ __forceinline__ GhLane gh_lane_fresh()
-{
-    uint32_t lane;
-    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lane));
-    return gh_lane_from(lane);
-}
-
 template <int K>
 __device__ __forceinline__ V4 gh_term(const uint8_t *lds, uint32_t xw, uint32_t lbw)
 {
@@ -669,9 +594,6 @@ __device__ __forceinline__ V4 gh_mul_main(const uint8_t *lds, const GhLane &g, V
     acc = v4xor3(acc, gh_term<2>(lds, x0, g.lb0), gh_term<3>(lds, x0, g.lb0));
     acc = v4xor3(acc, gh_term<4>(lds, x1, g.lb1), gh_term<5>(lds, x1, g.lb1));
     acc = v4xor3(acc, gh_term<6>(lds, x1, g.lb1), gh_term<7>(lds, x1, g.lb1));
-#if GHASH_HALF_BARRIER
-    __builtin_amdgcn_sched_barrier(0);
-#endif
     acc = v4xor3(acc, gh_term<8>(lds, x2, g.lb2), gh_term<9>(lds, x2, g.lb2));
     acc = v4xor3(acc, gh_term<10>(lds, x2, g.lb2), gh_term<11>(lds, x2, g.lb2));
     acc = v4xor3(acc, gh_term<12>(lds, x3, g.lb3), gh_term<13>(lds, x3, g.lb3));
@@ -1095,53 +1017,19 @@ __global__ void __launch_bounds__(WGT)
                         cw[b] = bswap32(cbase + (uint32_t)((it * KP + b) * G));
                         k[b] = V4{n0, n1, n2, cw[b]};
                     }
-#if PREFETCH_BARRIER
                     __builtin_amdgcn_sched_barrier(0); /* keep the prefetch at the top of the iteration */
-#endif
-#if PHASED
                     if (OPEN) {
+                        /* the input is the ciphertext: hash it in the same iteration */
                         ctr_ghash<ROUNDS, KP, true>(lds, lb_aes, rk, cc, cw, k, y, d, gl);
 #pragma unroll
                         for (int b = 0; b < KP; ++b)
                             store_full(dst + o + 16 * b * G, v4xor(d[b], k[b]));
                     } else {
+                        /* software pipelined: the ciphertext of iteration it is hashed during iteration it + 1 */
                         if (hash_pending)
                             ctr_ghash<ROUNDS, KP, true>(lds, lb_aes, rk, cc, cw, k, y, pend, gl);
                         else
                             ctr_ghash<ROUNDS, KP, false>(lds, lb_aes, rk, cc, cw, k, y, pend, gl);
-#pragma unroll
-                        for (int b = 0; b < KP; ++b) {
-                            pend[b] = v4xor(d[b], k[b]);
-                            store_full(dst + o + 16 * b * G, pend[b]);
-                        }
-                    }
-                    return;
-#endif
-#if ABLATE_AES /* timing-only diagnostic build: keystream = counter block */
-#elif CTR_SHORTCUT
-                    aes_ctr_n<ROUNDS, KP>(lds, lb_aes, rk, cc, cw, k);
-#else
-                    aes_encrypt_n<ROUNDS, KP>(lds, lb_aes, rk, k);
-#endif
-                    if (OPEN) {
-                        /* the input is the ciphertext: hash it in the same iteration */
-#pragma unroll
-                        for (int b = 0; b < KP; ++b)
-                            y = gh_mul_main(lds, LANE_FRESH, y, d[b]);
-#pragma unroll
-                        for (int b = 0; b < KP; ++b)
-                            store_full(dst + o + 16 * b * G, v4xor(d[b], k[b]));
-                    } else {
-                        /* software pipelined: the ciphertext of iteration it is hashed during iteration it + 1 */
-                        if (hash_pending) {
-#pragma unroll
-                            for (int b = 0; b < KP; ++b)
-#if ABLATE_GHASH /* timing-only diagnostic build */
-                                y = v4xor(y, pend[b]);
-#else
-                                y = gh_mul_main(lds, LANE_FRESH, y, pend[b]);
-#endif
-                        }
 #pragma unroll
                         for (int b = 0; b < KP; ++b) {
                             pend[b] = v4xor(d[b], k[b]);
