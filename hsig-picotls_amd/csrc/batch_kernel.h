@@ -850,7 +850,7 @@ __device__ __forceinline__ V4 finish_elem(const Elem &e, V4 in_blk, V4 ks, const
  * scalar unit (s_load into SGPRs) instead of per-lane vector loads.  in/out may alias (in place). */
 template <int G, int ROUNDS, bool OPEN, bool ALIGNED, int WGT>
 __global__ void __launch_bounds__(WGT)
-    aesgcm_batch_kernel(const ptls_hip_record_t *__restrict__ recs, const uint32_t *__restrict__ order,
+    aesgcm_batch_kernel(const ptls_hip_record_t *__restrict__ recs_ord, const uint32_t *__restrict__ order,
                         const Chunk *__restrict__ chunks, uint32_t nchunks,
                         const uint8_t *in, const uint8_t *__restrict__ aad, uint8_t *out, uint64_t *__restrict__ result,
                         const KeySlot *__restrict__ slots, const uint32_t *__restrict__ basis, const uint32_t *__restrict__ t0,
@@ -891,8 +891,11 @@ __global__ void __launch_bounds__(WGT)
                 break;
             const uint32_t ridx = (uint32_t)t * R + grp;
             const bool valid = ridx < ch.count;
-            const uint32_t rec_i = order[ch.first + (valid ? ridx : 0)];
-            const ptls_hip_record_t rec = recs[rec_i];
+            /* descriptors in chunk order: the record is one load away (its caller index only matters for
+             * result[] and supp[] at the end) */
+            const uint32_t pos = ch.first + (valid ? ridx : 0);
+            const ptls_hip_record_t rec = recs_ord[pos];
+            const uint32_t rec_i = order[pos];
             const int L = valid ? (int)rec.len : 0;
             const int A = valid ? (int)rec.aad_len : 0;
             const int na = (A + 15) >> 4, nc = (L + 15) >> 4;
@@ -1113,10 +1116,10 @@ template <int G, int R, bool O, int W>
 static hipError_t launch_one(unsigned grid, hipStream_t s, const KernelArgs &a, bool aligned)
 {
     if (aligned)
-        hipLaunchKernelGGL((aesgcm_batch_kernel<G, R, O, true, W>), dim3(grid), dim3(W), 0, s, a.recs, a.order, a.chunks,
+        hipLaunchKernelGGL((aesgcm_batch_kernel<G, R, O, true, W>), dim3(grid), dim3(W), 0, s, a.recs_ord, a.order, a.chunks,
                            a.nchunks, a.in, a.aad, a.out, a.result, a.slots, a.basis, a.t0, a.supp, a.hp_slots, a.mask);
     else
-        hipLaunchKernelGGL((aesgcm_batch_kernel<G, R, O, false, W>), dim3(grid), dim3(W), 0, s, a.recs, a.order, a.chunks,
+        hipLaunchKernelGGL((aesgcm_batch_kernel<G, R, O, false, W>), dim3(grid), dim3(W), 0, s, a.recs_ord, a.order, a.chunks,
                            a.nchunks, a.in, a.aad, a.out, a.result, a.slots, a.basis, a.t0, a.supp, a.hp_slots, a.mask);
     return hipGetLastError();
 }

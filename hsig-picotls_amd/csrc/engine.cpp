@@ -114,6 +114,7 @@ struct st_ptls_hip_batch_t {
     ptls_hip_engine_t *eng;
     size_t n;
     ptls_hip_record_t *d_recs;
+    ptls_hip_record_t *d_recs_ord; /* descriptors in chunk order (the batch kernel's view) */
     std::vector<ptls_hip_record_t> h_recs;
     Chunk *d_chunks;
     uint32_t *d_order;
@@ -452,8 +453,11 @@ static int plan_chunks(ptls_hip_batch_t *b)
         (void)hipFree(b->d_chunks);
     if (b->d_order != nullptr)
         (void)hipFree(b->d_order);
+    if (b->d_recs_ord != nullptr)
+        (void)hipFree(b->d_recs_ord);
     b->d_chunks = nullptr;
     b->d_order = nullptr;
+    b->d_recs_ord = nullptr;
     b->nchunks = (uint32_t)ch.size();
     if (ch.empty())
         return 0;
@@ -461,6 +465,11 @@ static int plan_chunks(ptls_hip_batch_t *b)
     HIP_TRY(hipMemcpy(b->d_chunks, ch.data(), ch.size() * sizeof(Chunk), hipMemcpyHostToDevice), PTLS_HIP_ENODEV);
     HIP_TRY(hipMalloc(&b->d_order, order.size() * sizeof(uint32_t)), PTLS_HIP_ENOMEM);
     HIP_TRY(hipMemcpy(b->d_order, order.data(), order.size() * sizeof(uint32_t), hipMemcpyHostToDevice), PTLS_HIP_ENODEV);
+    std::vector<ptls_hip_record_t> ord(order.size());
+    for (size_t k = 0; k < order.size(); ++k)
+        ord[k] = b->h_recs[order[k]];
+    HIP_TRY(hipMalloc(&b->d_recs_ord, ord.size() * sizeof(ptls_hip_record_t)), PTLS_HIP_ENOMEM);
+    HIP_TRY(hipMemcpy(b->d_recs_ord, ord.data(), ord.size() * sizeof(ptls_hip_record_t), hipMemcpyHostToDevice), PTLS_HIP_ENODEV);
     return 0;
 }
 
@@ -499,6 +508,7 @@ extern "C" void ptls_hip_batch_free(ptls_hip_batch_t *b)
         return;
     DeviceGuard g(b->eng->device);
     (void)hipFree(b->d_recs);
+    (void)hipFree(b->d_recs_ord);
     (void)hipFree(b->d_chunks);
     (void)hipFree(b->d_order);
     delete b;
@@ -556,6 +566,7 @@ static int run_batch(ptls_hip_batch_t *b, ptls_hip_keyset_t *ks, const void *in,
     DeviceGuard g(b->eng->device);
     KernelArgs a{};
     a.recs = b->d_recs;
+    a.recs_ord = b->d_recs_ord;
     a.order = b->d_order;
     a.chunks = b->d_chunks;
     a.nchunks = b->nchunks;
@@ -752,13 +763,13 @@ struct PipeSlot {
     hipStream_t stream;
     hipEvent_t done;
     uint8_t *d_in, *d_out, *d_aad, *d_mask;
-    ptls_hip_record_t *d_recs;
+    ptls_hip_record_t *d_recs, *d_recs_ord;
     Chunk *d_chunks;
     uint32_t *d_order;
     uint64_t *d_result;
     ptls_hip_supp_t *d_supp;
     /* pinned host staging for the slice's descriptors / chunks / record order / header-protection descriptors */
-    ptls_hip_record_t *h_recs;
+    ptls_hip_record_t *h_recs, *h_recs_ord;
     Chunk *h_chunks;
     uint32_t *h_order;
     ptls_hip_supp_t *h_supp;
@@ -791,6 +802,8 @@ extern "C" ptls_hip_pipeline_t *ptls_hip_pipeline_new(ptls_hip_engine_t *eng, si
              hipMalloc(&s.d_supp, p->max_recs * sizeof(ptls_hip_supp_t)) == hipSuccess &&
              hipHostMalloc(&s.h_supp, p->max_recs * sizeof(ptls_hip_supp_t), hipHostMallocDefault) == hipSuccess &&
              hipMalloc(&s.d_recs, p->max_recs * sizeof(ptls_hip_record_t)) == hipSuccess &&
+             hipMalloc(&s.d_recs_ord, p->max_recs * sizeof(ptls_hip_record_t)) == hipSuccess &&
+             hipHostMalloc(&s.h_recs_ord, p->max_recs * sizeof(ptls_hip_record_t), hipHostMallocDefault) == hipSuccess &&
              hipMalloc(&s.d_chunks, p->max_recs * sizeof(Chunk)) == hipSuccess &&
              hipMalloc(&s.d_order, p->max_recs * sizeof(uint32_t)) == hipSuccess &&
              hipHostMalloc(&s.h_order, p->max_recs * sizeof(uint32_t), hipHostMallocDefault) == hipSuccess &&
@@ -822,6 +835,8 @@ extern "C" void ptls_hip_pipeline_free(ptls_hip_pipeline_t *p)
         (void)hipFree(s.d_supp);
         (void)hipHostFree(s.h_supp);
         (void)hipFree(s.d_recs);
+        (void)hipFree(s.d_recs_ord);
+        (void)hipHostFree(s.h_recs_ord);
         (void)hipFree(s.d_chunks);
         (void)hipFree(s.d_order);
         (void)hipHostFree(s.h_order);
@@ -964,6 +979,10 @@ static int pipeline_run(ptls_hip_pipeline_t *p, ptls_hip_keyset_t *ks, const ptl
         }
         std::memcpy(s.h_chunks, ch.data(), ch.size() * sizeof(Chunk));
         std::memcpy(s.h_order, order.data(), cnt * sizeof(uint32_t));
+        for (size_t t = 0; t < cnt; ++t)
+            s.h_recs_ord[t] = s.h_recs[order[t]];
+        HIP_TRY(hipMemcpyAsync(s.d_recs_ord, s.h_recs_ord, cnt * sizeof(ptls_hip_record_t), hipMemcpyHostToDevice, s.stream),
+                PTLS_HIP_ENODEV);
         HIP_TRY(hipMemcpyAsync(s.d_order, s.h_order, cnt * sizeof(uint32_t), hipMemcpyHostToDevice, s.stream), PTLS_HIP_ENODEV);
         HIP_TRY(hipMemcpyAsync(s.d_recs, s.h_recs, cnt * sizeof(ptls_hip_record_t), hipMemcpyHostToDevice, s.stream),
                 PTLS_HIP_ENODEV);
@@ -981,6 +1000,7 @@ static int pipeline_run(ptls_hip_pipeline_t *p, ptls_hip_keyset_t *ks, const ptl
         }
         KernelArgs a{};
         a.recs = s.d_recs;
+        a.recs_ord = s.d_recs_ord;
         a.order = s.d_order;
         a.chunks = s.d_chunks;
         a.nchunks = (uint32_t)ch.size();
@@ -1320,6 +1340,7 @@ static uint64_t plugin_run(hip_aead_state *st, bool open, void *output, const vo
         plugin_check(hipMemcpyAsync(d_aad, aad, aadlen, hipMemcpyHostToDevice, st->stream), "upload(aad)");
     KernelArgs a{};
     a.recs = st->d_rec;
+    a.recs_ord = st->d_rec; /* one record: chunk order is the caller's */
     a.order = st->d_order;
     a.chunks = st->d_chunk;
     a.nchunks = 1;

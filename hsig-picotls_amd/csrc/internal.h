@@ -45,6 +45,7 @@ struct Chunk {
 
 struct KernelArgs {
     const ptls_hip_record_t *recs;
+    const ptls_hip_record_t *recs_ord; /* the same descriptors in chunk order: one dependent load per task */
     const uint32_t *order;  /* chunk positions -> record index (records of a chunk sorted by length) */
     const Chunk *chunks;
     uint32_t nchunks;
