@@ -50,6 +50,9 @@ __host__ __device__ constexpr uint32_t lds_bytes(int log2g)
 #ifndef PFPRIO
 #define PFPRIO 0 /* priority for the prefetch loads too: measured no gain */
 #endif
+#ifndef GEN_SKEWED
+#define GEN_SKEWED 1 /* generic elements through ctr_ghash (counter-mode shortcut, skewed, prioritised): c3 +2 %, c4 +4 % */
+#endif
 #ifndef SKEWED
 #define SKEWED 1 /* ctr_ghash_skewed (the lane's KP blocks 1/KP of a round apart) */
 #endif
@@ -943,7 +946,15 @@ __global__ void __launch_bounds__(WGT)
                 if (wave_max(big))
                     aes_encrypt_n<ROUNDS, 2>(lds, lb_aes, rk, ks);
                 else
+#if GEN_SKEWED
+                {
+                    const V4 nohash[2] = {V4{0, 0, 0, 0}, V4{0, 0, 0, 0}};
+                    V4 ydummy = V4{0, 0, 0, 0};
+                    ctr_ghash<ROUNDS, 2, false>(lds, lb_aes, rk, cc, cw, ks, ydummy, nohash, gl);
+                }
+#else
                     aes_ctr_n<ROUNDS, 2>(lds, lb_aes, rk, cc, cw, ks);
+#endif
 #pragma unroll
                 for (int b = 0; b < 2; ++b) {
                     const V4 x = finish_elem<OPEN, ALIGNED>(e[b], in[b], ks[b], aad_p, A, L, out_p, ek0);
@@ -962,8 +973,16 @@ __global__ void __launch_bounds__(WGT)
                         in0 = put_byte(in0, e0.nbytes - 1, ttype);
                 }
                 /* keystream for data block c (counter inc32(J0) + c), E_K(J0) for the length-block lane */
-                V4 ks0[1] = {V4{n0, n1, n2, e0.is_c ? bswap32((uint32_t)e0.c + 2u) : 0x01000000u}};
-                aes_encrypt_n<ROUNDS, 1>(lds, lb_aes, rk, ks0);
+                const uint32_t cw0[1] = {e0.is_c ? bswap32((uint32_t)e0.c + 2u) : 0x01000000u};
+                V4 ks0[1] = {V4{n0, n1, n2, cw0[0]}};
+#if GEN_SKEWED
+                if (!wave_max((e0.is_c && e0.c >= 65534) ? 1 : 0)) {
+                    const V4 nohash[1] = {V4{0, 0, 0, 0}};
+                    V4 ydummy = V4{0, 0, 0, 0};
+                    ctr_ghash<ROUNDS, 1, false>(lds, lb_aes, rk, cc, cw0, ks0, ydummy, nohash, gl);
+                } else
+#endif
+                    aes_encrypt_n<ROUNDS, 1>(lds, lb_aes, rk, ks0);
                 const V4 x0 = finish_elem<OPEN, ALIGNED>(e0, in0, ks0[0], aad_p, A, L, out_p, ek0);
                 if (e0.active)
                     y = gh_mul_main(lds, gl, y, x0);
