@@ -1,0 +1,12 @@
+#!/bin/bash
+# Copy the summaries written by tools/refresh_profiles.sh from gpurun_out/ into profiles/ (committed).
+set -e
+cd "$(dirname "$0")/.."
+tag=${1:-r01}
+for c in c2 c3 c4; do
+  cp gpurun_out/prof_${tag}_$c/trace/run_kernel_stats.csv profiles/${tag}_${c}_kernel_stats.csv
+  cp gpurun_out/prof_${tag}_$c/traffic_$c.json profiles/traffic_$c.json
+  cp gpurun_out/pmc_$c/lds_$c.json profiles/lds_$c.json
+  cp gpurun_out/pmc_$c/summary.txt profiles/${tag}_${c}_pmc_sq_summary.txt
+  grep '"metric"' gpurun_out/bench_${c}_full.log > profiles/${tag}_bench_${c}_latest.log
+done
