@@ -215,6 +215,29 @@ def test_differential_random(engine, oracle):
         hb.close()
 
 
+@pytest.mark.parametrize("lanes", [0, 2, 16])
+@pytest.mark.parametrize("key_len", [16, 32])
+def test_large_records_counter_past_16_bits(engine, oracle, key_len, lanes):
+    """records past 2^16 blocks (1 MiB): the counter-mode shortcut holds only while the 32-bit block
+    counter stays below 2^16, so the full-block stretch stops at block 65533 and the rest of the record
+    takes the full-AES path (inc32 stays exact: fusion's 64-bit lane increment equals it for any record
+    under 64 GiB, lib/fusion.c:406-418).  Lengths straddle the boundary; seal == oracle, open round trips."""
+    rng = np.random.default_rng(key_len + lanes)
+    lens = [65533 * 16 - 3, 65534 * 16, 65535 * 16 + 7, (1 << 21) + 3]
+    recs = []
+    for i, L in enumerate(lens):
+        key, iv = oracle.gen_key(50 + i, key_len)
+        recs.append((key, iv, 1000 + i, rng.integers(0, 256, 13, dtype=np.uint8).tobytes(),
+                     rng.integers(0, 256, L, dtype=np.uint8).tobytes()))
+    hb = HostBatch(engine, recs)
+    outs = hb.seal(lanes)
+    for r, o in zip(recs, outs):
+        assert o == oracle.seal(*r), len(r[4])
+    res, pts = hb.open(outs, lanes)
+    assert res == lens and pts == [r[4] for r in recs]
+    hb.close()
+
+
 def test_full_size_roundtrip_16k(engine, oracle):
     """64K x 16 KiB (1 GiB) synthetic records filled on the GPU: seal -> open must return every
     record with its length and the original bytes (size-independent property), and sampled records
