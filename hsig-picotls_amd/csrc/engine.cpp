@@ -146,6 +146,19 @@ class DeviceGuard {
     int prev_ = 0, dev_ = 0;
 };
 
+extern "C" int ptls_hip_is_supported(void)
+{
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess)
+        return 0;
+    for (int d = 0; d < ndev; ++d) {
+        hipDeviceProp_t prop;
+        if (hipGetDeviceProperties(&prop, d) == hipSuccess && std::strncmp(prop.gcnArchName, "gfx950", 6) == 0)
+            return 1;
+    }
+    return 0;
+}
+
 extern "C" ptls_hip_engine_t *ptls_hip_engine_new(int device)
 {
     int ndev = 0;

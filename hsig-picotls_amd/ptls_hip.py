@@ -67,6 +67,7 @@ SIGNATURES = {
                                   ctypes.POINTER(_sz)]),
     "ptls_hip_tls13_open_batch": (_i, [_vp, _vp, _vp, _vp, _vp, _vp]),
     "ptls_hip_pipeline_new": (_vp, [_vp, _sz]),
+    "ptls_hip_is_supported": (_i, []),
     "ptls_hip_pipeline_free": (None, [_vp]),
     "ptls_hip_pipeline_seal": (_i, [_vp, _vp, _vp, _sz, _vp, _vp, _vp]),
     "ptls_hip_pipeline_open": (_i, [_vp, _vp, _vp, _sz, _vp, _vp, _vp, _vp]),
@@ -258,6 +259,11 @@ class Batch:
         if self.ptr:
             lib().ptls_hip_batch_free(self.ptr)
             self.ptr = None
+
+
+def is_supported():
+    """True when a gfx950 device is visible (ptls_hip_is_supported, ~ ptls_fusion_is_supported_by_cpu)"""
+    return bool(lib().ptls_hip_is_supported())
 
 
 class Pipeline:

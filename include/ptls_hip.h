@@ -60,6 +60,11 @@ extern ptls_cipher_algorithm_t ptls_hip_aes128ctr, ptls_hip_aes256ctr;
  * the environment variable PTLS_HIP_DEVICE).  Must be called before the first context is made. */
 int ptls_hip_set_default_device(int device);
 
+/* 1 when a gfx950 (MI355X) device is visible to this process, else 0: the counterpart of
+ * ptls_fusion_is_supported_by_cpu (lib/fusion.c:2219-2249), for choosing the cipher suites at start-up.
+ * Counts devices without creating a context. */
+int ptls_hip_is_supported(void);
+
 /* ------------------------------------------------------------------------------------------ *
  * 2. batch extension                                                                          *
  * ------------------------------------------------------------------------------------------ */

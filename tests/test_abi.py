@@ -113,6 +113,7 @@ def test_fails_loudly_without_device():
     """no CPU fallback: engine construction errors out, and picotls's own ptls_aead_new_direct returns NULL
     for our algorithm (setup_crypto != 0, lib/picotls.c:6467-6470)"""
     L = ptls_hip.lib()
+    assert not ptls_hip.is_supported()  # ptls_fusion_is_supported_by_cpu's counterpart says no
     assert not L.ptls_hip_engine_new(0)
     assert "device" in ptls_hip.last_error().lower()
     with pytest.raises(ptls_hip.HipError):

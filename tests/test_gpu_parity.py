@@ -64,6 +64,11 @@ def test_gcm_test_vectors(engine, golden, lanes):
     hb.close()
 
 
+def test_is_supported_on_mi355x(engine):
+    """ptls_hip_is_supported (ptls_fusion_is_supported_by_cpu's counterpart) reports the gfx950 device"""
+    assert ptls_hip.is_supported()
+
+
 def test_tamper_returns_size_max_and_writes_plaintext(engine, golden):
     """aead_do_decrypt returns SIZE_MAX on a bad tag (lib/fusion.c:1162-1164) but the plaintext has
     already been written (decrypt-then-verify, :822-840); t/picotls.c test_ciphersuite flips a bit."""
