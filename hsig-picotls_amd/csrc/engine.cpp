@@ -1320,7 +1320,7 @@ static const size_t ST_REC = 0, ST_CHUNK = 64, ST_ORDER = 96, ST_RESULT = 128, S
 
 /* run one record through the batch kernel: in/out/aad are host buffers */
 static uint64_t plugin_run(hip_aead_state *st, bool open, void *output, const void *input, size_t len, uint64_t seq,
-                           const void *aad, size_t aadlen, const PluginSupp *ps = nullptr)
+                           const void *aad, size_t aadlen, const PluginSupp *ps = nullptr, const void *tag = nullptr)
 {
     DeviceGuard g(st->eng->device);
     const size_t in_len = open ? len + 16 : len;
@@ -1347,8 +1347,13 @@ static uint64_t plugin_run(hip_aead_state *st, bool open, void *output, const vo
     std::memcpy(st->h_stage + ST_ORDER, &order0, sizeof(order0));
     std::memcpy(st->h_stage + ST_SUPP, &sp, sizeof(sp));
     plugin_check(hipMemcpyAsync(st->d_rec, st->h_stage, ST_SUPP + sizeof(sp), hipMemcpyHostToDevice, st->stream), "upload(rec)");
-    if (in_len != 0)
+    if (tag != nullptr) { /* open with a detached tag (ptls_fusion_aesgcm_decrypt, lib/fusion.c:660-661) */
+        if (len != 0)
+            plugin_check(hipMemcpyAsync(d_in, input, len, hipMemcpyHostToDevice, st->stream), "upload(in)");
+        plugin_check(hipMemcpyAsync(d_in + len, tag, 16, hipMemcpyHostToDevice, st->stream), "upload(tag)");
+    } else if (in_len != 0) {
         plugin_check(hipMemcpyAsync(d_in, input, in_len, hipMemcpyHostToDevice, st->stream), "upload(in)");
+    }
     if (aadlen != 0)
         plugin_check(hipMemcpyAsync(d_aad, aad, aadlen, hipMemcpyHostToDevice, st->stream), "upload(aad)");
     KernelArgs a{};
@@ -1397,12 +1402,8 @@ static uint64_t plugin_run(hip_aead_state *st, bool open, void *output, const vo
     return result;
 }
 
-static void aead_dispose(ptls_aead_context_t *_ctx)
+static void state_free(hip_aead_state *st)
 {
-    auto *ctx = reinterpret_cast<hip_aead_context *>(_ctx);
-    hip_aead_state *st = ctx->st;
-    if (st == nullptr)
-        return;
     {
         DeviceGuard g(st->eng->device);
         ptls_hip_keyset_free(st->ks);
@@ -1417,6 +1418,14 @@ static void aead_dispose(ptls_aead_context_t *_ctx)
     }
     std::memset(st->iv, 0, sizeof(st->iv));
     delete st;
+}
+
+static void aead_dispose(ptls_aead_context_t *_ctx)
+{
+    auto *ctx = reinterpret_cast<hip_aead_context *>(_ctx);
+    if (ctx->st == nullptr)
+        return;
+    state_free(ctx->st);
     ctx->st = nullptr;
 }
 
@@ -1450,10 +1459,9 @@ static size_t aead_encrypt_final(ptls_aead_context_t *, void *)
     abort();
 }
 
-static void aead_encrypt(ptls_aead_context_t *_ctx, void *output, const void *input, size_t inlen, uint64_t seq, const void *aad,
+static void encrypt_supp(hip_aead_state *st, void *output, const void *input, size_t inlen, uint64_t seq, const void *aad,
                          size_t aadlen, ptls_aead_supplementary_encryption_t *supp)
 {
-    hip_aead_state *st = reinterpret_cast<hip_aead_context *>(_ctx)->st;
     if (supp != nullptr) {
         /* fused (lib/fusion.c:424-428, :636-650): our CTR context, same key size, sample inside the output */
         const hip_ctr_state *cs = ctr_state_of(supp->ctx);
@@ -1472,6 +1480,12 @@ static void aead_encrypt(ptls_aead_context_t *_ctx, void *output, const void *in
         std::memset(supp->output, 0, sizeof(supp->output));
         supp->ctx->do_transform(supp->ctx, supp->output, supp->output, sizeof(supp->output));
     }
+}
+
+static void aead_encrypt(ptls_aead_context_t *_ctx, void *output, const void *input, size_t inlen, uint64_t seq, const void *aad,
+                         size_t aadlen, ptls_aead_supplementary_encryption_t *supp)
+{
+    encrypt_supp(reinterpret_cast<hip_aead_context *>(_ctx)->st, output, input, inlen, seq, aad, aadlen, supp);
 }
 
 static void aead_encrypt_v(ptls_aead_context_t *_ctx, void *output, ptls_iovec_t *input, size_t incnt, uint64_t seq,
@@ -1499,26 +1513,19 @@ static size_t aead_decrypt(ptls_aead_context_t *_ctx, void *output, const void *
     return r == ~(uint64_t)0 ? SIZE_MAX : (size_t)r;
 }
 
-static int aesgcm_setup(ptls_aead_context_t *_ctx, int is_enc, const void *key, const void *iv, size_t key_size)
+/* one single-record AEAD state on the plugin engine's device (shared by the plugin contexts and the
+ * fusion-style low-level API) */
+static hip_aead_state *state_new(const void *key, const void *iv, size_t key_size)
 {
-    (void)is_enc; /* one context seals and opens, as fusion's (lib/fusion.c:1184-1206) */
-    auto *ctx = reinterpret_cast<hip_aead_context *>(_ctx);
-    if (key == nullptr) { /* IV-only re-setup (lib/fusion.c:1190-1191) */
-        if (ctx->st == nullptr)
-            return -1;
-        aead_set_iv(_ctx, iv);
-        return 0;
-    }
-    ctx->st = nullptr;
     ptls_hip_engine_t *eng = plugin_engine();
     if (eng == nullptr)
-        return -1;
+        return nullptr;
     DeviceGuard g(eng->device);
     auto *st = new hip_aead_state();
     st->eng = eng;
     if (hipStreamCreateWithFlags(&st->stream, hipStreamNonBlocking) != hipSuccess) {
         delete st;
-        return -1;
+        return nullptr;
     }
     st->ks = ptls_hip_keyset_new(eng, key_size, 1);
     bool ok = st->ks != nullptr && hipMalloc(&st->d_rec, 256) == hipSuccess &&
@@ -1531,14 +1538,29 @@ static int aesgcm_setup(ptls_aead_context_t *_ctx, int is_enc, const void *key, 
         (void)hipHostFree(st->h_stage);
         (void)hipStreamDestroy(st->stream);
         delete st;
-        return -1;
+        return nullptr;
     }
     st->d_chunk = reinterpret_cast<Chunk *>(reinterpret_cast<uint8_t *>(st->d_rec) + ST_CHUNK);
     st->d_order = reinterpret_cast<uint32_t *>(reinterpret_cast<uint8_t *>(st->d_rec) + ST_ORDER);
     st->d_result = reinterpret_cast<uint64_t *>(reinterpret_cast<uint8_t *>(st->d_rec) + ST_RESULT);
     std::memcpy(st->iv, iv, 12);
     st->iv_dirty = false;
-    ctx->st = st;
+    return st;
+}
+
+static int aesgcm_setup(ptls_aead_context_t *_ctx, int is_enc, const void *key, const void *iv, size_t key_size)
+{
+    (void)is_enc; /* one context seals and opens, as fusion's (lib/fusion.c:1184-1206) */
+    auto *ctx = reinterpret_cast<hip_aead_context *>(_ctx);
+    if (key == nullptr) { /* IV-only re-setup (lib/fusion.c:1190-1191) */
+        if (ctx->st == nullptr)
+            return -1;
+        aead_set_iv(_ctx, iv);
+        return 0;
+    }
+    ctx->st = state_new(key, iv, key_size);
+    if (ctx->st == nullptr)
+        return -1;
     ctx->super.dispose_crypto = aead_dispose;
     ctx->super.do_get_iv = aead_get_iv;
     ctx->super.do_set_iv = aead_set_iv;
@@ -1593,4 +1615,63 @@ ptls_aead_algorithm_t ptls_hip_aes256gcm = {"AES256-GCM",
                                             0,
                                             sizeof(hip_aead_context),
                                             aes256gcm_setup};
+}
+
+/* ---- fusion-style low-level single-record API (include/picotls/fusion.h:56-96, lib/fusion.c:400-1048) ----
+ * fusion passes the counter block as an x86 __m128i (calc_counter, lib/fusion.c:1126-1133: static IV xor
+ * seq); here the caller passes the 12-byte nonce it stands for, so the state's IV is the nonce and the
+ * record runs with seq 0 (nonce xor 0 == nonce). */
+struct ptls_hip_aesgcm_context {
+    hip_aead_state *st;
+};
+
+static void lowlevel_set_nonce(hip_aead_state *st, const void *nonce)
+{
+    if (std::memcmp(st->iv, nonce, 12) != 0) {
+        std::memcpy(st->iv, nonce, 12);
+        st->iv_dirty = true;
+    }
+}
+
+extern "C" ptls_hip_aesgcm_context_t *ptls_hip_aesgcm_new(const void *key, size_t key_size, size_t capacity)
+{
+    if (key == nullptr || (key_size != PTLS_AES128_KEY_SIZE && key_size != PTLS_AES256_KEY_SIZE))
+        return nullptr;
+    static const uint8_t zero_iv[12] = {0};
+    hip_aead_state *st = state_new(key, zero_iv, key_size);
+    if (st == nullptr)
+        return nullptr;
+    auto *ctx = new ptls_hip_aesgcm_context{st};
+    return ptls_hip_aesgcm_set_capacity(ctx, capacity);
+}
+
+extern "C" ptls_hip_aesgcm_context_t *ptls_hip_aesgcm_set_capacity(ptls_hip_aesgcm_context_t *ctx, size_t capacity)
+{
+    /* capacity = AAD + payload, as fusion's (lib/fusion.c:1017-1040); the staging also grows on demand */
+    DeviceGuard g(ctx->st->eng->device);
+    state_reserve(ctx->st, capacity + 16, 0);
+    return ctx;
+}
+
+extern "C" void ptls_hip_aesgcm_free(ptls_hip_aesgcm_context_t *ctx)
+{
+    if (ctx == nullptr)
+        return;
+    state_free(ctx->st);
+    delete ctx;
+}
+
+extern "C" void ptls_hip_aesgcm_encrypt(ptls_hip_aesgcm_context_t *ctx, void *output, const void *input, size_t inlen,
+                                        const void *nonce, const void *aad, size_t aadlen,
+                                        ptls_aead_supplementary_encryption_t *supp)
+{
+    lowlevel_set_nonce(ctx->st, nonce);
+    encrypt_supp(ctx->st, output, input, inlen, 0, aad, aadlen, supp);
+}
+
+extern "C" int ptls_hip_aesgcm_decrypt(ptls_hip_aesgcm_context_t *ctx, void *output, const void *input, size_t inlen,
+                                       const void *nonce, const void *aad, size_t aadlen, const void *tag)
+{
+    lowlevel_set_nonce(ctx->st, nonce);
+    return plugin_run(ctx->st, true, output, input, inlen, 0, aad, aadlen, nullptr, tag) != ~(uint64_t)0;
 }

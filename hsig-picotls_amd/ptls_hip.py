@@ -68,6 +68,11 @@ SIGNATURES = {
     "ptls_hip_tls13_open_batch": (_i, [_vp, _vp, _vp, _vp, _vp, _vp]),
     "ptls_hip_pipeline_new": (_vp, [_vp, _sz]),
     "ptls_hip_is_supported": (_i, []),
+    "ptls_hip_aesgcm_new": (_vp, [_vp, _sz, _sz]),
+    "ptls_hip_aesgcm_set_capacity": (_vp, [_vp, _sz]),
+    "ptls_hip_aesgcm_free": (None, [_vp]),
+    "ptls_hip_aesgcm_encrypt": (None, [_vp, _vp, _vp, _sz, _vp, _vp, _sz, _vp]),
+    "ptls_hip_aesgcm_decrypt": (_i, [_vp, _vp, _vp, _sz, _vp, _vp, _sz, _vp]),
     "ptls_hip_pipeline_free": (None, [_vp]),
     "ptls_hip_pipeline_seal": (_i, [_vp, _vp, _vp, _sz, _vp, _vp, _vp]),
     "ptls_hip_pipeline_open": (_i, [_vp, _vp, _vp, _sz, _vp, _vp, _vp, _vp]),
@@ -264,6 +269,44 @@ class Batch:
 def is_supported():
     """True when a gfx950 device is visible (ptls_hip_is_supported, ~ ptls_fusion_is_supported_by_cpu)"""
     return bool(lib().ptls_hip_is_supported())
+
+
+class AesGcm:
+    """fusion-style low-level single-record context (ptls_hip_aesgcm_*, ~ ptls_fusion_aesgcm_*,
+    include/picotls/fusion.h:56-96); `nonce` is the 12-byte GCM nonce fusion passes as its counter block"""
+
+    def __init__(self, key, capacity=0):
+        self.ptr = lib().ptls_hip_aesgcm_new(key, len(key), capacity)
+        if not self.ptr:
+            raise HipError(f"ptls_hip_aesgcm_new: {last_error()}")
+
+    def set_capacity(self, capacity):
+        self.ptr = lib().ptls_hip_aesgcm_set_capacity(self.ptr, capacity)
+
+    class Supp(ctypes.Structure):  # ptls_aead_supplementary_encryption_t, include/picotls.h:421-436
+        _fields_ = [("ctx", ctypes.c_void_p), ("input", ctypes.c_void_p), ("output", ctypes.c_uint8 * 16)]
+
+    def encrypt(self, data, nonce, aad, supp_cipher=None, sample_off=0):
+        """ciphertext || tag; with supp_cipher (a ptls_cipher_context_t address) also the supplementary
+        block AES-ECB(output[sample_off:sample_off+16]): returns (output, block)"""
+        out = ctypes.create_string_buffer(len(data) + 16)
+        supp = None
+        if supp_cipher is not None:
+            supp = self.Supp(supp_cipher, ctypes.addressof(out) + sample_off)
+        lib().ptls_hip_aesgcm_encrypt(self.ptr, out, data, len(data), nonce, aad, len(aad),
+                                      None if supp is None else ctypes.addressof(supp))
+        return out.raw if supp is None else (out.raw, bytes(supp.output))
+
+    def decrypt(self, data, nonce, aad, tag):
+        """(ok, plaintext): the plaintext is written whether or not the tag matches, as fusion's"""
+        out = ctypes.create_string_buffer(max(len(data), 1))
+        ok = lib().ptls_hip_aesgcm_decrypt(self.ptr, out, data, len(data), nonce, aad, len(aad), tag)
+        return bool(ok), out.raw[:len(data)]
+
+    def close(self):
+        if self.ptr:
+            lib().ptls_hip_aesgcm_free(self.ptr)
+            self.ptr = None
 
 
 class Pipeline:

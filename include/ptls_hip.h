@@ -65,6 +65,27 @@ int ptls_hip_set_default_device(int device);
  * Counts devices without creating a context. */
 int ptls_hip_is_supported(void);
 
+/* Fusion-style low-level single-record AES-GCM context (include/picotls/fusion.h:56-96,
+ * lib/fusion.c:400-1048), for callers that drive fusion below the AEAD plugin (as its benchmarks and
+ * tests do).  One record per call, host buffers, synchronous.
+ *   nonce   the 12-byte GCM nonce (static IV xor big-endian sequence number).  Fusion takes the
+ *           same value as a byte-swapped __m128i counter block (calc_counter, lib/fusion.c:1126-1133),
+ *           which is x86-only; the nonce bytes are the portable form of it.
+ *   capacity  maximum AAD + payload size, as fusion's; staging also grows on demand, and
+ *           set_capacity returns the same context.
+ * encrypt writes inlen bytes of ciphertext followed by the 16-byte tag.  supp (optional) is handled as
+ * by the AEAD plugin's do_encrypt.  decrypt reads inlen bytes of ciphertext and the detached 16-byte
+ * tag, always writes inlen bytes of plaintext, and returns 1 when the tag matches and 0 otherwise
+ * (lib/fusion.c:660-...).  new returns NULL for a key size other than 16 or 32, or without a device. */
+typedef struct ptls_hip_aesgcm_context ptls_hip_aesgcm_context_t;
+ptls_hip_aesgcm_context_t *ptls_hip_aesgcm_new(const void *key, size_t key_size, size_t capacity);
+ptls_hip_aesgcm_context_t *ptls_hip_aesgcm_set_capacity(ptls_hip_aesgcm_context_t *ctx, size_t capacity);
+void ptls_hip_aesgcm_free(ptls_hip_aesgcm_context_t *ctx);
+void ptls_hip_aesgcm_encrypt(ptls_hip_aesgcm_context_t *ctx, void *output, const void *input, size_t inlen, const void *nonce,
+                             const void *aad, size_t aadlen, ptls_aead_supplementary_encryption_t *supp);
+int ptls_hip_aesgcm_decrypt(ptls_hip_aesgcm_context_t *ctx, void *output, const void *input, size_t inlen, const void *nonce,
+                            const void *aad, size_t aadlen, const void *tag);
+
 /* ------------------------------------------------------------------------------------------ *
  * 2. batch extension                                                                          *
  * ------------------------------------------------------------------------------------------ */

@@ -118,6 +118,8 @@ def test_fails_loudly_without_device():
     assert "device" in ptls_hip.last_error().lower()
     with pytest.raises(ptls_hip.HipError):
         ptls_hip.Engine(0)
+    with pytest.raises(ptls_hip.HipError):  # the fusion-style low-level context too
+        ptls_hip.AesGcm(bytes(16), 64)
     from oracle_lib import REF_SO, Ref
     if Ref.available:
         ref = ctypes.CDLL(REF_SO)

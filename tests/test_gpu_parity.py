@@ -69,6 +69,68 @@ def test_is_supported_on_mi355x(engine):
     assert ptls_hip.is_supported()
 
 
+def test_lowlevel_context_fusion_tests(engine, oracle, golden):
+    """ptls_hip_aesgcm_* as t/fusion.c drives ptls_fusion_aesgcm_*: gcm_basic (:235-251), gcm_capacity
+    (:276-287, capacity 2 then a larger record) and gcm_test_vectors (:289-343, without and with the supp
+    block from ptls_hip_aes128ctr); counter block 0 there is the all-zero nonce here"""
+    k = golden["kats"]
+    zero_nonce = bytes(12)
+    b1 = k["aead"][0]
+    ctx = ptls_hip.AesGcm(bytes(16), 5 + 16)
+    exp = bytes.fromhex(b1["out"])
+    assert ctx.encrypt(bytes(16), zero_nonce, b"hello") == exp
+    assert ctx.decrypt(exp[:16], zero_nonce, b"hello", exp[16:]) == (True, bytes(16))
+    ctx.close()
+    cap = k["aead"][2]
+    ctx = ptls_hip.AesGcm(bytes(16), 2)
+    exp = bytes.fromhex(cap["out"])
+    assert ctx.encrypt(b"X", zero_nonce, b"a") == exp
+    assert ctx.decrypt(exp[:1], zero_nonce, b"a", exp[1:]) == (True, b"X")
+    big = bytes(range(256)) * 20  # past the initial capacity: staging grows
+    assert ctx.encrypt(big, zero_nonce, b"a") == oracle.seal(bytes(16), zero_nonce, 0, b"a", big)
+    ctx.set_capacity(1 << 16)
+    assert ctx.encrypt(b"X", zero_nonce, b"a") == exp
+    ctx.close()
+    from oracle_lib import Ref
+    tv = k["gcm_test_vectors"]
+    ctx = ptls_hip.AesGcm(bytes(16), 2048)
+    for v in tv:
+        out = ctx.encrypt(bytes(v["ptlen"]), zero_nonce, bytes(v["aadlen"]))
+        assert out[v["ptlen"]:].hex() == v["tag"], v
+        ok, pt = ctx.decrypt(out[:v["ptlen"]], zero_nonce, bytes(v["aadlen"]), out[v["ptlen"]:])
+        assert ok and pt == bytes(v["ptlen"])
+    if Ref.available:
+        import plugin_driver
+        drv = plugin_driver.PluginDriver()
+        cctx = drv.cipher_new(128, bytes([1] * 16))
+        for v in tv:
+            out, supp = ctx.encrypt(bytes(v["ptlen"]), zero_nonce, bytes(v["aadlen"]), cctx, 2)
+            assert out[v["ptlen"]:].hex() == v["tag"] and supp.hex() == v["supp"], v
+        drv.cipher_free(cctx)
+    ctx.close()
+
+
+def test_lowlevel_context_random_and_tamper(engine, oracle):
+    """ptls_hip_aesgcm_* against the oracle on random keys/nonces/lengths, the nonce changing per call;
+    a bad detached tag returns 0 with the plaintext still written (lib/fusion.c:660-..., decrypt-then-verify)"""
+    rng = np.random.default_rng(1234)
+    for key_len in (16, 32):
+        key = rng.integers(0, 256, key_len, dtype=np.uint8).tobytes()
+        ctx = ptls_hip.AesGcm(key, 1500)
+        for _ in range(12):
+            nonce = rng.integers(0, 256, 12, dtype=np.uint8).tobytes()
+            aad = rng.integers(0, 256, int(rng.integers(0, 40)), dtype=np.uint8).tobytes()
+            text = rng.integers(0, 256, int(rng.integers(0, 5000)), dtype=np.uint8).tobytes()
+            out = ctx.encrypt(text, nonce, aad)
+            assert out == oracle.seal(key, nonce, 0, aad, text)
+            assert ctx.decrypt(out[:len(text)], nonce, aad, out[len(text):]) == (True, text)
+            bad = bytearray(out[len(text):])
+            bad[5] ^= 0x80
+            ok, pt = ctx.decrypt(out[:len(text)], nonce, aad, bytes(bad))
+            assert not ok and pt == text
+        ctx.close()
+
+
 def test_tamper_returns_size_max_and_writes_plaintext(engine, golden):
     """aead_do_decrypt returns SIZE_MAX on a bad tag (lib/fusion.c:1162-1164) but the plaintext has
     already been written (decrypt-then-verify, :822-840); t/picotls.c test_ciphersuite flips a bit."""
