@@ -56,6 +56,9 @@ __host__ __device__ constexpr uint32_t lds_bytes(int log2g)
 #ifndef SKEWED
 #define SKEWED 1 /* ctr_ghash_skewed (the lane's KP blocks 1/KP of a round apart) */
 #endif
+#ifndef SPLIT_PROBE
+#define SPLIT_PROBE 0 /* timing ablation only: 1 = AES-CTR part alone, 2 = GHASH part alone (wrong output) */
+#endif
 #ifndef PURE_BLOCKS
 #define PURE_BLOCKS 2 /* data blocks per lane per iteration of the branch-free loop */
 #endif
@@ -875,7 +878,7 @@ __global__ void __launch_bounds__(WGT)
 
     for (uint32_t ci = blockIdx.x; ci < nchunks; ci += gridDim.x) {
         const Chunk ch = chunks[ci];
-        if (ch.key != cur_key) {
+        if (SPLIT_PROBE != 1 && ch.key != cur_key) {
             __syncthreads();
             build_ghash_tables(lds, basis + (size_t)ch.key * (NPOW * 128 * 4), LOG2G);
             __syncthreads();
@@ -943,7 +946,8 @@ __global__ void __launch_bounds__(WGT)
                     ks[b] = V4{n0, n1, n2, cw[b]};
                     big |= (e[b].is_c && e[b].c >= 65534) ? 1 : 0;
                 }
-                if (wave_max(big))
+                if (SPLIT_PROBE == 2) {
+                } else if (wave_max(big))
                     aes_encrypt_n<ROUNDS, 2>(lds, lb_aes, rk, ks);
                 else
 #if GEN_SKEWED
@@ -958,7 +962,7 @@ __global__ void __launch_bounds__(WGT)
 #pragma unroll
                 for (int b = 0; b < 2; ++b) {
                     const V4 x = finish_elem<OPEN, ALIGNED>(e[b], in[b], ks[b], aad_p, A, L, out_p, ek0);
-                    if (e[b].active)
+                    if (SPLIT_PROBE != 1 && e[b].active)
                         y = gh_mul_main(lds, gl, y, x);
                 }
             };
@@ -976,7 +980,8 @@ __global__ void __launch_bounds__(WGT)
                 const uint32_t cw0[1] = {e0.is_c ? bswap32((uint32_t)e0.c + 2u) : 0x01000000u};
                 V4 ks0[1] = {V4{n0, n1, n2, cw0[0]}};
 #if GEN_SKEWED
-                if (!wave_max((e0.is_c && e0.c >= 65534) ? 1 : 0)) {
+                if (SPLIT_PROBE == 2) {
+                } else if (!wave_max((e0.is_c && e0.c >= 65534) ? 1 : 0)) {
                     const V4 nohash[1] = {V4{0, 0, 0, 0}};
                     V4 ydummy = V4{0, 0, 0, 0};
                     ctr_ghash<ROUNDS, 1, false>(lds, lb_aes, rk, cc, cw0, ks0, ydummy, nohash, gl);
@@ -984,7 +989,7 @@ __global__ void __launch_bounds__(WGT)
 #endif
                     aes_encrypt_n<ROUNDS, 1>(lds, lb_aes, rk, ks0);
                 const V4 x0 = finish_elem<OPEN, ALIGNED>(e0, in0, ks0[0], aad_p, A, L, out_p, ek0);
-                if (e0.active)
+                if (SPLIT_PROBE != 1 && e0.active)
                     y = gh_mul_main(lds, gl, y, x0);
             };
 
@@ -1007,7 +1012,7 @@ __global__ void __launch_bounds__(WGT)
             /* AAD elements: GHASH only (no keystream); y = 0 * P ^ x = x for the first one */
             const int naad = wave_max(my_mlo);
             for (int j = 0; j < naad; ++j) {
-                if (j < my_mlo) {
+                if (SPLIT_PROBE != 1 && j < my_mlo) {
                     const Elem e = elem_of(i0 + j * G, N, na, nc, L);
                     const V4 x = load_block<ALIGNED>(aad_p + 16 * e.i, min(16, A - 16 * e.i));
                     y = j == 0 ? x : gh_mul_main(lds, gl, y, x);
@@ -1040,7 +1045,16 @@ __global__ void __launch_bounds__(WGT)
                         k[b] = V4{n0, n1, n2, cw[b]};
                     }
                     __builtin_amdgcn_sched_barrier(0); /* keep the prefetch at the top of the iteration */
-                    if (OPEN) {
+                    if (SPLIT_PROBE == 1) {
+                        ctr_ghash<ROUNDS, KP, false>(lds, lb_aes, rk, cc, cw, k, y, d, gl);
+#pragma unroll
+                        for (int b = 0; b < KP; ++b)
+                            store_full(dst + o + 16 * b * G, v4xor(d[b], k[b]));
+                    } else if (SPLIT_PROBE == 2) {
+#pragma unroll
+                        for (int b = 0; b < KP; ++b)
+                            y = gh_mul_main(lds, gl, y, d[b]);
+                    } else if (OPEN) {
                         /* the input is the ciphertext: hash it in the same iteration */
                         ctr_ghash<ROUNDS, KP, true>(lds, lb_aes, rk, cc, cw, k, y, d, gl);
 #pragma unroll
@@ -1067,7 +1081,7 @@ __global__ void __launch_bounds__(WGT)
                 }
                 if (it < npure)
                     pure_iter(it, true, bufB, bufA);
-                if (!OPEN) {
+                if (!OPEN && SPLIT_PROBE == 0) {
 #pragma unroll
                     for (int b = 0; b < KP; ++b)
                         y = gh_mul_main(lds, gl, y, pend[b]);
@@ -1088,7 +1102,7 @@ __global__ void __launch_bounds__(WGT)
              * from the end of the GHASH input; sum_q y_q * H^(q+1) by a shuffle tree */
             const int q = (nc - r) & (G - 1);
 #pragma unroll
-            for (int lvl = 0; lvl < LOG2G; ++lvl) {
+            for (int lvl = 0; lvl < (SPLIT_PROBE == 1 ? 0 : LOG2G); ++lvl) {
                 const int d = 1 << lvl;
                 const int src = (lane & ~(G - 1)) | ((r - d) & (G - 1));
                 V4 v;

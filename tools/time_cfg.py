@@ -1,0 +1,52 @@
+#!/usr/bin/env python3
+"""Timing-only probe (no parity checks) over one of bench.py's workloads: median seal and open kernel
+times of each library given on the command line.  For ablation builds whose output is wrong."""
+import argparse, os, sys
+import numpy as np
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "hsig-picotls_amd"))
+ap = argparse.ArgumentParser()
+ap.add_argument("libs", nargs="+")
+ap.add_argument("--config", default="c4")
+ap.add_argument("--lanes", type=int, default=0)
+args = ap.parse_args()
+import torch
+import bench
+cfg = dict(bench.CONFIGS[args.config])
+for lib in args.libs:
+    os.environ["PTLS_HIP_LIB"] = lib
+    import ptls_hip
+    ptls_hip.LIB_PATH = lib
+    ptls_hip._lib = None
+    eng = ptls_hip.Engine(0)
+    idx, recs, in_total, out_total, lens = bench.make_workload(cfg, 0)
+    keys, ivs = bench.make_keys(cfg)
+    ks = ptls_hip.KeySet(eng, cfg["key_len"], cfg["keys"])
+    ks.set(0, keys, ivs)
+    sb = ptls_hip.Batch(eng, recs)
+    if args.lanes:
+        sb.set_lanes(args.lanes)
+    ro = recs.copy()
+    ro["in_off"], ro["out_off"] = recs["out_off"], recs["in_off"]
+    ob = ptls_hip.Batch(eng, ro)
+    ob.set_lanes(sb.lanes)
+    d_pt = torch.zeros(in_total + 64, dtype=torch.uint8, device="cuda")
+    d_ct = torch.zeros(out_total + 64, dtype=torch.uint8, device="cuda")
+    d_out = torch.empty(in_total + 64, dtype=torch.uint8, device="cuda")
+    d_aad = torch.zeros(len(recs) * 16, dtype=torch.uint8, device="cuda")
+    d_res = torch.zeros(len(recs), dtype=torch.int64, device="cuda")
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+    ts = []
+    for i in range(6):
+        ev[0].record(); sb.seal(ks, d_pt, d_aad, d_ct); ev[1].record(); ob.open(ks, d_ct, d_aad, d_out, d_res); ev[2].record()
+        torch.cuda.synchronize()
+        if i:
+            ts.append((ev[0].elapsed_time(ev[1]), ev[1].elapsed_time(ev[2])))
+    s, o = np.median(np.array(ts), axis=0)
+    gib = float(lens.sum()) / 2 ** 30
+    print(f"{os.path.basename(lib)} {args.config} lanes={sb.lanes}: seal {s:.3f} ms ({gib / s * 1e3:.1f} GiB/s)  "
+          f"open {o:.3f} ms ({gib / o * 1e3:.1f} GiB/s)", flush=True)
+    sb.close(); ob.close(); ks.close(); eng.close()
+    del d_pt, d_ct, d_out
+    torch.cuda.empty_cache()
