@@ -1583,6 +1583,37 @@ static int aes256gcm_setup(ptls_aead_context_t *ctx, int is_enc, const void *key
     return aesgcm_setup(ctx, is_enc, key, iv, PTLS_AES256_KEY_SIZE);
 }
 
+/* ptls_non_temporal_aes{128,256}gcm's contract (non_temporal_setup, lib/fusion.c:2109-2142): an encrypt
+ * context has do_encrypt / do_encrypt_v and no do_decrypt, a decrypt context the reverse, and the
+ * deprecated init/update/final are NULL.  The bytes are those of the fusion AEAD (the NT engine differs
+ * only in its x86 store and reduction strategy), so the records run through the same kernel. */
+static int non_temporal_setup(ptls_aead_context_t *_ctx, int is_enc, const void *key, const void *iv, size_t key_size)
+{
+    const int ret = aesgcm_setup(_ctx, is_enc, key, iv, key_size);
+    if (ret != 0 || key == nullptr)
+        return ret;
+    _ctx->do_encrypt_init = nullptr;
+    _ctx->do_encrypt_update = nullptr;
+    _ctx->do_encrypt_final = nullptr;
+    if (is_enc) {
+        _ctx->do_decrypt = nullptr;
+    } else {
+        _ctx->do_encrypt = nullptr;
+        _ctx->do_encrypt_v = nullptr;
+    }
+    return 0;
+}
+
+static int non_temporal_aes128gcm_setup(ptls_aead_context_t *ctx, int is_enc, const void *key, const void *iv)
+{
+    return non_temporal_setup(ctx, is_enc, key, iv, PTLS_AES128_KEY_SIZE);
+}
+
+static int non_temporal_aes256gcm_setup(ptls_aead_context_t *ctx, int is_enc, const void *key, const void *iv)
+{
+    return non_temporal_setup(ctx, is_enc, key, iv, PTLS_AES256_KEY_SIZE);
+}
+
 /* Field-for-field the values of ptls_fusion_aes{128,256}ctr / aes{128,256}gcm (lib/fusion.c:1219-1256). */
 extern "C" {
 ptls_cipher_algorithm_t ptls_hip_aes128ctr = {"AES128-CTR", PTLS_AES128_KEY_SIZE, 1, PTLS_AES_IV_SIZE, sizeof(hip_ctr_context),
@@ -1615,6 +1646,34 @@ ptls_aead_algorithm_t ptls_hip_aes256gcm = {"AES256-GCM",
                                             0,
                                             sizeof(hip_aead_context),
                                             aes256gcm_setup};
+/* the values of ptls_non_temporal_aes{128,256}gcm (lib/fusion.c:2154-2179): TLS 1.2 IV split 4 + 8,
+ * non_temporal = 1, align_bits = 6 (64-byte output buffers; this engine accepts any alignment) */
+ptls_aead_algorithm_t ptls_hip_non_temporal_aes128gcm = {"AES128-GCM",
+                                                         PTLS_AESGCM_CONFIDENTIALITY_LIMIT,
+                                                         PTLS_AESGCM_INTEGRITY_LIMIT,
+                                                         &ptls_hip_aes128ctr,
+                                                         nullptr,
+                                                         PTLS_AES128_KEY_SIZE,
+                                                         PTLS_AESGCM_IV_SIZE,
+                                                         PTLS_AESGCM_TAG_SIZE,
+                                                         {4, 8},
+                                                         1,
+                                                         6,
+                                                         sizeof(hip_aead_context),
+                                                         non_temporal_aes128gcm_setup};
+ptls_aead_algorithm_t ptls_hip_non_temporal_aes256gcm = {"AES256-GCM",
+                                                         PTLS_AESGCM_CONFIDENTIALITY_LIMIT,
+                                                         PTLS_AESGCM_INTEGRITY_LIMIT,
+                                                         &ptls_hip_aes256ctr,
+                                                         nullptr,
+                                                         PTLS_AES256_KEY_SIZE,
+                                                         PTLS_AESGCM_IV_SIZE,
+                                                         PTLS_AESGCM_TAG_SIZE,
+                                                         {4, 8},
+                                                         1,
+                                                         6,
+                                                         sizeof(hip_aead_context),
+                                                         non_temporal_aes256gcm_setup};
 }
 
 /* ---- fusion-style low-level single-record API (include/picotls/fusion.h:56-96, lib/fusion.c:400-1048) ----

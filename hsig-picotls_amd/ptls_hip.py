@@ -82,7 +82,8 @@ SIGNATURES = {
     "ptls_hip_host_register": (_i, [_vp, _sz]),
     "ptls_hip_host_unregister": (_i, [_vp]),
 }
-DATA_SYMBOLS = ("ptls_hip_aes128ctr", "ptls_hip_aes128gcm", "ptls_hip_aes256ctr", "ptls_hip_aes256gcm")
+DATA_SYMBOLS = ("ptls_hip_aes128ctr", "ptls_hip_aes128gcm", "ptls_hip_aes256ctr", "ptls_hip_aes256gcm",
+                "ptls_hip_non_temporal_aes128gcm", "ptls_hip_non_temporal_aes256gcm")
 
 _lib = None
 

@@ -48,6 +48,12 @@ const char *ptls_hip_last_error(void);
  * addition implement do_encrypt_v (fusion asserts "FIXME" there, lib/fusion.c:1145-1149). */
 extern ptls_aead_algorithm_t ptls_hip_aes128gcm, ptls_hip_aes256gcm;
 
+/* Replace ptls_non_temporal_aes128gcm / ptls_non_temporal_aes256gcm (lib/fusion.c:2109-2179): the same
+ * field values (TLS 1.2 IV sizes {4, 8}, non_temporal = 1, align_bits = 6) and the same per-direction
+ * vtable (is_enc: do_encrypt + do_encrypt_v, no do_decrypt; otherwise do_decrypt only; init/update/final
+ * NULL).  Output bytes equal the fusion AEAD's, as the reference's own are. */
+extern ptls_aead_algorithm_t ptls_hip_non_temporal_aes128gcm, ptls_hip_non_temporal_aes256gcm;
+
 /* Replace ptls_fusion_aes128ctr / ptls_fusion_aes256ctr (lib/fusion.c:1050-1100, :1219-1230), the
  * `ctr_cipher` of the AEAD objects above and the cipher QUIC stacks use for header protection.
  * Same contract as fusion's: do_init(iv) computes one keystream block AES-ECB(key, iv) on the GPU, and

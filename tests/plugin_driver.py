@@ -53,6 +53,8 @@ class PluginDriver:
         self.ref.ptls_cipher_free.argtypes = [c.c_void_p]
         self.algos = {128: c.addressof(c.c_char.in_dll(hip, "ptls_hip_aes128gcm")),
                       256: c.addressof(c.c_char.in_dll(hip, "ptls_hip_aes256gcm"))}
+        self.nt_algos = {128: c.addressof(c.c_char.in_dll(hip, "ptls_hip_non_temporal_aes128gcm")),
+                         256: c.addressof(c.c_char.in_dll(hip, "ptls_hip_non_temporal_aes256gcm"))}
         self.ctr_algos = {128: c.addressof(c.c_char.in_dll(hip, "ptls_hip_aes128ctr")),
                           256: c.addressof(c.c_char.in_dll(hip, "ptls_hip_aes256ctr"))}
 
@@ -74,8 +76,9 @@ class PluginDriver:
         CIPHER_TRANSFORM(vt.do_transform)(ctx, out, data, len(data))
         return out.raw[:len(data)]
 
-    def new(self, bits, key, iv, is_enc=1):
-        ctx = self.ref.ptls_aead_new_direct(self.algos[bits], is_enc, key, iv)
+    def new(self, bits, key, iv, is_enc=1, non_temporal=False):
+        algo = (self.nt_algos if non_temporal else self.algos)[bits]
+        ctx = self.ref.ptls_aead_new_direct(algo, is_enc, key, iv)
         assert ctx, "ptls_aead_new_direct returned NULL: " + ptls_hip.last_error()
         return ctx
 

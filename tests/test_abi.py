@@ -80,6 +80,26 @@ def test_algorithm_objects_mirror_fusion():
         assert a.conf == 0x2000000 and a.integ == 0x40000000000000
         assert (a.fixed_iv, a.record_iv, a.bits & 1, a.align_bits) == (0, 0, 0, 0)
         assert a.context_size >= 80 and a.setup
+    # ptls_non_temporal_aes{128,256}gcm (lib/fusion.c:2154-2179): TLS 1.2 IV split, non_temporal, 64-B alignment
+    for name, ks, label in (("ptls_hip_non_temporal_aes128gcm", 16, b"AES128-GCM"),
+                            ("ptls_hip_non_temporal_aes256gcm", 32, b"AES256-GCM")):
+        a = Algo.in_dll(L, name)
+        assert a.name == label and a.key_size == ks and a.iv_size == 12 and a.tag_size == 16
+        assert a.conf == 0x2000000 and a.integ == 0x40000000000000
+        assert (a.fixed_iv, a.record_iv, a.bits & 1, a.align_bits) == (4, 8, 1, 6)
+        assert a.context_size >= 80 and a.setup
+    from oracle_lib import REF_SO, Ref
+    if Ref.available:  # and field for field against the reference's own objects
+        ref = ctypes.CDLL(REF_SO)
+        for ours, theirs in (("ptls_hip_aes128gcm", "ptls_fusion_aes128gcm"),
+                             ("ptls_hip_aes256gcm", "ptls_fusion_aes256gcm"),
+                             ("ptls_hip_non_temporal_aes128gcm", "ptls_non_temporal_aes128gcm"),
+                             ("ptls_hip_non_temporal_aes256gcm", "ptls_non_temporal_aes256gcm")):
+            a, b = Algo.in_dll(L, ours), Algo.in_dll(ref, theirs)
+            fields = ("name", "conf", "integ", "key_size", "iv_size", "tag_size", "fixed_iv", "record_iv",
+                      "bits", "align_bits")
+            assert [getattr(a, f) for f in fields] == [getattr(b, f) for f in fields], ours
+            assert (a.ecb is None) == (b.ecb is None)
 
 
 def test_ctr_objects_mirror_fusion():

@@ -344,6 +344,39 @@ def test_full_size_roundtrip_16k(engine, oracle):
         o.close()
 
 
+def test_non_temporal_objects_through_reference_picotls(engine, oracle):
+    """ptls_hip_non_temporal_aes{128,256}gcm through the reference's ptls_aead_new_direct: per-direction
+    vtables as non_temporal_setup (lib/fusion.c:2109-2142) sets them, do_encrypt_v (what ptls_send uses)
+    and do_decrypt equal to lib/fusion.c's bytes"""
+    from oracle_lib import Ref
+    if not Ref.available:
+        pytest.skip("oracle/_ref not built")
+    import plugin_driver
+    drv = plugin_driver.PluginDriver()
+    ref = Ref()
+    rng = np.random.default_rng(4242)
+    for bits in (128, 256):
+        key = rng.integers(0, 256, bits // 8, dtype=np.uint8).tobytes()
+        iv = rng.integers(0, 256, 12, dtype=np.uint8).tobytes()
+        enc = drv.new(bits, key, iv, is_enc=1, non_temporal=True)
+        dec = drv.new(bits, key, iv, is_enc=0, non_temporal=True)
+        ve, vd = plugin_driver.AeadContext.from_address(enc), plugin_driver.AeadContext.from_address(dec)
+        assert ve.do_encrypt and ve.do_encrypt_v and not ve.do_decrypt
+        assert vd.do_decrypt and not vd.do_encrypt and not vd.do_encrypt_v
+        assert not (ve.do_encrypt_init or ve.do_encrypt_update or ve.do_encrypt_final)
+        for L in (0, 1, 16, 100, 1350, 16384):
+            seq = int(rng.integers(0, 2 ** 40))
+            aad = rng.integers(0, 256, 5, dtype=np.uint8).tobytes()
+            text = rng.integers(0, 256, L, dtype=np.uint8).tobytes()
+            expect = ref.seal(key, iv, seq, aad, text)
+            cut = [0, L // 3, L]
+            assert drv.encrypt_v(enc, [text[cut[i]:cut[i + 1]] for i in range(2)], seq, aad) == expect
+            assert drv.encrypt(enc, text, seq, aad) == expect
+            assert drv.decrypt(dec, expect, seq, aad) == text
+        drv.free(enc)
+        drv.free(dec)
+
+
 def test_plugin_through_reference_picotls(engine, oracle, golden):
     """Drop-in: the reference's own ptls_aead_new_direct / ptls_aead_xor_iv (oracle/_ref, i.e.
     lib/picotls.c) instantiate ptls_hip_aes128gcm / aes256gcm and drive them through the vtable,
