@@ -55,7 +55,8 @@ __global__ void __launch_bounds__(256) tls13_inner_kernel(const ptls_hip_record_
 template <int ROUNDS>
 __global__ void __launch_bounds__(256) aesecb_batch_kernel(const ptls_hip_supp_t *__restrict__ supp, uint32_t n,
                                                            const uint8_t *__restrict__ src, uint8_t *__restrict__ mask,
-                                                           const KeySlot *__restrict__ hp_slots, const uint32_t *__restrict__ t0)
+                                                           const KeySlot *__restrict__ hp_slots, uint32_t hp_nslots,
+                                                           const uint32_t *__restrict__ t0)
 {
     __shared__ __attribute__((aligned(16))) uint8_t lds[LDS_AES + 65536];
     build_aes_tables(lds, t0);
@@ -63,7 +64,7 @@ __global__ void __launch_bounds__(256) aesecb_batch_kernel(const ptls_hip_supp_t
     const uint32_t lb_aes = (uint32_t)(threadIdx.x & 31) * 4u | LDS_AES;
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
         const ptls_hip_supp_t sp = supp[i];
-        if (sp.flags & PTLS_HIP_SUPP_ENABLE) {
+        if ((sp.flags & PTLS_HIP_SUPP_ENABLE) && sp.hp_key < hp_nslots) {
             const V4 m = aes_encrypt<ROUNDS>(lds, lb_aes, hp_slots[sp.hp_key].rk, load_full(src + sp.sample_off));
             store_full(mask + sp.mask_off, m);
         }
@@ -302,13 +303,13 @@ int launch_tls13_inner(const ptls_hip_record_t *recs, uint32_t n, const uint8_t 
 }
 
 int launch_aesecb(int rounds, const ptls_hip_supp_t *supp, uint32_t n, const uint8_t *src, uint8_t *mask, const KeySlot *hp_slots,
-                  const uint32_t *t0, unsigned grid, void *stream)
+                  uint32_t hp_nslots, const uint32_t *t0, unsigned grid, void *stream)
 {
     hipStream_t s = static_cast<hipStream_t>(stream);
     if (rounds == 10)
-        hipLaunchKernelGGL(aesecb_batch_kernel<10>, dim3(grid), dim3(256), 0, s, supp, n, src, mask, hp_slots, t0);
+        hipLaunchKernelGGL(aesecb_batch_kernel<10>, dim3(grid), dim3(256), 0, s, supp, n, src, mask, hp_slots, hp_nslots, t0);
     else
-        hipLaunchKernelGGL(aesecb_batch_kernel<14>, dim3(grid), dim3(256), 0, s, supp, n, src, mask, hp_slots, t0);
+        hipLaunchKernelGGL(aesecb_batch_kernel<14>, dim3(grid), dim3(256), 0, s, supp, n, src, mask, hp_slots, hp_nslots, t0);
     return (int)hipGetLastError();
 }
 

@@ -860,7 +860,8 @@ __global__ void __launch_bounds__(WGT)
                         const Chunk *__restrict__ chunks, uint32_t nchunks,
                         const uint8_t *in, const uint8_t *__restrict__ aad, uint8_t *out, uint64_t *__restrict__ result,
                         const KeySlot *__restrict__ slots, const uint32_t *__restrict__ basis, const uint32_t *__restrict__ t0,
-                        const ptls_hip_supp_t *__restrict__ supp, const KeySlot *__restrict__ hp_slots, uint8_t *mask)
+                        const ptls_hip_supp_t *__restrict__ supp, const KeySlot *__restrict__ hp_slots, uint32_t hp_nslots,
+                        uint8_t *mask)
 {
     constexpr int LOG2G = G == 1 ? 0 : G == 2 ? 1 : G == 4 ? 2 : G == 8 ? 3 : 4;
     __shared__ __attribute__((aligned(16))) uint8_t lds[lds_bytes(LOG2G)];
@@ -1134,7 +1135,7 @@ __global__ void __launch_bounds__(WGT)
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
                 if (valid && r == 0) {
                     const ptls_hip_supp_t sp = supp[rec_i];
-                    if (sp.flags & PTLS_HIP_SUPP_ENABLE) {
+                    if ((sp.flags & PTLS_HIP_SUPP_ENABLE) && sp.hp_key < hp_nslots) {
                         const V4 sample = load_full(out + sp.sample_off);
                         const V4 m = aes_encrypt<ROUNDS>(lds, lb_aes, hp_slots[sp.hp_key].rk, sample);
                         store_full(mask + sp.mask_off, m);
@@ -1150,10 +1151,10 @@ static hipError_t launch_one(unsigned grid, hipStream_t s, const KernelArgs &a, 
 {
     if (aligned)
         hipLaunchKernelGGL((aesgcm_batch_kernel<G, R, O, true, W>), dim3(grid), dim3(W), 0, s, a.recs_ord, a.order, a.chunks,
-                           a.nchunks, a.in, a.aad, a.out, a.result, a.slots, a.basis, a.t0, a.supp, a.hp_slots, a.mask);
+                           a.nchunks, a.in, a.aad, a.out, a.result, a.slots, a.basis, a.t0, a.supp, a.hp_slots, a.hp_nslots, a.mask);
     else
         hipLaunchKernelGGL((aesgcm_batch_kernel<G, R, O, false, W>), dim3(grid), dim3(W), 0, s, a.recs_ord, a.order, a.chunks,
-                           a.nchunks, a.in, a.aad, a.out, a.result, a.slots, a.basis, a.t0, a.supp, a.hp_slots, a.mask);
+                           a.nchunks, a.in, a.aad, a.out, a.result, a.slots, a.basis, a.t0, a.supp, a.hp_slots, a.hp_nslots, a.mask);
     return hipGetLastError();
 }
 

@@ -125,6 +125,7 @@ struct st_ptls_hip_batch_t {
     bool all_aligned; /* every descriptor's in/out/aad offset is a multiple of 16 */
     int auto_lanes; /* chosen from the record lengths */
     bool forced;
+    uint32_t max_key; /* largest key slot any record names (checked against the keyset at seal/open) */
 };
 
 class DeviceGuard {
@@ -498,6 +499,9 @@ extern "C" ptls_hip_batch_t *ptls_hip_batch_new(ptls_hip_engine_t *eng, const pt
     b->eng = eng;
     b->n = n;
     b->h_recs.assign(recs, recs + n);
+    b->max_key = 0;
+    for (size_t i = 0; i < n; ++i)
+        b->max_key = std::max(b->max_key, recs[i].key);
     b->auto_lanes = b->lanes = choose_lanes(b->h_recs);
     if (n != 0) {
         if (hipMalloc(&b->d_recs, n * sizeof(ptls_hip_record_t)) != hipSuccess ||
@@ -574,6 +578,8 @@ static int run_batch(ptls_hip_batch_t *b, ptls_hip_keyset_t *ks, const void *in,
                                      "AEAD's key size, and mask must be given");
     if (b->n == 0)
         return 0;
+    if (b->max_key >= ks->nslots)
+        return fail(PTLS_HIP_EINVAL, "seal/open: a record names key slot %u, the keyset has %zu", b->max_key, ks->nslots);
     if (in == nullptr || out == nullptr || (open && result == nullptr))
         return fail(PTLS_HIP_EINVAL, "seal/open: null buffer");
     DeviceGuard g(b->eng->device);
@@ -592,6 +598,7 @@ static int run_batch(ptls_hip_batch_t *b, ptls_hip_keyset_t *ks, const void *in,
     a.t0 = b->eng->d_t0;
     a.supp = supp;
     a.hp_slots = hp_ks != nullptr ? hp_ks->d_slots : nullptr;
+    a.hp_nslots = hp_ks != nullptr ? (uint32_t)hp_ks->nslots : 0;
     a.mask = static_cast<uint8_t *>(mask);
     const bool base_aligned = ((reinterpret_cast<uintptr_t>(in) | reinterpret_cast<uintptr_t>(a.aad) |
                                 reinterpret_cast<uintptr_t>(out)) & 15) == 0;
@@ -630,7 +637,8 @@ extern "C" int ptls_hip_aesecb_batch(ptls_hip_engine_t *eng, ptls_hip_keyset_t *
     DeviceGuard g(eng->device);
     const unsigned grid = (unsigned)std::min<size_t>((n + 255) / 256, (size_t)eng->ncu * 4);
     const int e = launch_aesecb(hp_ks->key_size == 16 ? 10 : 14, supp, (uint32_t)n, static_cast<const uint8_t *>(src),
-                                static_cast<uint8_t *>(mask), hp_ks->d_slots, eng->d_t0, grid, stream);
+                                static_cast<uint8_t *>(mask), hp_ks->d_slots, (uint32_t)hp_ks->nslots, eng->d_t0, grid,
+                                stream);
     if (e != 0)
         return fail(PTLS_HIP_ELAUNCH, "aesecb_batch: kernel launch failed: %s", hipGetErrorString((hipError_t)e));
     return 0;
@@ -901,6 +909,9 @@ static int pipeline_run(ptls_hip_pipeline_t *p, ptls_hip_keyset_t *ks, const ptl
     if (p == nullptr || ks == nullptr || ks->eng != p->eng || (n != 0 && (recs == nullptr || h_in == nullptr || h_out == nullptr)) ||
         (open && h_result == nullptr))
         return fail(PTLS_HIP_EINVAL, "pipeline seal/open: bad arguments");
+    for (size_t i = 0; i < n; ++i)
+        if (recs[i].key >= ks->nslots)
+            return fail(PTLS_HIP_EINVAL, "pipeline: record %zu names key slot %u, the keyset has %zu", i, recs[i].key, ks->nslots);
     DeviceGuard g(p->eng->device);
     const int rounds = ks->key_size == 16 ? 10 : 14;
     const size_t tag_in = open ? 16 : 0, tag_out = open ? 0 : 16;
@@ -1027,6 +1038,7 @@ static int pipeline_run(ptls_hip_pipeline_t *p, ptls_hip_keyset_t *ks, const ptl
         if (supp != nullptr) {
             a.supp = s.d_supp;
             a.hp_slots = hp_ks->d_slots;
+            a.hp_nslots = (uint32_t)hp_ks->nslots;
             a.mask = s.d_mask;
         }
         const unsigned grid = std::min<unsigned>((unsigned)ch.size(), (unsigned)p->eng->ncu);
@@ -1196,7 +1208,7 @@ static void ctr_init(ptls_cipher_context_t *_ctx, const void *iv)
     std::memcpy(st->h_stage + 32, iv, 16);
     plugin_check(hipMemcpyAsync(st->d_buf, st->h_stage, 48, hipMemcpyHostToDevice, st->stream), "ctr upload");
     const int e = launch_aesecb(st->ks->key_size == 16 ? 10 : 14, reinterpret_cast<const ptls_hip_supp_t *>(st->d_buf), 1,
-                                st->d_buf, st->d_buf, st->ks->d_slots, st->eng->d_t0, 1, st->stream);
+                                st->d_buf, st->d_buf, st->ks->d_slots, 1, st->eng->d_t0, 1, st->stream);
     if (e != 0) {
         g_err = hipGetErrorString((hipError_t)e);
         plugin_die("ctr launch");
@@ -1373,6 +1385,7 @@ static uint64_t plugin_run(hip_aead_state *st, bool open, void *output, const vo
         uint8_t *d_stage = reinterpret_cast<uint8_t *>(st->d_rec);
         a.supp = reinterpret_cast<const ptls_hip_supp_t *>(d_stage + ST_SUPP);
         a.hp_slots = ps->hp_slots;
+        a.hp_nslots = 1;
         a.mask = d_stage + ST_MASK;
     }
     const size_t n = (aadlen + 15) / 16 + (len + 15) / 16 + 1;

@@ -171,7 +171,8 @@ int ptls_hip_batch_lanes(ptls_hip_batch_t *batch);
 int ptls_hip_batch_set_workgroup(ptls_hip_batch_t *batch, int threads);
 int ptls_hip_batch_workgroup(ptls_hip_batch_t *batch);
 
-/* Asynchronous on `stream`; all pointers are device (or device-accessible) memory. */
+/* Asynchronous on `stream`; all pointers are device (or device-accessible) memory.  Fails with
+ * PTLS_HIP_EINVAL (nothing launched) when a record names a key slot outside `ks`. */
 int ptls_hip_aesgcm_seal_batch(ptls_hip_batch_t *batch, ptls_hip_keyset_t *ks, const void *in, const void *aad, void *out,
                                void *stream);
 int ptls_hip_aesgcm_open_batch(ptls_hip_batch_t *batch, ptls_hip_keyset_t *ks, const void *in, const void *aad, void *out,
@@ -181,7 +182,9 @@ int ptls_hip_aesgcm_open_batch(ptls_hip_batch_t *batch, ptls_hip_keyset_t *ks, c
  * One descriptor per record (same index as the batch's descriptors): mask + mask_off receives the
  * 16-byte AES-ECB(hp key slot `hp_key`, 16 bytes at sample_off) -- for seal the sample is read from
  * `out` AFTER the record (ciphertext and tag) is written, so it may cover the tag, exactly like
- * fusion's supplementary block.  Records with (flags & 1) == 0 are skipped.  The header-protection
+ * fusion's supplementary block.  Records with (flags & 1) == 0, or whose hp_key is outside the
+ * header-protection keyset (the descriptors are device data, so this is checked on the device), are
+ * skipped and their mask bytes left untouched.  The header-protection
  * keyset must have the AEAD keyset's key size (fusion runs the supp block with the AEAD's rounds). */
 typedef struct st_ptls_hip_supp_t {
     uint64_t sample_off;

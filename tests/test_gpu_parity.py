@@ -131,6 +131,30 @@ def test_lowlevel_context_random_and_tamper(engine, oracle):
         ctx.close()
 
 
+def test_key_slot_out_of_range_is_rejected(engine):
+    """a record naming a key slot outside the keyset fails with EINVAL before anything is launched
+    (device-resident batch and host pipeline), instead of reading past the keyset on the device"""
+    recs, it, ot, _ = ptls_hip.layout_records(np.array([100, 200]), np.array([5, 5]), np.array([0, 1]), np.array([0, 1]))
+    ks = ptls_hip.KeySet(engine, 16, 1)
+    ks.set(0, bytes(16), bytes(12))
+    b = ptls_hip.Batch(engine, recs)
+    d_in = torch.zeros(it + 64, dtype=torch.uint8, device="cuda")
+    d_out = torch.zeros(ot + 64, dtype=torch.uint8, device="cuda")
+    with pytest.raises(ptls_hip.HipError, match="key slot 1"):
+        b.seal(ks, d_in, d_in, d_out)
+    pipe = ptls_hip.Pipeline(engine, 64 << 10)
+    h_in = torch.zeros(it + 64, dtype=torch.uint8).pin_memory()
+    h_out = torch.zeros(ot + 64, dtype=torch.uint8).pin_memory()
+    with pytest.raises(ptls_hip.HipError, match="key slot 1"):
+        pipe.seal(ks, recs, h_in, h_in, h_out)
+    ks2 = ptls_hip.KeySet(engine, 16, 2)
+    ks2.set(0, bytes(32), bytes(24))
+    b.seal(ks2, d_in, d_in, d_out)  # in range: runs
+    torch.cuda.synchronize()
+    for o in (pipe, b, ks, ks2):
+        o.close()
+
+
 def test_tamper_returns_size_max_and_writes_plaintext(engine, golden):
     """aead_do_decrypt returns SIZE_MAX on a bad tag (lib/fusion.c:1162-1164) but the plaintext has
     already been written (decrypt-then-verify, :822-840); t/picotls.c test_ciphersuite flips a bit."""
@@ -440,7 +464,8 @@ def test_seal_batch_quic_header_protection(engine, oracle, key_len, path):
     """QUIC header protection fused into the seal launch (fusion's supp,
     lib/fusion.c:424-428, :636-650).  Packets of 20-1500 B with 16-40 B headers as AAD, 3 AEAD keys,
     2 header-protection keys, samples anywhere in ciphertext || tag (incl. covering the tag), some
-    records without HP.  Ciphertext == oracle, mask == AES-ECB(hp key, sample of the output)."""
+    records without HP, some naming an hp key slot outside the keyset (skipped, mask untouched).
+    Ciphertext == oracle, mask == AES-ECB(hp key, sample of the output)."""
     rng = np.random.default_rng(key_len)
     hp_keys = [rng.integers(0, 256, key_len, dtype=np.uint8).tobytes() for _ in range(2)]
     recs = []
@@ -456,8 +481,9 @@ def test_seal_batch_quic_header_protection(engine, oracle, key_len, path):
         L = len(r[4])
         off = int(rng.integers(0, L + 1)) if j % 5 else L  # j % 5 == 0: sample == the tag
         enabled = j % 7 != 3
-        rows.append((int(rec["out_off"]) + off, 16 * j, j % 2, ptls_hip.SUPP_ENABLE if enabled else 0))
-        expect.append((off, j % 2, enabled))
+        hp_key = 7 if j % 11 == 5 else j % 2  # 7: outside the 2-slot keyset -> skipped on the device
+        rows.append((int(rec["out_off"]) + off, 16 * j, hp_key, ptls_hip.SUPP_ENABLE if enabled else 0))
+        expect.append((off, j % 2, enabled and hp_key < 2))
     h_in = hb._input([r[4] for r in recs])
     h_aad = np.concatenate([hb.aad, np.zeros(16, np.uint8)])
     if path == "device":
