@@ -32,12 +32,12 @@ namespace ptls_hip {
 /* ---------------- LDS map (bytes) ---------------- */
 constexpr uint32_t LDS_GMAIN = 0;            /* 64 KiB: row v (256 B) = 16 positions x 16 B, P = H^G       */
 constexpr uint32_t LDS_AES = 65536;          /* 64 KiB: row v = [T0 x32 lane slots | T2 x32 lane slots]  */
-constexpr uint32_t LDS_GTREE = 131072;       /* up to 4 x 8 KiB nibble tables for H^1, H^2, H^4, H^8: [p(32)][v(16)] */
+constexpr uint32_t LDS_GTREE = 131072;       /* 3 x 8 KiB nibble tables for H^1, H^2, H^4: [p(32)][v(16)] */
 constexpr uint32_t LDS_TREE_STRIDE = 8192;
-/* the tree needs max(log2 G, 1) nibble tables: 152 KiB for G <= 8, all 160 KiB of the CU for G = 16 */
+constexpr int TREE_TABLES = 3; /* G = 16's level for H^8 multiplies by H^4 twice, so every G fits in 152 KiB */
 __host__ __device__ constexpr uint32_t lds_bytes(int log2g)
 {
-    return LDS_GTREE + (log2g > 3 ? log2g : 3) * LDS_TREE_STRIDE;
+    return (void)log2g, LDS_GTREE + TREE_TABLES * LDS_TREE_STRIDE;
 }
 
 /* Tuning switches (defaults are the measured best):
@@ -58,6 +58,9 @@ __host__ __device__ constexpr uint32_t lds_bytes(int log2g)
 #endif
 #ifndef SPLIT_PROBE
 #define SPLIT_PROBE 0 /* timing ablation only: 1 = AES-CTR part alone, 2 = GHASH part alone (wrong output) */
+#endif
+#ifndef DYN_DEAL
+#define DYN_DEAL 1 /* waves draw tasks from a workgroup counter in LDS instead of a fixed per-chunk deal: c2 +3 %, c3 +5 %, c4 +5 % */
 #endif
 #ifndef PURE_BLOCKS
 #define PURE_BLOCKS 2 /* data blocks per lane per iteration of the branch-free loop */
@@ -683,7 +686,8 @@ __device__ void build_ghash_tables(uint8_t *lds, const uint32_t *__restrict__ ba
                 acc = v4xor(acc, ld_basis(bm, 8 * p + 7 - t));
         lds128_store(lds, LDS_GMAIN + v * 256 + p * 16, acc);
     }
-    const int ntree = log2g > 1 ? log2g : 1; /* H^(2^d) for the tree levels d < log2 G; d = 0 (H) always */
+    /* H^(2^d) for the tree levels d < log2 G (at most H^4); d = 0 (H) always */
+    const int ntree = log2g < 1 ? 1 : log2g > TREE_TABLES ? TREE_TABLES : log2g;
     for (int e = threadIdx.x; e < ntree * 512; e += blockDim.x) {
         const int d = e >> 9, p = (e >> 4) & 31, v = e & 15;
         const int w = p >> 3, j = p & 7;
@@ -864,7 +868,11 @@ __global__ void __launch_bounds__(WGT)
                         uint8_t *mask)
 {
     constexpr int LOG2G = G == 1 ? 0 : G == 2 ? 1 : G == 4 ? 2 : G == 8 ? 3 : 4;
-    __shared__ __attribute__((aligned(16))) uint8_t lds[lds_bytes(LOG2G)];
+    /* DYN_DEAL: the task counter sits after the tables */
+    constexpr bool DYN = DYN_DEAL != 0;
+    static_assert(lds_bytes(LOG2G) + 16 <= 163840, "tables + task counter must fit the CU's 160 KiB");
+    __shared__ __attribute__((aligned(16))) uint8_t lds[lds_bytes(LOG2G) + (DYN ? 16 : 0)];
+    uint32_t *const task_ctr = reinterpret_cast<uint32_t *>(lds + lds_bytes(LOG2G));
     constexpr int R = 64 / G; /* records per wave task */
 
     const int lane = threadIdx.x & 63;
@@ -876,26 +884,52 @@ __global__ void __launch_bounds__(WGT)
 
     build_aes_tables(lds, t0);
     uint32_t cur_key = 0xffffffffu;
+    /* DYN: g = the wave's next task in the workgroup's same-key run of chunks (drawn, not yet used);
+     * cbase = tasks of the run's chunks before the current one */
+    uint32_t g = 0, cbase = 0;
+    bool have_g = false;
 
     for (uint32_t ci = blockIdx.x; ci < nchunks; ci += gridDim.x) {
         const Chunk ch = chunks[ci];
         if (SPLIT_PROBE != 1 && ch.key != cur_key) {
             __syncthreads();
             build_ghash_tables(lds, basis + (size_t)ch.key * (NPOW * 128 * 4), LOG2G);
+            if (DYN && threadIdx.x == 0)
+                *task_ctr = 0;
             __syncthreads();
             cur_key = ch.key;
+            cbase = 0;
+            have_g = false; /* a task drawn past the old key's run belongs to no chunk */
         }
         const KeySlot *__restrict__ slot = slots + ch.key;
         const uint32_t *__restrict__ rk = slot->rk;
         const int ntasks = (int)((ch.count + R - 1) / R);
 
-        /* snake order over the chunk's tasks (records sorted by decreasing length): the waves that drew the
-         * longest tasks in one pass draw the shortest ones in the next */
+        /* DYN: a wave draws its next task when it finishes one, across the chunks of a same-key run, in order
+         * (records sorted by decreasing length: longest first).  Waves on one SIMD do not progress equally
+         * (issue arbitration favours the older wave), so a fixed deal leaves the slowest wave on the critical
+         * path.  Otherwise: snake order over the chunk's tasks, the waves that drew the longest tasks in one
+         * pass draw the shortest ones in the next. */
         constexpr int NW = WGT / 64;
         for (int pass = 0;; ++pass) {
-            const int t = pass * NW + ((pass & 1) ? NW - 1 - wave : wave);
-            if (t >= ntasks)
-                break;
+            int t;
+            if (DYN) {
+                if (!have_g) {
+                    uint32_t v = 0;
+                    if (lane == 0)
+                        v = __hip_atomic_fetch_add(task_ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    g = __builtin_amdgcn_readfirstlane(v);
+                    have_g = true;
+                }
+                t = (int)(g - cbase);
+                if (t >= ntasks)
+                    break; /* keep g for the next chunk of the run */
+                have_g = false;
+            } else {
+                t = pass * NW + ((pass & 1) ? NW - 1 - wave : wave);
+                if (t >= ntasks)
+                    break;
+            }
             const uint32_t ridx = (uint32_t)t * R + grp;
             const bool valid = ridx < ch.count;
             /* descriptors in chunk order: the record is one load away (its caller index only matters for
@@ -1111,7 +1145,13 @@ __global__ void __launch_bounds__(WGT)
                 v.w1 = __shfl(y.w1, src, 64);
                 v.w2 = __shfl(y.w2, src, 64);
                 v.w3 = __shfl(y.w3, src, 64);
-                const V4 w = gh_mul_nibble(lds, LDS_GTREE + lvl * LDS_TREE_STRIDE, v);
+                V4 w;
+                if (lvl < TREE_TABLES) {
+                    w = gh_mul_nibble(lds, LDS_GTREE + lvl * LDS_TREE_STRIDE, v);
+                } else { /* H^8 = H^4 * H^4 */
+                    const uint32_t t4 = LDS_GTREE + (TREE_TABLES - 1) * LDS_TREE_STRIDE;
+                    w = gh_mul_nibble(lds, t4, gh_mul_nibble(lds, t4, v));
+                }
                 if ((q & (2 * d - 1)) == 0)
                     y = v4xor(y, w);
             }
@@ -1143,6 +1183,7 @@ __global__ void __launch_bounds__(WGT)
                 }
             }
         }
+        cbase += (uint32_t)ntasks;
     }
 }
 
