@@ -869,7 +869,7 @@ __global__ void __launch_bounds__(WGT)
 {
     constexpr int LOG2G = G == 1 ? 0 : G == 2 ? 1 : G == 4 ? 2 : G == 8 ? 3 : 4;
     /* DYN_DEAL: the task counter sits after the tables */
-    constexpr bool DYN = DYN_DEAL != 0;
+    constexpr bool DYN = DYN_DEAL != 0 && SPLIT_PROBE != 1; /* the counter is reset at key switches, which SPLIT_PROBE 1 skips */
     static_assert(lds_bytes(LOG2G) + 16 <= 163840, "tables + task counter must fit the CU's 160 KiB");
     __shared__ __attribute__((aligned(16))) uint8_t lds[lds_bytes(LOG2G) + (DYN ? 16 : 0)];
     uint32_t *const task_ctr = reinterpret_cast<uint32_t *>(lds + lds_bytes(LOG2G));
