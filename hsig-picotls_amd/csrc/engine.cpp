@@ -421,14 +421,18 @@ static int plan_wg(const std::vector<Chunk> &ch, int lanes)
     return WG_ALT;
 }
 
-/* chunk = run of records with one key slot, sized to keep all waves of a workgroup busy for a few tasks.
- * Inside a chunk the records are ordered by decreasing length, so the 64/lanes records a wave processes
- * together have similar lengths (their branch-free full-block stretch is limited by the shortest). */
-static void build_chunks(const ptls_hip_record_t *recs, size_t n, int lanes, std::vector<Chunk> &ch, std::vector<uint32_t> &order,
-                         bool &all_aligned)
+/* chunk = run of records with one key slot, sized to keep all waves of a workgroup busy for a few tasks
+ * (at most 32 wave tasks), but small enough that a batch of fewer tasks still spreads over every CU (the
+ * grid is one workgroup per chunk up to the CU count).  Inside a chunk the records are ordered by
+ * decreasing length, so the 64/lanes records a wave processes together have similar lengths (their
+ * branch-free full-block stretch is limited by the shortest). */
+static void build_chunks(const ptls_hip_record_t *recs, size_t n, int lanes, unsigned ncu, std::vector<Chunk> &ch,
+                         std::vector<uint32_t> &order, bool &all_aligned)
 {
     const uint32_t per_task = 64u / (uint32_t)lanes;
-    const uint32_t max_chunk = per_task * (WG_MAX / 64) * 2;
+    const size_t tasks = (n + per_task - 1) / per_task;
+    const size_t spread = (tasks + (ncu ? ncu : 1) - 1) / (ncu ? ncu : 1); /* tasks per chunk for >= ncu chunks */
+    const uint32_t max_chunk = per_task * (uint32_t)std::max<size_t>(1, std::min<size_t>((WG_MAX / 64) * 2, spread));
     ch.clear();
     order.resize(n);
     all_aligned = true;
@@ -461,7 +465,7 @@ static int plan_chunks(ptls_hip_batch_t *b)
 {
     std::vector<Chunk> ch;
     std::vector<uint32_t> order;
-    build_chunks(b->h_recs.data(), b->n, b->lanes, ch, order, b->all_aligned);
+    build_chunks(b->h_recs.data(), b->n, b->lanes, (unsigned)b->eng->ncu, ch, order, b->all_aligned);
     b->wg = b->forced_wg ? b->forced_wg : plan_wg(ch, b->lanes);
     if (b->d_chunks != nullptr)
         (void)hipFree(b->d_chunks);
@@ -983,7 +987,7 @@ static int pipeline_run(ptls_hip_pipeline_t *p, ptls_hip_keyset_t *ks, const ptl
             lanes = choose_lanes(tmp);
         }
         bool aligned;
-        build_chunks(s.h_recs, cnt, lanes, ch, order, aligned);
+        build_chunks(s.h_recs, cnt, lanes, (unsigned)p->eng->ncu, ch, order, aligned);
         const uint64_t mask_base = mk.lo & ~(uint64_t)15;
         if (supp != nullptr) {
             for (size_t t = 0; t < cnt; ++t) {

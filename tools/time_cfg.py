@@ -10,10 +10,13 @@ ap = argparse.ArgumentParser()
 ap.add_argument("libs", nargs="+")
 ap.add_argument("--config", default="c4")
 ap.add_argument("--lanes", type=int, default=0)
+ap.add_argument("--records", type=int, default=0, help="override the config's record count")
 args = ap.parse_args()
 import torch
 import bench
 cfg = dict(bench.CONFIGS[args.config])
+if args.records:
+    cfg["n"] = args.records
 for lib in args.libs:
     os.environ["PTLS_HIP_LIB"] = lib
     import ptls_hip
