@@ -406,9 +406,21 @@ static int choose_lanes(const std::vector<ptls_hip_record_t> &recs)
     const double mean = sum / (double)recs.size();
     const double per_run = (double)recs.size() / (double)runs;
     const int g = mean >= 128 ? 8 : mean >= 48 ? 4 : mean >= 16 ? 2 : 1;
+    /* key runs too short to amortise the per-key GHASH tables: the key-independent wave-per-record kernel */
+    if (per_run < SPARSE_MAX_PER_RUN)
+        return SPARSE_LANES;
     if (g == 8 && mean >= 256 && per_run < (double)(WG_ALT / 64) * (64 / 8))
         return 16;
     return g;
+}
+
+/* grid of a launch: one workgroup per CU at most (both kernels fill the LDS); the batch kernel takes one
+ * workgroup per chunk, the sparse kernel one per 12 records (a record per wave) */
+static unsigned plan_grid(size_t n, size_t nchunks, int lanes, unsigned ncu)
+{
+    if (lanes == SPARSE_LANES)
+        return (unsigned)std::max<size_t>(1, std::min<size_t>((n + 11) / 12, (size_t)ncu));
+    return (unsigned)std::min<size_t>(nchunks, ncu);
 }
 
 static int plan_wg(const std::vector<Chunk> &ch, int lanes)
@@ -429,7 +441,7 @@ static int plan_wg(const std::vector<Chunk> &ch, int lanes)
 static void build_chunks(const ptls_hip_record_t *recs, size_t n, int lanes, unsigned ncu, std::vector<Chunk> &ch,
                          std::vector<uint32_t> &order, bool &all_aligned)
 {
-    const uint32_t per_task = 64u / (uint32_t)lanes;
+    const uint32_t per_task = lanes >= 64 ? 1u : 64u / (uint32_t)lanes;
     const size_t tasks = (n + per_task - 1) / per_task;
     const size_t spread = (tasks + (ncu ? ncu : 1) - 1) / (ncu ? ncu : 1); /* tasks per chunk for >= ncu chunks */
     const uint32_t max_chunk = per_task * (uint32_t)std::max<size_t>(1, std::min<size_t>((WG_MAX / 64) * 2, spread));
@@ -542,8 +554,8 @@ extern "C" size_t ptls_hip_batch_count(ptls_hip_batch_t *b)
 
 extern "C" int ptls_hip_batch_set_lanes(ptls_hip_batch_t *b, int lanes)
 {
-    if (b == nullptr || !(lanes == 0 || lanes == 1 || lanes == 2 || lanes == 4 || lanes == 8 || lanes == 16))
-        return fail(PTLS_HIP_EINVAL, "batch_set_lanes: lanes must be 0, 1, 2, 4, 8 or 16");
+    if (b == nullptr || !(lanes == 0 || lanes == 1 || lanes == 2 || lanes == 4 || lanes == 8 || lanes == 16 || lanes == SPARSE_LANES))
+        return fail(PTLS_HIP_EINVAL, "batch_set_lanes: lanes must be 0, 1, 2, 4, 8, 16 or 64");
     DeviceGuard g(b->eng->device);
     const int want = lanes == 0 ? b->auto_lanes : lanes;
     if (want == b->lanes)
@@ -607,7 +619,7 @@ static int run_batch(ptls_hip_batch_t *b, ptls_hip_keyset_t *ks, const void *in,
     const bool base_aligned = ((reinterpret_cast<uintptr_t>(in) | reinterpret_cast<uintptr_t>(a.aad) |
                                 reinterpret_cast<uintptr_t>(out)) & 15) == 0;
     const bool aligned = base_aligned && b->all_aligned;
-    const unsigned grid = std::min<unsigned>(b->nchunks, (unsigned)b->eng->ncu);
+    const unsigned grid = plan_grid(b->n, b->nchunks, b->lanes, (unsigned)b->eng->ncu);
     const int rounds = ks->key_size == 16 ? 10 : 14;
     int e = launch_batch(b->lanes, rounds, open, b->wg, grid, stream, a, aligned);
     if (e != 0)
@@ -1045,7 +1057,7 @@ static int pipeline_run(ptls_hip_pipeline_t *p, ptls_hip_keyset_t *ks, const ptl
             a.hp_nslots = (uint32_t)hp_ks->nslots;
             a.mask = s.d_mask;
         }
-        const unsigned grid = std::min<unsigned>((unsigned)ch.size(), (unsigned)p->eng->ncu);
+        const unsigned grid = plan_grid(cnt, ch.size(), lanes, (unsigned)p->eng->ncu);
         const int e = launch_batch(lanes, rounds, open, plan_wg(ch, lanes), grid, s.stream, a, aligned);
         if (e != 0)
             return fail(PTLS_HIP_ELAUNCH, "pipeline: kernel launch failed: %s", hipGetErrorString((hipError_t)e));

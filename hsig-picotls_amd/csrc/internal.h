@@ -3,7 +3,7 @@
  *
  * HBM layout:
  *   key slots    KeySlot[nslots]             512 B each: round keys, static IV, H powers
- *   GHASH basis  uint4[nslots][NPOW][128]    10 KiB per slot: P * x^e for P in {H, H^2, H^4, H^8, H^16}
+ *   GHASH basis  uint4[nslots][NPOW][128]    14 KiB per slot: P * x^e for P in {H, H^2, ..., H^64}
  *   records      ptls_hip_record_t[n]        48 B descriptors (caller's order)
  *   chunks       Chunk[nchunks]              runs of <= CHUNK_RECS records sharing one key slot
  *   payloads     caller's buffers, untouched layout (in / aad / out)
@@ -16,8 +16,13 @@
 
 namespace ptls_hip {
 
-constexpr int NPOW = 5;          /* H^1, H^2, H^4, H^8, H^16 */
-constexpr int MAX_LANES = 16;    /* lanes per record (G) supported: 1, 2, 4, 8, 16 */
+constexpr int NPOW = 7;          /* H^1, H^2, H^4, H^8, H^16 (batch kernel tables), H^32, H^64 (sparse kernel) */
+constexpr int MAX_LANES = 16;    /* lanes per record (G) of the batch kernel: 1, 2, 4, 8, 16 */
+constexpr int SPARSE_LANES = 64; /* "lanes" value of the wave-per-record kernel (sparse_kernel.hip) */
+/* the planner picks that kernel when a batch's key runs hold fewer records than this on average */
+#ifndef SPARSE_MAX_PER_RUN
+#define SPARSE_MAX_PER_RUN 8
+#endif
 /* one workgroup per CU (LDS-limited); 768 threads (3 waves per SIMD, 168 VGPRs) by default, 512 selectable
  * per batch (engine.cpp:plan_wg).  WG_MAX bounds the chunk size the planner cuts key runs into. */
 constexpr int WG_MAX = 1024;
@@ -70,6 +75,7 @@ int launch_batch_g2(int rounds, bool open, int wg, unsigned grid, void *stream, 
 int launch_batch_g4(int rounds, bool open, int wg, unsigned grid, void *stream, const KernelArgs &a, bool aligned);
 int launch_batch_g8(int rounds, bool open, int wg, unsigned grid, void *stream, const KernelArgs &a, bool aligned);
 int launch_batch_g16(int rounds, bool open, int wg, unsigned grid, void *stream, const KernelArgs &a, bool aligned);
+int launch_batch_sparse(int rounds, bool open, unsigned grid, void *stream, const KernelArgs &a, bool aligned);
 int launch_batch(int lanes, int rounds, bool open, int wg, unsigned grid, void *stream, const KernelArgs &a, bool aligned);
 int launch_keysetup(KeySlot *slots, uint32_t *basis, const uint8_t *keys, const uint8_t *ivs, uint32_t first, uint32_t count,
                     int key_size, const uint32_t *t0, void *stream);

@@ -1,0 +1,224 @@
+/*
+ * sparse_kernel.hip -- AES-GCM seal/open for batches whose key slots hold very few records each
+ * (a server sealing one record for each of many connections).  Same bytes as lib/fusion.c
+ * (ptls_fusion_aesgcm_encrypt :400-658 / _decrypt :660-844), same record descriptors and chunk plan
+ * as aesgcm_batch_kernel (batch_kernel.h), selected by the planner as "64 lanes per record".
+ *
+ * Why a second kernel: aesgcm_batch_kernel keeps ONE key's 8-bit GHASH window tables
+ * in the workgroup's LDS, so each key switch costs a table build and two workgroup barriers, and a key
+ * run of one record leaves 11 of 12 waves waiting (20 GiB/s at 65 536 records over 65 536 keys).
+ * Here every wave works alone on one record at a time:
+ *   - 64 lanes per record: lane l takes GHASH elements e = l, l + 64, ... (Horner with P = H^64), then
+ *     a 6-level shuffle tree multiplies lane l's sum by H^(q+1), q = (N - 1 - l) mod 64;
+ *   - each wave owns an 8 KiB 4-bit-window table in LDS ([nibble position p][value v] = v at p times P),
+ *     rebuilt from the key's basis P * x^e (keysetup: H^(2^t) * x^e, t = 0..6) for P = H^64 before the
+ *     record and for H, H^2, ..., H^32 during the tree: 8 ds_write_b128 per lane per build, no barrier
+ *     (a wave's LDS operations complete in order);
+ *   - a multiply is 32 ds_read_b128 (gh_mul_nibble); AES-CTR uses the batch kernel's 32x-replicated
+ *     T-tables (64 KiB) and round keys through the scalar unit.  64 KiB + 12 x 8 KiB = the CU's 160 KiB.
+ */
+#include "batch_kernel.h"
+
+namespace ptls_hip {
+
+constexpr int SPARSE_WG = 768;
+constexpr uint32_t SP_TAB = 65536; /* per-wave nibble tables, 8 KiB each */
+
+/* T0 / T2 replicated per lane slot at LDS offset 0 (the batch kernel's layout minus its 64 KiB base) */
+__device__ void build_aes_tables_at0(uint8_t *lds, const uint32_t *__restrict__ t0)
+{
+    for (int e = threadIdx.x; e < 256 * 32; e += blockDim.x) {
+        const int v = e >> 5, s = e & 31;
+        const uint32_t t = t0[v];
+        *reinterpret_cast<uint32_t *>(lds + v * 256 + s * 4) = t;
+        *reinterpret_cast<uint32_t *>(lds + v * 256 + 128 + s * 4) = (t << 16) | (t >> 16);
+    }
+}
+
+/* the wave's LDS operations are processed in order: only the compiler must not move them across this */
+__device__ __forceinline__ void wave_lds_sync()
+{
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+/* the wave's nibble table of P (bp[e] = P * x^e, GCM bit e = byte e/8, bit 7 - e%8) at LDS offset tab,
+ * laid out as gh_mul_nibble reads it: entry [p = 8w + j][v] = v at bits 4j..4j+3 of raw word w, times P.
+ * Lane l writes position l/2, values 8(l&1) .. 8(l&1) + 7. */
+__device__ __forceinline__ void build_wave_table(uint8_t *lds, uint32_t tab, const uint4 *__restrict__ bp, int lane)
+{
+    const int p = lane >> 1, w = p >> 3, j = p & 7;
+    V4 b[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+        const int u = 4 * j + t; /* bit u of little-endian word w = raw byte 4w + u/8, bit u%8 */
+        const uint4 v = bp[8 * (4 * w + (u >> 3)) + 7 - (u & 7)];
+        b[t] = V4{v.x, v.y, v.z, v.w};
+    }
+    const V4 hi = (lane & 1) ? b[3] : V4{0, 0, 0, 0};
+    const uint32_t row = tab + (uint32_t)p * 256u + (uint32_t)(lane & 1) * 128u;
+    const V4 b01 = v4xor(b[0], b[1]);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        const V4 lo = (k & 3) == 0 ? V4{0, 0, 0, 0} : (k & 3) == 1 ? b[0] : (k & 3) == 2 ? b[1] : b01;
+        const V4 e = (k & 4) ? v4xor3(hi, lo, b[2]) : v4xor(hi, lo);
+        lds128_store(lds, row + (uint32_t)k * 16u, e);
+    }
+}
+
+template <int ROUNDS, bool OPEN, bool ALIGNED>
+__global__ void __launch_bounds__(SPARSE_WG)
+    aesgcm_sparse_kernel(const ptls_hip_record_t *__restrict__ recs_ord, const uint32_t *__restrict__ order,
+                         const Chunk *__restrict__ chunks, uint32_t nchunks, const uint8_t *in, const uint8_t *__restrict__ aad,
+                         uint8_t *out, uint64_t *__restrict__ result, const KeySlot *__restrict__ slots,
+                         const uint32_t *__restrict__ basis, const uint32_t *__restrict__ t0, const ptls_hip_supp_t *__restrict__ supp,
+                         const KeySlot *__restrict__ hp_slots, uint32_t hp_nslots, uint8_t *mask)
+{
+    __shared__ __attribute__((aligned(16))) uint8_t lds[SP_TAB + (SPARSE_WG / 64) * 8192];
+    static_assert(SP_TAB + (SPARSE_WG / 64) * 8192 <= 163840, "AES tables + per-wave GHASH tables must fit the CU's 160 KiB");
+    const int lane = threadIdx.x & 63;
+    const uint32_t lb_aes = (uint32_t)(lane & 31) * 4u; /* table base 0: byte 2 of the address is 0 */
+    const uint32_t tab = SP_TAB + (uint32_t)(threadIdx.x >> 6) * 8192u;
+    build_aes_tables_at0(lds, t0);
+    __syncthreads();
+    if (nchunks == 0)
+        return;
+    /* build_chunks places the chunks' records contiguously from position 0 */
+    const Chunk last = chunks[nchunks - 1];
+    const uint32_t nrecs = last.first + last.count;
+    const uint32_t waves = gridDim.x * (SPARSE_WG / 64);
+    const uint32_t w0 = __builtin_amdgcn_readfirstlane(blockIdx.x * (SPARSE_WG / 64) + (threadIdx.x >> 6));
+
+    for (uint32_t pos = w0; pos < nrecs; pos += waves) {
+        const ptls_hip_record_t rec = recs_ord[pos];
+        const uint32_t rec_i = order[pos];
+        const uint32_t key = __builtin_amdgcn_readfirstlane(rec.key);
+        const KeySlot *__restrict__ slot = slots + key;
+        const uint32_t *__restrict__ rk = slot->rk;
+        const uint4 *__restrict__ bs = reinterpret_cast<const uint4 *>(basis) + (size_t)key * (NPOW * 128);
+        const int L = (int)__builtin_amdgcn_readfirstlane(rec.len);
+        const int A = (int)__builtin_amdgcn_readfirstlane(rec.aad_len);
+        const int na = (A + 15) >> 4, nc = (L + 15) >> 4;
+        const int N = na + nc + 1;
+        const bool tflag = !OPEN && (rec.flags & 1u) != 0 && L > 0;
+        const uint32_t ttype = (rec.flags >> 8) & 0xffu;
+        const uint8_t *in_p = in + rec.in_off;
+        uint8_t *out_p = out + rec.out_off;
+        const uint8_t *aad_p = aad + rec.aad_off;
+        const uint32_t n0 = slot->iv[0], n1 = slot->iv[1] ^ bswap32((uint32_t)(rec.seq >> 32)),
+                       n2 = slot->iv[2] ^ bswap32((uint32_t)rec.seq);
+        const CtrConst cc = ctr_const(lds, lb_aes, rk, n0, n1, n2);
+        const int iters = (N + 63) >> 6;
+        wave_lds_sync(); /* the previous record's tree reads are done */
+        build_wave_table(lds, tab, bs + 6 * 128, lane); /* H^64 */
+        wave_lds_sync();
+
+        V4 y = V4{0, 0, 0, 0}, ek0 = V4{0, 0, 0, 0};
+        /* elements m and m + 1 of the lane (m + 1 may be past `iters`: inactive), AES blocks interleaved */
+        for (int m = 0; m < iters; m += 2) {
+            Elem e[2];
+            V4 inb[2], ks[2];
+            uint32_t cw[2];
+            int big = 0;
+#pragma unroll
+            for (int b = 0; b < 2; ++b) {
+                e[b] = elem_of(lane + (m + b) * 64, N, na, nc, L);
+                inb[b] = V4{0, 0, 0, 0};
+                if (e[b].is_c) {
+                    const bool tb = tflag && e[b].c == nc - 1; /* the block holding the content-type byte */
+                    inb[b] = load_block<ALIGNED>(in_p + 16 * (size_t)e[b].c, e[b].nbytes - (tb ? 1 : 0));
+                    if (tb)
+                        inb[b] = put_byte(inb[b], e[b].nbytes - 1, ttype);
+                }
+                /* keystream for data block c (counter inc32(J0) + c), E_K(J0) for the length-block lane */
+                cw[b] = e[b].is_c ? bswap32((uint32_t)e[b].c + 2u) : 0x01000000u;
+                ks[b] = V4{n0, n1, n2, cw[b]};
+                big |= (e[b].is_c && e[b].c >= 65534) ? 1 : 0;
+            }
+            if (wave_max(big))
+                aes_encrypt_n<ROUNDS, 2>(lds, lb_aes, rk, ks);
+            else
+                aes_ctr_n<ROUNDS, 2>(lds, lb_aes, rk, cc, cw, ks);
+#pragma unroll
+            for (int b = 0; b < 2; ++b) {
+                const V4 x = finish_elem<OPEN, ALIGNED>(e[b], inb[b], ks[b], aad_p, A, L, out_p, ek0);
+                if (m + b == 0)
+                    y = x; /* 0 * P ^ x */
+                else if (e[b].active)
+                    y = v4xor(gh_mul_nibble(lds, tab, y), x); /* y * H^64 ^ x */
+            }
+        }
+
+        /* lane l's sum times H^(q+1), q = distance of its last element from the end: times H, then a shuffle
+         * tree over q (level d: lanes with q = 0 mod 2d absorb the lane holding q + d, i.e. lane l - d, times H^d) */
+        const int q = (N - 1 - lane) & 63;
+#pragma unroll 1
+        for (int lvl = 0; lvl < 6; ++lvl) {
+            wave_lds_sync();
+            build_wave_table(lds, tab, bs + lvl * 128, lane); /* H^(2^lvl) */
+            wave_lds_sync();
+            if (lvl == 0)
+                y = gh_mul_nibble(lds, tab, y);
+            const int d = 1 << lvl;
+            const int src = (lane - d) & 63;
+            V4 v;
+            v.w0 = __shfl(y.w0, src, 64);
+            v.w1 = __shfl(y.w1, src, 64);
+            v.w2 = __shfl(y.w2, src, 64);
+            v.w3 = __shfl(y.w3, src, 64);
+            const V4 w = gh_mul_nibble(lds, tab, v);
+            if ((q & (2 * d - 1)) == 0)
+                y = v4xor(y, w);
+        }
+        if (q == 0) {
+            const V4 tag = v4xor(y, ek0);
+            if (OPEN) {
+                const V4 rt = load_block<false>(in_p + L, 16);
+                const bool ok = rt.w0 == tag.w0 && rt.w1 == tag.w1 && rt.w2 == tag.w2 && rt.w3 == tag.w3;
+                result[rec_i] = ok ? (uint64_t)L : ~(uint64_t)0;
+            } else {
+                store_full(out_p + L, tag);
+            }
+        }
+        if (!OPEN && supp != nullptr) {
+            /* QUIC header protection after the record (lib/fusion.c:636-650), as in aesgcm_batch_kernel: the
+             * sample may cover the tag written by another lane of this wave */
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            if (lane == 0) {
+                const ptls_hip_supp_t sp = supp[rec_i];
+                if ((sp.flags & PTLS_HIP_SUPP_ENABLE) && sp.hp_key < hp_nslots) {
+                    const V4 sample = load_full(out + sp.sample_off);
+                    const V4 mk = aes_encrypt<ROUNDS>(lds, lb_aes, hp_slots[sp.hp_key].rk, sample);
+                    store_full(mask + sp.mask_off, mk);
+                }
+            }
+        }
+    }
+}
+
+template <int R, bool O>
+static hipError_t launch_sparse_one(unsigned grid, hipStream_t s, const KernelArgs &a, bool aligned)
+{
+    if (aligned)
+        hipLaunchKernelGGL((aesgcm_sparse_kernel<R, O, true>), dim3(grid), dim3(SPARSE_WG), 0, s, a.recs_ord, a.order, a.chunks,
+                           a.nchunks, a.in, a.aad, a.out, a.result, a.slots, a.basis, a.t0, a.supp, a.hp_slots, a.hp_nslots, a.mask);
+    else
+        hipLaunchKernelGGL((aesgcm_sparse_kernel<R, O, false>), dim3(grid), dim3(SPARSE_WG), 0, s, a.recs_ord, a.order, a.chunks,
+                           a.nchunks, a.in, a.aad, a.out, a.result, a.slots, a.basis, a.t0, a.supp, a.hp_slots, a.hp_nslots, a.mask);
+    return hipGetLastError();
+}
+
+int launch_batch_sparse(int rounds, bool open, unsigned grid, void *stream, const KernelArgs &a, bool aligned)
+{
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    hipError_t e;
+    if (rounds == 10)
+        e = open ? launch_sparse_one<10, true>(grid, s, a, aligned) : launch_sparse_one<10, false>(grid, s, a, aligned);
+    else
+        e = open ? launch_sparse_one<14, true>(grid, s, a, aligned) : launch_sparse_one<14, false>(grid, s, a, aligned);
+    return (int)e;
+}
+
+} // namespace ptls_hip

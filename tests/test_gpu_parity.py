@@ -25,7 +25,7 @@ from make_golden import CONFIGS, config_record, sweep_inputs  # noqa: E402
 from oracle_lib import tls_aad  # noqa: E402
 
 UINT64_MAX = (1 << 64) - 1
-LANES = (1, 2, 4, 8, 16)
+LANES = (1, 2, 4, 8, 16, 64)  # 64: the wave-per-record sparse-key kernel
 
 
 def kat_records(golden):
@@ -251,7 +251,7 @@ def test_unaligned_layout(engine, oracle, align):
 
 
 @pytest.mark.parametrize("wg", [512, 768])
-@pytest.mark.parametrize("lanes", [2, 4, 8, 16])
+@pytest.mark.parametrize("lanes", [2, 4, 8, 16, 64])
 def test_key_runs_mixed_lengths(engine, oracle, wg, lanes):
     """BASELINE configs[3] shape in miniature: AES-256, several keys with runs of 150-400 records of
     random 0..6000-byte lengths (the planner reorders each key chunk by length), every workgroup size"""
@@ -306,7 +306,7 @@ def test_differential_random(engine, oracle):
         hb.close()
 
 
-@pytest.mark.parametrize("lanes", [0, 2, 16])
+@pytest.mark.parametrize("lanes", [0, 2, 16, 64])
 @pytest.mark.parametrize("key_len", [16, 32])
 def test_large_records_counter_past_16_bits(engine, oracle, key_len, lanes):
     """records past 2^16 blocks (1 MiB): the counter-mode shortcut holds only while the 32-bit block
@@ -458,22 +458,25 @@ def _supp_array(rows):
     return torch.from_numpy(arr.view(np.uint8)).cuda()
 
 
+@pytest.mark.parametrize("keys", ["3", "per_packet"])
 @pytest.mark.parametrize("path", ["device", "pipeline"])
 @pytest.mark.parametrize("key_len", [16, 32])
-def test_seal_batch_quic_header_protection(engine, oracle, key_len, path):
+def test_seal_batch_quic_header_protection(engine, oracle, key_len, path, keys):
     """QUIC header protection fused into the seal launch (fusion's supp,
     lib/fusion.c:424-428, :636-650).  Packets of 20-1500 B with 16-40 B headers as AAD, 3 AEAD keys,
     2 header-protection keys, samples anywhere in ciphertext || tag (incl. covering the tag), some
     records without HP, some naming an hp key slot outside the keyset (skipped, mask untouched).
-    Ciphertext == oracle, mask == AES-ECB(hp key, sample of the output)."""
+    Ciphertext == oracle, mask == AES-ECB(hp key, sample of the output).  keys="per_packet": every packet
+    has its own AEAD key (one record per key run), which the planner sends to the sparse-key kernel."""
     rng = np.random.default_rng(key_len)
     hp_keys = [rng.integers(0, 256, key_len, dtype=np.uint8).tobytes() for _ in range(2)]
     recs = []
     for i in range(600):
         L = int(rng.integers(20, 1500))
-        key, iv = oracle.gen_key(i * 3 // 600, key_len)
+        key, iv = oracle.gen_key(i * 3 // 600 if keys == "3" else 1000 + i, key_len)
         recs.append((key, iv, 10_000 + i, oracle.stream(900 + i, int(rng.integers(16, 41))), oracle.stream(3000 + i, L)))
     hb = HostBatch(engine, recs)
+    assert (hb.batch.lanes == 64) == (keys == "per_packet")
     hp = ptls_hip.KeySet(engine, key_len, 2)
     hp.set(0, b"".join(hp_keys), None)
     rows, expect = [], []
