@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """bench.py -- device-resident AES-GCM seal+open throughput of the MI355X engine (BASELINE.json metric).
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c4|c5]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c4|c4s|c5]
 
 One step = seal of the whole per-GPU batch followed by open of the sealed batch (the BASELINE metric is
 "seal+open"), inputs already resident in HBM.  Default workload = BASELINE.json configs[1]
@@ -42,6 +42,9 @@ CONFIGS = {  # SURVEY.md §8(d); n = records per GPU
                desc="AES-128-GCM, 4M x 1350 B QUIC records, 13 B AAD, single key (configs[2])"),
     "c4": dict(n=4 << 20, L=None, key_len=32, keys=1 << 16, aad="tls",
                desc="AES-256-GCM, 4M mixed 64 B-16 KiB records, 64K keys (configs[3])"),
+    "c4s": dict(n=1 << 16, L=None, key_len=32, keys=1 << 16, aad="tls",
+                desc="AES-256-GCM, 64K mixed 64 B-16 KiB records, ONE per key over 64K keys (a server batch of one "
+                     "record per connection; configs[3]'s first 64K records; sparse-key kernel)"),
     "c5": dict(n=4 << 20, L=1350, key_len=16, keys=1, aad="quic",
                desc="AES-128-GCM, 32M x 1350 B records sharded 4M per GPU over 8 GPUs (configs[4])"),
 }
@@ -187,7 +190,7 @@ def max_over_ranks(x, world, device):
 
 def golden_check(cfg_name, idx, recs, d_ct):
     """compare sampled sealed records with the digests lib/fusion.c produced (tests/golden/configs.json)"""
-    name = {"c2": "c2_tls16k_aes128", "c3": "c3_quic1350_aes128", "c4": "c4_mixed_aes256_64k",
+    name = {"c2": "c2_tls16k_aes128", "c3": "c3_quic1350_aes128", "c4": "c4_mixed_aes256_64k", "c4s": "c4_mixed_aes256_64k",
             "c5": "c5_quic1350_aes128_8gpu"}[cfg_name]
     with open(os.path.join(ROOT, "tests", "golden", "configs.json")) as f:
         golden = {r["i"]: r["sha256"] for r in json.load(f)["configs"][name]["records"]}
@@ -425,15 +428,16 @@ def main():
         "key_setup_from_secrets_s": None if secrets_s is None else round(secrets_s, 4),
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
-                     "kernel": "aesgcm_batch_kernel (seal)", "algorithmic_bytes_per_launch": alg_bytes},
+                     "kernel": ("aesgcm_sparse_kernel (seal)" if seal_b.lanes == 64 else "aesgcm_batch_kernel (seal)"), "algorithmic_bytes_per_launch": alg_bytes},
         "parity": {"open_all_ok": ok_open, "roundtrip_bytes_equal": ok_pt, "golden_records_checked": golden_n},
     }
     copy_gbs = device_copy_gbs()
     result["roofline"]["measured_copy_gbs"] = copy_gbs
     result["roofline"]["frac_of_measured_copy"] = round(achieved / copy_gbs, 4)
-    ceil = lds_issue_ceiling(cfg["key_len"])
-    ceil["frac"] = round(result["seal_gibps"] / world / ceil["seal_gibps"], 4)
-    result["roofline"]["lds_issue_ceiling"] = ceil
+    if seal_b.lanes != 64:  # the batch kernel's LDS model (the sparse-key kernel is latency-bound)
+        ceil = lds_issue_ceiling(cfg["key_len"])
+        ceil["frac"] = round(result["seal_gibps"] / world / ceil["seal_gibps"], 4)
+        result["roofline"]["lds_issue_ceiling"] = ceil
     if not args.no_e2e and world == 1:  # PCIe path is per GPU; at N > 1 the ranks would share the host links
         result["host_e2e"] = host_e2e(args, cfg, eng, ks, recs, lens, d_pt, d_aad, aad_len)
     tfile = os.path.join(ROOT, "profiles", f"traffic_{args.config}.json")
@@ -443,7 +447,7 @@ def main():
         result["roofline"]["traffic"] = tr.get("hbm_bytes_per_seal_launch")
         result["roofline"]["traffic_source"] = os.path.relpath(tfile, ROOT)
     lfile = os.path.join(ROOT, "profiles", f"lds_{args.config}.json")
-    if os.path.exists(lfile):  # LDS-array occupancy of the same kernel from its PMC pass (the bound that binds)
+    if os.path.exists(lfile) and "lds_issue_ceiling" in result["roofline"]:  # LDS-array occupancy of the same kernel from its PMC pass (the bound that binds)
         with open(lfile) as f:
             result["roofline"]["lds_issue_ceiling"]["lds_array_busy_measured"] = json.load(f)["lds_array_busy_frac"]
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

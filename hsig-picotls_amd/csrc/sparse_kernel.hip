@@ -21,7 +21,15 @@
 
 namespace ptls_hip {
 
-constexpr int SPARSE_WG = 768;
+#ifndef SPARSE_WG
+#define SPARSE_WG 768 /* 12 waves: 64 KiB AES tables + 12 x 8 KiB wave tables = 160 KiB */
+#endif
+#ifndef SPARSE_PE
+#define SPARSE_PE 2 /* GHASH elements (AES blocks) per lane per main-loop iteration */
+#endif
+#ifndef SPARSE_TREE_ATTR
+#define SPARSE_TREE_ATTR __attribute__((noinline)) /* inlined, the tree spills the main loop's registers: c2-shaped -8 %, c3-shaped -30 % */
+#endif
 constexpr uint32_t SP_TAB = 65536; /* per-wave nibble tables, 8 KiB each */
 
 /* T0 / T2 replicated per lane slot at LDS offset 0 (the batch kernel's layout minus its 64 KiB base) */
@@ -45,17 +53,22 @@ __device__ __forceinline__ void wave_lds_sync()
 
 /* the wave's nibble table of P (bp[e] = P * x^e, GCM bit e = byte e/8, bit 7 - e%8) at LDS offset tab,
  * laid out as gh_mul_nibble reads it: entry [p = 8w + j][v] = v at bits 4j..4j+3 of raw word w, times P.
- * Lane l writes position l/2, values 8(l&1) .. 8(l&1) + 7. */
-__device__ __forceinline__ void build_wave_table(uint8_t *lds, uint32_t tab, const uint4 *__restrict__ bp, int lane)
+ * Lane l writes position l/2, values 8(l&1) .. 8(l&1) + 7: load_wave_basis fetches the lane's four basis
+ * vectors (issued early to hide their latency), store_wave_table writes the eight combinations. */
+__device__ __forceinline__ void load_wave_basis(const uint4 *__restrict__ bp, int lane, V4 (&b)[4])
 {
     const int p = lane >> 1, w = p >> 3, j = p & 7;
-    V4 b[4];
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
         const int u = 4 * j + t; /* bit u of little-endian word w = raw byte 4w + u/8, bit u%8 */
         const uint4 v = bp[8 * (4 * w + (u >> 3)) + 7 - (u & 7)];
         b[t] = V4{v.x, v.y, v.z, v.w};
     }
+}
+
+__device__ __forceinline__ void store_wave_table(uint8_t *lds, uint32_t tab, const V4 (&b)[4], int lane)
+{
+    const int p = lane >> 1;
     const V4 hi = (lane & 1) ? b[3] : V4{0, 0, 0, 0};
     const uint32_t row = tab + (uint32_t)p * 256u + (uint32_t)(lane & 1) * 128u;
     const V4 b01 = v4xor(b[0], b[1]);
@@ -65,6 +78,35 @@ __device__ __forceinline__ void build_wave_table(uint8_t *lds, uint32_t tab, con
         const V4 e = (k & 4) ? v4xor3(hi, lo, b[2]) : v4xor(hi, lo);
         lds128_store(lds, row + (uint32_t)k * 16u, e);
     }
+}
+
+/* lane's GHASH sum times H^(q+1), summed over the wave into the lane with q == 0: times H, then a shuffle
+ * tree over q (level d: lanes with q = 0 mod 2d absorb the lane holding q + d, i.e. lane l - d, times H^d) */
+__device__ SPARSE_TREE_ATTR V4 ghash_tree(uint8_t *lds, uint32_t tab, const uint4 *__restrict__ bs, int lane, int q, V4 y)
+{
+    V4 b[4];
+    load_wave_basis(bs, lane, b); /* H */
+#pragma unroll 1
+    for (int lvl = 0; lvl < 6; ++lvl) {
+        wave_lds_sync();
+        store_wave_table(lds, tab, b, lane); /* H^(2^lvl) */
+        wave_lds_sync();
+        if (lvl < 5)
+            load_wave_basis(bs + (lvl + 1) * 128, lane, b); /* the next level's, in flight during this one */
+        if (lvl == 0)
+            y = gh_mul_nibble(lds, tab, y);
+        const int d = 1 << lvl;
+        const int src = (lane - d) & 63;
+        V4 v;
+        v.w0 = __shfl(y.w0, src, 64);
+        v.w1 = __shfl(y.w1, src, 64);
+        v.w2 = __shfl(y.w2, src, 64);
+        v.w3 = __shfl(y.w3, src, 64);
+        const V4 w = gh_mul_nibble(lds, tab, v);
+        if ((q & (2 * d - 1)) == 0)
+            y = v4xor(y, w);
+    }
+    return y;
 }
 
 template <int ROUNDS, bool OPEN, bool ALIGNED>
@@ -111,18 +153,22 @@ __global__ void __launch_bounds__(SPARSE_WG)
         const CtrConst cc = ctr_const(lds, lb_aes, rk, n0, n1, n2);
         const int iters = (N + 63) >> 6;
         wave_lds_sync(); /* the previous record's tree reads are done */
-        build_wave_table(lds, tab, bs + 6 * 128, lane); /* H^64 */
+        {
+            V4 b[4];
+            load_wave_basis(bs + 6 * 128, lane, b); /* H^64 */
+            store_wave_table(lds, tab, b, lane);
+        }
         wave_lds_sync();
 
         V4 y = V4{0, 0, 0, 0}, ek0 = V4{0, 0, 0, 0};
-        /* elements m and m + 1 of the lane (m + 1 may be past `iters`: inactive), AES blocks interleaved */
-        for (int m = 0; m < iters; m += 2) {
-            Elem e[2];
-            V4 inb[2], ks[2];
-            uint32_t cw[2];
+        /* elements m .. m + SPARSE_PE - 1 of the lane (past `iters`: inactive), their AES blocks interleaved */
+        for (int m = 0; m < iters; m += SPARSE_PE) {
+            Elem e[SPARSE_PE];
+            V4 inb[SPARSE_PE], ks[SPARSE_PE];
+            uint32_t cw[SPARSE_PE];
             int big = 0;
 #pragma unroll
-            for (int b = 0; b < 2; ++b) {
+            for (int b = 0; b < SPARSE_PE; ++b) {
                 e[b] = elem_of(lane + (m + b) * 64, N, na, nc, L);
                 inb[b] = V4{0, 0, 0, 0};
                 if (e[b].is_c) {
@@ -137,11 +183,11 @@ __global__ void __launch_bounds__(SPARSE_WG)
                 big |= (e[b].is_c && e[b].c >= 65534) ? 1 : 0;
             }
             if (wave_max(big))
-                aes_encrypt_n<ROUNDS, 2>(lds, lb_aes, rk, ks);
+                aes_encrypt_n<ROUNDS, SPARSE_PE>(lds, lb_aes, rk, ks);
             else
-                aes_ctr_n<ROUNDS, 2>(lds, lb_aes, rk, cc, cw, ks);
+                aes_ctr_n<ROUNDS, SPARSE_PE>(lds, lb_aes, rk, cc, cw, ks);
 #pragma unroll
-            for (int b = 0; b < 2; ++b) {
+            for (int b = 0; b < SPARSE_PE; ++b) {
                 const V4 x = finish_elem<OPEN, ALIGNED>(e[b], inb[b], ks[b], aad_p, A, L, out_p, ek0);
                 if (m + b == 0)
                     y = x; /* 0 * P ^ x */
@@ -152,25 +198,9 @@ __global__ void __launch_bounds__(SPARSE_WG)
 
         /* lane l's sum times H^(q+1), q = distance of its last element from the end: times H, then a shuffle
          * tree over q (level d: lanes with q = 0 mod 2d absorb the lane holding q + d, i.e. lane l - d, times H^d) */
+        /* q = distance of the lane's last element from the end of the GHASH input */
         const int q = (N - 1 - lane) & 63;
-#pragma unroll 1
-        for (int lvl = 0; lvl < 6; ++lvl) {
-            wave_lds_sync();
-            build_wave_table(lds, tab, bs + lvl * 128, lane); /* H^(2^lvl) */
-            wave_lds_sync();
-            if (lvl == 0)
-                y = gh_mul_nibble(lds, tab, y);
-            const int d = 1 << lvl;
-            const int src = (lane - d) & 63;
-            V4 v;
-            v.w0 = __shfl(y.w0, src, 64);
-            v.w1 = __shfl(y.w1, src, 64);
-            v.w2 = __shfl(y.w2, src, 64);
-            v.w3 = __shfl(y.w3, src, 64);
-            const V4 w = gh_mul_nibble(lds, tab, v);
-            if ((q & (2 * d - 1)) == 0)
-                y = v4xor(y, w);
-        }
+        y = ghash_tree(lds, tab, bs, lane, q, y);
         if (q == 0) {
             const V4 tag = v4xor(y, ek0);
             if (OPEN) {

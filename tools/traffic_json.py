@@ -10,7 +10,7 @@ out, cfg = sys.argv[1], sys.argv[2]
 
 def per_launch(counter):
     f = glob.glob(f"{out}/pmc_{counter}/**/run_counter_collection.csv", recursive=True)
-    rows = [r for r in csv.DictReader(open(f[0])) if r["Kernel_Name"].startswith("aesgcm_batch_kernel")]
+    rows = [r for r in csv.DictReader(open(f[0])) if r["Kernel_Name"].startswith(("aesgcm_batch_kernel", "aesgcm_sparse_kernel"))]
     ids = sorted({int(r["Dispatch_Id"]) for r in rows})
     by = {}
     for r in rows:
@@ -36,7 +36,7 @@ stats = glob.glob(f"{out}/trace/**/run_kernel_stats.csv", recursive=True)
 avg_ns = None
 if stats:
     for r in csv.DictReader(open(stats[0])):
-        if r["Name"].startswith("aesgcm_batch_kernel"):
+        if r["Name"].startswith(("aesgcm_batch_kernel", "aesgcm_sparse_kernel")):
             avg_ns = float(r["AverageNs"])
 print(json.dumps({
     "config": cfg,
