@@ -24,6 +24,9 @@ namespace ptls_hip {
 #ifndef SPARSE_WG
 #define SPARSE_WG 768 /* 12 waves: 64 KiB AES tables + 12 x 8 KiB wave tables = 160 KiB */
 #endif
+#ifndef SPARSE_ABLATE
+#define SPARSE_ABLATE 0 /* timing ablation only (wrong output): 1 = no tree, 2 = no main-loop multiply, 3 = no H^64 table build */
+#endif
 #ifndef SPARSE_PE
 #define SPARSE_PE 2 /* GHASH elements (AES blocks) per lane per main-loop iteration */
 #endif
@@ -153,7 +156,7 @@ __global__ void __launch_bounds__(SPARSE_WG)
         const CtrConst cc = ctr_const(lds, lb_aes, rk, n0, n1, n2);
         const int iters = (N + 63) >> 6;
         wave_lds_sync(); /* the previous record's tree reads are done */
-        {
+        if (SPARSE_ABLATE != 3) {
             V4 b[4];
             load_wave_basis(bs + 6 * 128, lane, b); /* H^64 */
             store_wave_table(lds, tab, b, lane);
@@ -191,7 +194,7 @@ __global__ void __launch_bounds__(SPARSE_WG)
                 const V4 x = finish_elem<OPEN, ALIGNED>(e[b], inb[b], ks[b], aad_p, A, L, out_p, ek0);
                 if (m + b == 0)
                     y = x; /* 0 * P ^ x */
-                else if (e[b].active)
+                else if (SPARSE_ABLATE != 2 && e[b].active)
                     y = v4xor(gh_mul_nibble(lds, tab, y), x); /* y * H^64 ^ x */
             }
         }
@@ -200,7 +203,8 @@ __global__ void __launch_bounds__(SPARSE_WG)
          * tree over q (level d: lanes with q = 0 mod 2d absorb the lane holding q + d, i.e. lane l - d, times H^d) */
         /* q = distance of the lane's last element from the end of the GHASH input */
         const int q = (N - 1 - lane) & 63;
-        y = ghash_tree(lds, tab, bs, lane, q, y);
+        if (SPARSE_ABLATE != 1)
+            y = ghash_tree(lds, tab, bs, lane, q, y);
         if (q == 0) {
             const V4 tag = v4xor(y, ek0);
             if (OPEN) {
