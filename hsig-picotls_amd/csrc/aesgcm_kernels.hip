@@ -193,7 +193,7 @@ __global__ void keysetup_kernel(KeySlot *slots, uint32_t *basis, const uint8_t *
     h.w3 = (uint32_t)s[12] | ((uint32_t)s[13] << 8) | ((uint32_t)s[14] << 16) | ((uint32_t)s[15] << 24);
 
     U128 p = u128_from_raw(h);
-    uint4 *bs = reinterpret_cast<uint4 *>(basis) + (size_t)(first + k) * NPOW * 128;
+    uint4 *bs = reinterpret_cast<uint4 *>(basis) + (size_t)(first + k) * BASIS_VECS;
     for (int t = 0; t < NPOW; ++t) {
         if (t != 0)
             p = gf_mul_slow(p, p);
@@ -208,6 +208,14 @@ __global__ void keysetup_kernel(KeySlot *slots, uint32_t *basis, const uint8_t *
             bs[t * 128 + e] = make_uint4(br.w0, br.w1, br.w2, br.w3);
             b = gf_mulx(b);
         }
+    }
+    /* H^1 .. H^64 (the sparse kernel's lane q multiplies its partial sum by H^(q+1)) */
+    const U128 hh = u128_from_raw(h);
+    U128 pk = hh;
+    for (int q = 0; q < LANE_POWS; ++q) {
+        const V4 pr = u128_to_raw(pk);
+        bs[NPOW * 128 + q] = make_uint4(pr.w0, pr.w1, pr.w2, pr.w3);
+        pk = gf_mul_slow(pk, hh);
     }
 }
 

@@ -893,7 +893,7 @@ __global__ void __launch_bounds__(WGT)
         const Chunk ch = chunks[ci];
         if (SPLIT_PROBE != 1 && ch.key != cur_key) {
             __syncthreads();
-            build_ghash_tables(lds, basis + (size_t)ch.key * (NPOW * 128 * 4), LOG2G);
+            build_ghash_tables(lds, basis + (size_t)ch.key * (BASIS_VECS * 4), LOG2G);
             if (DYN && threadIdx.x == 0)
                 *task_ctr = 0;
             __syncthreads();

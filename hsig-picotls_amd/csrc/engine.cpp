@@ -217,7 +217,7 @@ extern "C" int ptls_hip_engine_cu_count(ptls_hip_engine_t *e)
 /* keysets                                                                                         */
 /* ---------------------------------------------------------------------------------------------- */
 
-static const size_t BASIS_WORDS_PER_SLOT = (size_t)NPOW * 128 * 4;
+static const size_t BASIS_WORDS_PER_SLOT = (size_t)BASIS_VECS * 4;
 
 extern "C" ptls_hip_keyset_t *ptls_hip_keyset_new(ptls_hip_engine_t *eng, size_t key_size, size_t nslots)
 {

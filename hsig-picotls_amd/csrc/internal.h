@@ -3,7 +3,7 @@
  *
  * HBM layout:
  *   key slots    KeySlot[nslots]             512 B each: round keys, static IV, H powers
- *   GHASH basis  uint4[nslots][NPOW][128]    14 KiB per slot: P * x^e for P in {H, H^2, ..., H^64}
+ *   GHASH basis  uint4[nslots][BASIS_VECS]   15 KiB per slot: P * x^e for P in {H, H^2, ..., H^64}, then H^1..H^64
  *   records      ptls_hip_record_t[n]        48 B descriptors (caller's order)
  *   chunks       Chunk[nchunks]              runs of <= CHUNK_RECS records sharing one key slot
  *   payloads     caller's buffers, untouched layout (in / aad / out)
@@ -17,6 +17,9 @@
 namespace ptls_hip {
 
 constexpr int NPOW = 7;          /* H^1, H^2, H^4, H^8, H^16 (batch kernel tables), H^32, H^64 (sparse kernel) */
+/* GHASH basis slot: NPOW x 128 vectors P * x^e, then H^1 .. H^64 (the sparse kernel's per-lane final powers) */
+constexpr int LANE_POWS = 64;
+constexpr int BASIS_VECS = NPOW * 128 + LANE_POWS; /* uint4 per key slot (15 KiB) */
 constexpr int MAX_LANES = 16;    /* lanes per record (G) of the batch kernel: 1, 2, 4, 8, 16 */
 constexpr int SPARSE_LANES = 64; /* "lanes" value of the wave-per-record kernel (sparse_kernel.hip) */
 /* the planner picks that kernel when a batch's key runs hold fewer records than this on average */

@@ -25,13 +25,10 @@ namespace ptls_hip {
 #define SPARSE_WG 768 /* 12 waves: 64 KiB AES tables + 12 x 8 KiB wave tables = 160 KiB */
 #endif
 #ifndef SPARSE_ABLATE
-#define SPARSE_ABLATE 0 /* timing ablation only (wrong output): 1 = no tree, 2 = no main-loop multiply, 3 = no H^64 table build */
+#define SPARSE_ABLATE 0 /* timing ablation only (wrong output): 1 = no final lane combination, 2 = no main-loop multiply, 3 = no H^64 table build */
 #endif
 #ifndef SPARSE_PE
 #define SPARSE_PE 2 /* GHASH elements (AES blocks) per lane per main-loop iteration */
-#endif
-#ifndef SPARSE_TREE_ATTR
-#define SPARSE_TREE_ATTR __attribute__((noinline)) /* inlined, the tree spills the main loop's registers: c2-shaped -8 %, c3-shaped -30 % */
 #endif
 constexpr uint32_t SP_TAB = 65536; /* per-wave nibble tables, 8 KiB each */
 
@@ -83,33 +80,43 @@ __device__ __forceinline__ void store_wave_table(uint8_t *lds, uint32_t tab, con
     }
 }
 
-/* lane's GHASH sum times H^(q+1), summed over the wave into the lane with q == 0: times H, then a shuffle
- * tree over q (level d: lanes with q = 0 mod 2d absorb the lane holding q + d, i.e. lane l - d, times H^d) */
-__device__ SPARSE_TREE_ATTR V4 ghash_tree(uint8_t *lds, uint32_t tab, const uint4 *__restrict__ bs, int lane, int q, V4 y)
+/* x * y in GF(2^128), GCM bit order (SP 800-38D Algorithm 1), both operands per lane, on the VALU: 128 steps
+ * of "Z ^= V if bit i of x; V = V * x^1" with 32-bit big-endian words (11 VALU per step) */
+__device__ __forceinline__ V4 gf_mul_valu(V4 xr, V4 yr)
 {
-    V4 b[4];
-    load_wave_basis(bs, lane, b); /* H */
-#pragma unroll 1
-    for (int lvl = 0; lvl < 6; ++lvl) {
-        wave_lds_sync();
-        store_wave_table(lds, tab, b, lane); /* H^(2^lvl) */
-        wave_lds_sync();
-        if (lvl < 5)
-            load_wave_basis(bs + (lvl + 1) * 128, lane, b); /* the next level's, in flight during this one */
-        if (lvl == 0)
-            y = gh_mul_nibble(lds, tab, y);
-        const int d = 1 << lvl;
-        const int src = (lane - d) & 63;
-        V4 v;
-        v.w0 = __shfl(y.w0, src, 64);
-        v.w1 = __shfl(y.w1, src, 64);
-        v.w2 = __shfl(y.w2, src, 64);
-        v.w3 = __shfl(y.w3, src, 64);
-        const V4 w = gh_mul_nibble(lds, tab, v);
-        if ((q & (2 * d - 1)) == 0)
-            y = v4xor(y, w);
+    const uint32_t x[4] = {bswap32(xr.w0), bswap32(xr.w1), bswap32(xr.w2), bswap32(xr.w3)};
+    uint32_t v0 = bswap32(yr.w0), v1 = bswap32(yr.w1), v2 = bswap32(yr.w2), v3 = bswap32(yr.w3);
+    uint32_t z0 = 0, z1 = 0, z2 = 0, z3 = 0;
+#pragma unroll
+    for (int i = 0; i < 128; ++i) {
+        const uint32_t m = (uint32_t)__builtin_amdgcn_sbfe((int)x[i >> 5], 31u - (uint32_t)(i & 31), 1u); /* 0 or ~0 */
+        z0 = __builtin_amdgcn_bitop3_b32(z0, m, v0, 0x78); /* z ^ (m & v) */
+        z1 = __builtin_amdgcn_bitop3_b32(z1, m, v1, 0x78);
+        z2 = __builtin_amdgcn_bitop3_b32(z2, m, v2, 0x78);
+        z3 = __builtin_amdgcn_bitop3_b32(z3, m, v3, 0x78);
+        const uint32_t c = (uint32_t)__builtin_amdgcn_sbfe((int)v3, 0u, 1u); /* the bit shifted out */
+        v3 = __builtin_amdgcn_alignbit(v2, v3, 1);
+        v2 = __builtin_amdgcn_alignbit(v1, v2, 1);
+        v1 = __builtin_amdgcn_alignbit(v0, v1, 1);
+        v0 = (v0 >> 1) ^ (c & 0xe1000000u); /* R = 11100001 || 0^120 */
     }
-    return y;
+    return V4{bswap32(z0), bswap32(z1), bswap32(z2), bswap32(z3)};
+}
+
+/* sum over the wave of (lane's GHASH sum) * H^(q+1): one VALU multiply by the lane's own power (keysetup's
+ * H^1..H^64 table), then an XOR butterfly; every lane ends with the total */
+__device__ __forceinline__ V4 ghash_combine(const uint4 *__restrict__ bs, int q, V4 y)
+{
+    const uint4 hp = bs[NPOW * 128 + q]; /* H^(q+1) */
+    V4 z = gf_mul_valu(y, V4{hp.x, hp.y, hp.z, hp.w});
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        z.w0 ^= __shfl_xor(z.w0, o, 64);
+        z.w1 ^= __shfl_xor(z.w1, o, 64);
+        z.w2 ^= __shfl_xor(z.w2, o, 64);
+        z.w3 ^= __shfl_xor(z.w3, o, 64);
+    }
+    return z;
 }
 
 template <int ROUNDS, bool OPEN, bool ALIGNED>
@@ -141,7 +148,7 @@ __global__ void __launch_bounds__(SPARSE_WG)
         const uint32_t key = __builtin_amdgcn_readfirstlane(rec.key);
         const KeySlot *__restrict__ slot = slots + key;
         const uint32_t *__restrict__ rk = slot->rk;
-        const uint4 *__restrict__ bs = reinterpret_cast<const uint4 *>(basis) + (size_t)key * (NPOW * 128);
+        const uint4 *__restrict__ bs = reinterpret_cast<const uint4 *>(basis) + (size_t)key * BASIS_VECS;
         const int L = (int)__builtin_amdgcn_readfirstlane(rec.len);
         const int A = (int)__builtin_amdgcn_readfirstlane(rec.aad_len);
         const int na = (A + 15) >> 4, nc = (L + 15) >> 4;
@@ -204,7 +211,7 @@ __global__ void __launch_bounds__(SPARSE_WG)
         /* q = distance of the lane's last element from the end of the GHASH input */
         const int q = (N - 1 - lane) & 63;
         if (SPARSE_ABLATE != 1)
-            y = ghash_tree(lds, tab, bs, lane, q, y);
+            y = ghash_combine(bs, q, y);
         if (q == 0) {
             const V4 tag = v4xor(y, ek0);
             if (OPEN) {
