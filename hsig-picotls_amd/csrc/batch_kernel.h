@@ -62,6 +62,11 @@ __host__ __device__ constexpr uint32_t lds_bytes(int log2g)
 #ifndef DYN_DEAL
 #define DYN_DEAL 1 /* waves draw tasks from a workgroup counter in LDS instead of a fixed per-chunk deal: c2 +3 %, c3 +5 %, c4 +5 % */
 #endif
+#ifndef VALU_TREE
+#define VALU_TREE 0 /* 1: combine a record's G partial sums by one VALU multiply per lane (H^(q+1) from the key slot's
+                       power table) and an XOR butterfly instead of the log2(G)-level LDS nibble-table tree.
+                       Parity-green, measured c2 / c4 equal and c3 -4 %; the sparse kernel uses it. */
+#endif
 #ifndef PURE_BLOCKS
 #define PURE_BLOCKS 2 /* data blocks per lane per iteration of the branch-free loop */
 #endif
@@ -653,6 +658,29 @@ __device__ __forceinline__ V4 gh_mul_nibble(const uint8_t *lds, uint32_t table, 
     return acc;
 }
 
+/* x * y in GF(2^128), GCM bit order (SP 800-38D Algorithm 1), both operands per lane, on the VALU: 128 steps
+ * of "Z ^= V if bit i of x; V = V * x^1" with 32-bit big-endian words (11 VALU per step) */
+__device__ __forceinline__ V4 gf_mul_valu(V4 xr, V4 yr)
+{
+    const uint32_t x[4] = {bswap32(xr.w0), bswap32(xr.w1), bswap32(xr.w2), bswap32(xr.w3)};
+    uint32_t v0 = bswap32(yr.w0), v1 = bswap32(yr.w1), v2 = bswap32(yr.w2), v3 = bswap32(yr.w3);
+    uint32_t z0 = 0, z1 = 0, z2 = 0, z3 = 0;
+#pragma unroll
+    for (int i = 0; i < 128; ++i) {
+        const uint32_t m = (uint32_t)__builtin_amdgcn_sbfe((int)x[i >> 5], 31u - (uint32_t)(i & 31), 1u); /* 0 or ~0 */
+        z0 = __builtin_amdgcn_bitop3_b32(z0, m, v0, 0x78); /* z ^ (m & v) */
+        z1 = __builtin_amdgcn_bitop3_b32(z1, m, v1, 0x78);
+        z2 = __builtin_amdgcn_bitop3_b32(z2, m, v2, 0x78);
+        z3 = __builtin_amdgcn_bitop3_b32(z3, m, v3, 0x78);
+        const uint32_t c = (uint32_t)__builtin_amdgcn_sbfe((int)v3, 0u, 1u); /* the bit shifted out */
+        v3 = __builtin_amdgcn_alignbit(v2, v3, 1);
+        v2 = __builtin_amdgcn_alignbit(v1, v2, 1);
+        v1 = __builtin_amdgcn_alignbit(v0, v1, 1);
+        v0 = (v0 >> 1) ^ (c & 0xe1000000u); /* R = 11100001 || 0^120 */
+    }
+    return V4{bswap32(z0), bswap32(z1), bswap32(z2), bswap32(z3)};
+}
+
 /* ---------------- table construction in LDS ---------------- */
 
 __device__ __forceinline__ V4 ld_basis(const uint32_t *b, int e)
@@ -1136,6 +1164,20 @@ __global__ void __launch_bounds__(WGT)
             /* combine the G partial sums of each record: position q = distance of a lane's last element
              * from the end of the GHASH input; sum_q y_q * H^(q+1) by a shuffle tree */
             const int q = (nc - r) & (G - 1);
+#if VALU_TREE
+            V4 s = V4{0, 0, 0, 0};
+            if (SPLIT_PROBE != 1) {
+                const uint4 hp = reinterpret_cast<const uint4 *>(basis)[(size_t)ch.key * BASIS_VECS + NPOW * 128 + q]; /* H^(q+1) */
+                s = gf_mul_valu(y, V4{hp.x, hp.y, hp.z, hp.w});
+#pragma unroll
+                for (int o = G / 2; o > 0; o >>= 1) {
+                    s.w0 ^= __shfl_xor(s.w0, o, 64);
+                    s.w1 ^= __shfl_xor(s.w1, o, 64);
+                    s.w2 ^= __shfl_xor(s.w2, o, 64);
+                    s.w3 ^= __shfl_xor(s.w3, o, 64);
+                }
+            }
+#else
 #pragma unroll
             for (int lvl = 0; lvl < (SPLIT_PROBE == 1 ? 0 : LOG2G); ++lvl) {
                 const int d = 1 << lvl;
@@ -1155,8 +1197,11 @@ __global__ void __launch_bounds__(WGT)
                 if ((q & (2 * d - 1)) == 0)
                     y = v4xor(y, w);
             }
+#endif
             if (valid && q == 0) {
+#if !VALU_TREE
                 const V4 s = gh_mul_nibble(lds, LDS_GTREE, y); /* * H */
+#endif
                 const V4 tag = v4xor(s, ek0);
                 if (OPEN) {
                     const V4 rt = load_full(in_p + L);

@@ -80,29 +80,6 @@ __device__ __forceinline__ void store_wave_table(uint8_t *lds, uint32_t tab, con
     }
 }
 
-/* x * y in GF(2^128), GCM bit order (SP 800-38D Algorithm 1), both operands per lane, on the VALU: 128 steps
- * of "Z ^= V if bit i of x; V = V * x^1" with 32-bit big-endian words (11 VALU per step) */
-__device__ __forceinline__ V4 gf_mul_valu(V4 xr, V4 yr)
-{
-    const uint32_t x[4] = {bswap32(xr.w0), bswap32(xr.w1), bswap32(xr.w2), bswap32(xr.w3)};
-    uint32_t v0 = bswap32(yr.w0), v1 = bswap32(yr.w1), v2 = bswap32(yr.w2), v3 = bswap32(yr.w3);
-    uint32_t z0 = 0, z1 = 0, z2 = 0, z3 = 0;
-#pragma unroll
-    for (int i = 0; i < 128; ++i) {
-        const uint32_t m = (uint32_t)__builtin_amdgcn_sbfe((int)x[i >> 5], 31u - (uint32_t)(i & 31), 1u); /* 0 or ~0 */
-        z0 = __builtin_amdgcn_bitop3_b32(z0, m, v0, 0x78); /* z ^ (m & v) */
-        z1 = __builtin_amdgcn_bitop3_b32(z1, m, v1, 0x78);
-        z2 = __builtin_amdgcn_bitop3_b32(z2, m, v2, 0x78);
-        z3 = __builtin_amdgcn_bitop3_b32(z3, m, v3, 0x78);
-        const uint32_t c = (uint32_t)__builtin_amdgcn_sbfe((int)v3, 0u, 1u); /* the bit shifted out */
-        v3 = __builtin_amdgcn_alignbit(v2, v3, 1);
-        v2 = __builtin_amdgcn_alignbit(v1, v2, 1);
-        v1 = __builtin_amdgcn_alignbit(v0, v1, 1);
-        v0 = (v0 >> 1) ^ (c & 0xe1000000u); /* R = 11100001 || 0^120 */
-    }
-    return V4{bswap32(z0), bswap32(z1), bswap32(z2), bswap32(z3)};
-}
-
 /* sum over the wave of (lane's GHASH sum) * H^(q+1): one VALU multiply by the lane's own power (keysetup's
  * H^1..H^64 table), then an XOR butterfly; every lane ends with the total */
 __device__ __forceinline__ V4 ghash_combine(const uint4 *__restrict__ bs, int q, V4 y)
