@@ -140,7 +140,7 @@ __global__ void __launch_bounds__(SPARSE_WG)
         const CtrConst cc = ctr_const(lds, lb_aes, rk, n0, n1, n2);
         const int iters = (N + 63) >> 6;
         wave_lds_sync(); /* the previous record's tree reads are done */
-        if (SPARSE_ABLATE != 3) {
+        if (SPARSE_ABLATE != 3 && iters > 1) { /* N <= 64: one element per lane, no Horner step */
             V4 b[4];
             load_wave_basis(bs + 6 * 128, lane, b); /* H^64 */
             store_wave_table(lds, tab, b, lane);
