@@ -471,6 +471,10 @@ static void build_chunks(const ptls_hip_record_t *recs, size_t n, int lanes, uns
         all_aligned = all_aligned && (c.flags & 1u);
         ch.push_back(c);
     }
+    /* the sparse kernel's waves take records grid-stride: in decreasing length over the whole batch, every
+     * wave gets a similar share of bytes (the chunks then only give it the record count) */
+    if (lanes == SPARSE_LANES)
+        std::stable_sort(order.begin(), order.end(), [&](uint32_t x, uint32_t y) { return recs[x].len > recs[y].len; });
 }
 
 static int plan_chunks(ptls_hip_batch_t *b)
