@@ -3,13 +3,17 @@
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c4|c4s|c5]
 
+--gpus N > 1 without a launcher starts N rank processes itself (torch.distributed.run on 127.0.0.1, before
+any GPU call); under a launcher WORLD_SIZE must equal N.
+
 One step = seal of the whole per-GPU batch followed by open of the sealed batch (the BASELINE metric is
 "seal+open"), inputs already resident in HBM.  Default workload = BASELINE.json configs[1]
 ("c2": 1M x 16 KiB TLS records, AES-128-GCM, one key) on every GPU: records are sharded by range,
 each rank owns its own 1M records (weak scaling), no collective touches the data path; ranks only
 meet at the barriers and the max-over-ranks of the timed region.
 
-Rank 0 prints ONE JSON line.  value = whole-job GiB/s = sum over ranks of 2 * sum(L) per step / time.
+Rank 0 prints ONE JSON line.  value = whole-job GiB/s = sum over ranks of 2 * sum(L) per step / the slowest
+rank's time; per_rank lists every rank's own rate.
 Extra fields: roofline (seal kernel vs the 8 TB/s HBM peak), cpu_baseline (lib/fusion.c on this host's
 cores, oracle/_ref), parity (sampled records vs the golden digests of lib/fusion.c + full open check).
 """
@@ -114,25 +118,56 @@ def make_keys(cfg):
     return s[:, :kl].tobytes(), s[:, kl:kl + 12].tobytes()
 
 
-def cpu_baseline(cfg_name, cfg, budget_s=4.0):
-    """lib/fusion.c (oracle/_ref, built unmodified from the reference) on this host's cores, over a bounded
-    sample of the same workload shape: distinct record buffers, same AAD form, one context per thread."""
-    import ctypes
-    from oracle_lib import REF_SO, Ref, ORACLE_SO
-    L = cfg["L"] or 8224
-    nrec = max(64, min(4096, (64 << 20) // max(L, 1)))
-    stride = (L + 16 + 63) // 64 * 64
-    idx = np.arange(nrec, dtype=np.uint64)
-    data = np.zeros((nrec, stride), dtype=np.uint8)
-    data[:, :L] = stream_bytes(np.uint64(SEED_DATA) ^ idx, L)
-    aad_len = 5 if cfg["aad"] == "tls" else 13
-    aad = build_aad(cfg, idx, np.full(nrec, L, dtype=np.uint64)).reshape(nrec, 16)[:, :aad_len].copy()
-    key, iv = (b"\x11" * cfg["key_len"]), b"\x22" * 12
+def cpu_share():
+    """(cpus to use, cpus in the affinity mask, cgroup CPU quota or None): every CPU this process may run on,
+    bounded by the container's CPU quota (a GPU box shows the whole machine in its mask but grants a share)"""
     try:
-        ncpu = len(os.sched_getaffinity(0))
+        aff = sorted(os.sched_getaffinity(0))
     except AttributeError:
-        ncpu = os.cpu_count() or 1
-    threads = max(1, min(16, ncpu))
+        aff = list(range(os.cpu_count() or 1))
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:  # cgroup v2: "<quota> <period>" or "max <period>"
+            q, per = f.read().split()
+            if q != "max":
+                quota = int(q) / int(per)
+    except (OSError, ValueError):
+        try:
+            with open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us") as f1, open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as f2:
+                q, per = int(f1.read()), int(f2.read())
+                if q > 0:
+                    quota = q / per
+        except (OSError, ValueError):
+            pass
+    n = len(aff) if quota is None else max(1, min(len(aff), int(quota + 1e-9)))
+    return aff[:n], len(aff), quota
+
+
+def _steady(run_rep, min_reps=5, min_s=3.0, max_s=12.0, tol=0.10):
+    """repeat run_rep() (-> GiB/s of one rep) until the last min_reps agree within tol of their median, or max_s"""
+    rates, t0 = [], time.time()
+    while True:
+        rates.append(run_rep())
+        last = rates[-min_reps:]
+        spread = (max(last) - min(last)) / float(np.median(last))
+        el = time.time() - t0
+        if len(rates) >= min_reps and ((spread <= tol and el >= min_s) or el >= max_s):
+            return dict(median=round(float(np.median(last)), 3), min=round(min(last), 3), max=round(max(last), 3),
+                        spread=round(spread, 4), reps=len(rates), reps_used=len(last))
+
+
+def cpu_baseline(cfg_name, cfg):
+    """lib/fusion.c (oracle/_ref, built unmodified from the reference) on this host's cores: distinct record
+    buffers of the config's shape (about 1 GiB, larger than the CPU caches, like the GPU's HBM-resident batch),
+    the config's AAD form, one ptls_aead_context_t per pinned thread.  Each rep = one seal
+    pass + one open pass over the sample (repeated inside the rep to last >= 0.3 s); reps repeat until five
+    agree within 10 %.  Reported: median of those five, min / max, for 1 thread and for every CPU available."""
+    import ctypes
+    from oracle_lib import Ref, ORACLE_SO
+    L = cfg["L"] or 8224
+    nrec = max(64, (1 << 30) // L)
+    stride = (L + 16 + 63) // 64 * 64
+    aad_len = 5 if cfg["aad"] == "tls" else 13
     if not Ref.available:
         o = ctypes.CDLL(ORACLE_SO)
         o.oracle_bench_seal.restype = ctypes.c_double
@@ -141,28 +176,43 @@ def cpu_baseline(cfg_name, cfg, budget_s=4.0):
         t = o.oracle_bench_seal(cfg["key_len"], n, L, 1)
         return dict(value=n * L / t / GIB, unit="GiB/s (seal only)", cores=1, kind="port",
                     sample=f"{n} x {L} B records, oracle C port, single thread")
+    rng = np.random.default_rng(2024)
+    data = np.frombuffer(rng.bytes(nrec * stride), dtype=np.uint8).reshape(nrec, stride).copy()
+    idx = np.arange(nrec, dtype=np.uint64)
+    aad = build_aad(cfg, idx, np.full(nrec, L, dtype=np.uint64)).reshape(nrec, 16)[:, :aad_len].copy()
+    key, iv = (b"\x11" * cfg["key_len"]), b"\x22" * 12
+    cpus, n_aff, quota = cpu_share()
+    threads = len(cpus)
     ref = Ref()
     ct = np.zeros_like(data)
     pt = np.zeros_like(data)
-    cpus = sorted(os.sched_getaffinity(0))[:threads] if hasattr(os, "sched_getaffinity") else None
 
-    def run(do_open, src, dst, nthreads):
-        arr = (ctypes.c_int * nthreads)(*cpus[:nthreads]) if cpus else None
+    def run(do_open, src, dst, nthreads, passes, aad_arr, alen):
+        arr = (ctypes.c_int * nthreads)(*cpus[:nthreads])
         return ref.lib.ref_bench(cfg["key_len"] * 8, do_open, key, iv, src.ctypes.data, dst.ctypes.data, nrec, L, stride,
-                                 aad.ctypes.data, aad_len, nthreads, arr)
+                                 aad_arr.ctypes.data, alen, nthreads, arr, passes)
 
-    out = {}
-    for nthreads in sorted({1, threads}):
-        run(0, data, ct, nthreads)  # warm-up (+ produces valid ciphertext for open)
-        reps, ts, to = 0, 0.0, 0.0
-        t_start = time.time()
-        while time.time() - t_start < budget_s / 2 or reps < 3:
-            ts += run(0, data, ct, nthreads)
-            to += run(1, ct, pt, nthreads)
-            reps += 1
+    def measure(nthreads, aad_arr, alen):
+        run(0, data, ct, nthreads, 1, aad_arr, alen)  # warm-up, and valid ciphertext for open
+        t1 = run(0, data, ct, nthreads, 1, aad_arr, alen) + run(1, ct, pt, nthreads, 1, aad_arr, alen)
+        passes = max(1, int(np.ceil(0.3 / max(t1, 1e-6))))
+        st = _steady(lambda: 2 * passes * nrec * L / (run(0, data, ct, nthreads, passes, aad_arr, alen) +
+                                                      run(1, ct, pt, nthreads, passes, aad_arr, alen)) / GIB)
         assert np.array_equal(pt[:, :L], data[:, :L]), "reference round trip failed"
-        out[nthreads] = dict(seal=reps * nrec * L / ts / GIB, open=reps * nrec * L / to / GIB,
-                             both=2 * reps * nrec * L / (ts + to) / GIB, reps=reps)
+        st["passes_per_rep"] = passes
+        return st
+
+    out = {n: measure(n, aad, aad_len) for n in sorted({1, threads})}
+    # BASELINE configs[0]'s shape: 4K x 16 KiB with t/ptlsbench.c's 32-byte AAD uint64_t h[4], h[0] = seq (:129-141)
+    h = np.zeros((nrec, 4), dtype="<u8")
+    h[:, 0] = np.arange(1, nrec + 1, dtype=np.uint64)
+    h8 = h.view(np.uint8).reshape(nrec, 32).copy()
+    conf1 = None
+    if L == 16384:
+        saved = nrec
+        nrec = 4096
+        conf1 = {n: measure(n, h8, 32) for n in sorted({1, threads})}
+        nrec = saved
     cpu_model = ""
     try:
         with open("/proc/cpuinfo") as f:
@@ -170,11 +220,36 @@ def cpu_baseline(cfg_name, cfg, budget_s=4.0):
     except OSError:
         pass
     best = out[threads]
-    return dict(value=round(best["both"], 3), unit="GiB/s seal+open", cores=threads, kind="reference",
-                single_core=round(out[1]["both"], 3), seal_gibps=round(best["seal"], 3), open_gibps=round(best["open"], 3),
-                fusion_can_aesni256=bool(ref.lib.ref_fusion_can_aesni256()), cpu=cpu_model,
-                sample=f"{nrec} x {L} B distinct records ({cfg_name} shape, {aad_len} B AAD), lib/fusion.c via "
-                       f"ptls_aead_encrypt/decrypt, {best['reps']} passes, {threads} pinned threads")
+    res = dict(value=best["median"], unit="GiB/s seal+open", cores=threads, kind="reference",
+               min=best["min"], max=best["max"], spread=best["spread"], reps=best["reps"],
+               single_core=out[1]["median"], single_core_min=out[1]["min"], single_core_spread=out[1]["spread"],
+               cpus_in_affinity=n_aff, cgroup_cpu_quota=quota,
+               fusion_can_aesni256=bool(ref.lib.ref_fusion_can_aesni256()), cpu=cpu_model,
+               sample=f"{nrec} x {L} B distinct records ({nrec * L / GIB:.2f} GiB, {cfg_name} shape, {aad_len} B AAD), "
+                      f"lib/fusion.c via ptls_aead_encrypt/decrypt, one context per pinned thread; median of 5 reps "
+                      f"within {best['spread'] * 100:.1f} %, {threads} threads")
+    if conf1 is not None:
+        res["config1_ptlsbench_aad"] = dict(
+            sample="BASELINE configs[0]: 4096 x 16384 B, 32-B AAD h[4] with h[0] = seq (t/ptlsbench.c:129-141)",
+            single_core=conf1[1]["median"], all_cores=conf1[threads]["median"], all_cores_spread=conf1[threads]["spread"],
+            cores=threads, unit="GiB/s seal+open")
+    return res
+
+
+def plugin_ptlsbench():
+    """the drop-in plugin path at t/ptlsbench.c's own shape (N = 1000 records of L = 1500 B, bench_run_one
+    :88-173): ptls_aead_encrypt / ptls_aead_decrypt through the reference's picotls on lib/fusion.c's
+    ptls_fusion_aes128gcm and on ptls_hip_aes128gcm (one synchronous single-record launch per call)"""
+    import ctypes
+    import ptls_hip
+    from oracle_lib import Ref, ref_ptlsbench
+    if not Ref.available:
+        return None
+    hip = ctypes.addressof(ctypes.c_char.in_dll(ptls_hip.lib(), "ptls_hip_aes128gcm"))
+    fus = Ref().algo("ptls_fusion_aes128gcm")
+    ref_ptlsbench(hip, 50, 1500)  # warm-up: context creation, module load
+    return {"fusion_aes128gcm": ref_ptlsbench(fus), "hip_aes128gcm": ref_ptlsbench(hip),
+            "note": "Mbps as ptlsbench prints it (8 * N * L / microseconds), wall clock and process CPU time"}
 
 
 def max_over_ranks(x, world, device):
@@ -186,6 +261,45 @@ def max_over_ranks(x, world, device):
     t = torch.tensor([x], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
+
+
+def gather_ranks(vals, world, device):
+    """every rank's list of floats (all_gather; the timing summary, not the data path)"""
+    if world == 1:
+        return [list(vals)]
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor(vals, dtype=torch.float64, device=device)
+    out = [torch.empty_like(t) for _ in range(world)]
+    dist.all_gather(out, t)
+    return [o.tolist() for o in out]
+
+
+def _free_port():
+    import socket
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        return sk.getsockname()[1]
+
+
+def launch_ranks(args):
+    """`bench.py --gpus N` without a launcher around it: start N rank processes (one per GPU) through
+    torch.distributed.run on 127.0.0.1, BEFORE this process touches any GPU, relay their output and exit with
+    their status.  Under a launcher (WORLD_SIZE set) the world size must equal --gpus."""
+    world_env = os.environ.get("WORLD_SIZE")
+    if world_env is not None:
+        if int(world_env) != args.gpus:
+            sys.stderr.write(f"bench.py: WORLD_SIZE={world_env} but --gpus {args.gpus}\n")
+            sys.exit(2)
+        return
+    if args.gpus <= 1:
+        return
+    import subprocess
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+    sys.exit(subprocess.call(cmd, env=env))
 
 
 def golden_check(cfg_name, idx, recs, d_ct):
@@ -287,6 +401,46 @@ def host_e2e(args, cfg, eng, ks, recs, lens, d_pt, d_aad, aad_len):
                 note="pinned host buffers; wall clock around ptls_hip_pipeline_seal/open incl. H2D + D2H")
 
 
+def report_ranks(result, per_rank, world, steps, elapsed):
+    """per-rank and whole-node rates from every rank's [seconds, plaintext bytes per step, seal ms, open ms]:
+    whole node = sum of all ranks' bytes / the slowest rank's time"""
+    total_bytes = sum(r[1] for r in per_rank) * 2 * steps  # seal + open each pass over the plaintext
+    result["value"] = round(total_bytes / elapsed / GIB, 2)
+    result["per_rank"] = [{"rank": i, "gibps": round(2 * r[1] * steps / r[0] / GIB, 2), "seconds": round(r[0], 4),
+                           "seal_gibps": round(r[1] / (r[2] * 1e-3) / GIB, 2) if r[2] > 0 else None,
+                           "open_gibps": round(r[1] / (r[3] * 1e-3) / GIB, 2) if r[3] > 0 else None}
+                          for i, r in enumerate(per_rank)]
+    result["whole_node_gibps"] = result["value"]
+
+
+def dry_run(args, cfg, world, rank):
+    """CPU rehearsal of the multi-rank path (tests/test_multirank.py): the same launcher, barriers, max-over-ranks
+    and per-rank gather over gloo, with a sleep standing in for the GPU work"""
+    import torch.distributed as dist
+    if world > 1:
+        dist.init_process_group("gloo")
+    idx, recs, in_total, out_total, lens = make_workload(cfg, rank)
+    sum_L = int(lens.sum())
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        time.sleep(0.02 * (rank + 1))
+    mine = time.perf_counter() - t0
+    if world > 1:
+        dist.barrier()
+    elapsed = max_over_ranks(mine, world, "cpu")
+    per_rank = gather_ranks([mine, float(sum_L), 0.0, 0.0], world, "cpu")
+    result = {"metric": "dry run (no GPU)", "value": None, "unit": "GiB/s", "n_gpus": world, "steps": args.steps,
+              "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3), "dry_run": True,
+              "records_per_rank": len(recs), "first_index_per_rank": gather_ranks([float(idx[0])], world, "cpu")}
+    report_ranks(result, per_rank, world, args.steps, elapsed)
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -297,23 +451,28 @@ def main():
     ap.add_argument("--records", type=int, default=0, help="override records per GPU (smaller runs)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true", help="skip the host-resident (pinned H2D/D2H) measurement")
+    ap.add_argument("--no-plugin", action="store_true", help="skip the ptlsbench-shape plugin timing")
     ap.add_argument("--e2e-records", type=int, default=0, help="records in the host-resident sample (default: 1 GiB)")
+    ap.add_argument("--dry-run", action="store_true", help=argparse.SUPPRESS)  # CPU rehearsal of the rank logic (tests)
     args = ap.parse_args()
-
-    import torch
-    import torch.distributed as dist
-    import ptls_hip
+    launch_ranks(args)  # N > 1 without a launcher: re-run as N ranks, before any GPU call
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    cfg = dict(CONFIGS[args.config])
+    if args.records:
+        cfg["n"] = args.records
+    if args.dry_run:
+        return dry_run(args, cfg, world, rank)
+
+    import torch
+    import torch.distributed as dist
+    import ptls_hip
     torch.cuda.set_device(local)
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
-    cfg = dict(CONFIGS[args.config])
-    if args.records:
-        cfg["n"] = args.records
     eng = ptls_hip.Engine(local)
     idx, recs, in_total, out_total, lens = make_workload(cfg, rank)
     n = len(recs)
@@ -380,6 +539,7 @@ def main():
     for _ in range(args.steps):
         step()
     torch.cuda.synchronize()
+    mine = time.perf_counter() - t0
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -391,6 +551,7 @@ def main():
         step(ktimes)
     seal_ms = float(np.median([a for a, _ in ktimes]))
     open_ms = float(np.median([b for _, b in ktimes]))
+    per_rank = gather_ranks([mine, float(sum_L), seal_ms, open_ms], world, "cuda")
 
     # parity: every record opens to its length and original bytes; sampled records == lib/fusion.c
     ok_open = bool((d_res == torch.tensor(lens.astype(np.int64), device="cuda")).all())
@@ -401,12 +562,11 @@ def main():
 
     alg_bytes = int(2 * sum_L + n * (aad_len + 16))  # 2L + A + 16 per record, per launch
     achieved = alg_bytes / (seal_ms * 1e-3) / 1e9
-    value = world * 2 * sum_L * args.steps / elapsed / GIB
 
     result = {
         "metric": "GiB/s AES-128-GCM seal+open, device-resident, 16KiB records, 1/2/4/8 GPU"
         if args.config == "c2" else f"GiB/s AES-GCM seal+open, device-resident ({args.config})",
-        "value": round(value, 2),
+        "value": None,
         "unit": "GiB/s",
         "n_gpus": world,
         "steps": args.steps,
@@ -420,8 +580,8 @@ def main():
         "config": {"workload": cfg["desc"], "records_per_gpu": n, "record_bytes": cfg["L"] or "mixed 64-16384",
                    "aad_bytes": aad_len, "keys": cfg["keys"], "key_bits": cfg["key_len"] * 8,
                    "lanes_per_record": seal_b.lanes, "parallelism": f"records sharded by range over {world} GPU(s), no collective"},
-        "seal_gibps": round(world * sum_L / (seal_ms * 1e-3) / GIB, 2),
-        "open_gibps": round(world * sum_L / (open_ms * 1e-3) / GIB, 2),
+        "seal_gibps": round(sum(r[1] / (r[2] * 1e-3) for r in per_rank) / GIB, 2),
+        "open_gibps": round(sum(r[1] / (r[3] * 1e-3) for r in per_rank) / GIB, 2),
         "seal_ms": round(seal_ms, 3),
         "open_ms": round(open_ms, 3),
         "key_setup_s": round(setup_s, 4),
@@ -431,12 +591,13 @@ def main():
                      "kernel": ("aesgcm_sparse_kernel (seal)" if seal_b.lanes == 64 else "aesgcm_batch_kernel (seal)"), "algorithmic_bytes_per_launch": alg_bytes},
         "parity": {"open_all_ok": ok_open, "roundtrip_bytes_equal": ok_pt, "golden_records_checked": golden_n},
     }
+    report_ranks(result, per_rank, world, args.steps, elapsed)
     copy_gbs = device_copy_gbs()
     result["roofline"]["measured_copy_gbs"] = copy_gbs
     result["roofline"]["frac_of_measured_copy"] = round(achieved / copy_gbs, 4)
     if seal_b.lanes != 64:  # the batch kernel's LDS model (the sparse-key kernel is latency-bound)
         ceil = lds_issue_ceiling(cfg["key_len"])
-        ceil["frac"] = round(result["seal_gibps"] / world / ceil["seal_gibps"], 4)
+        ceil["frac"] = round(seal_ms and (sum_L / (seal_ms * 1e-3) / GIB) / ceil["seal_gibps"], 4)
         result["roofline"]["lds_issue_ceiling"] = ceil
     if not args.no_e2e and world == 1:  # PCIe path is per GPU; at N > 1 the ranks would share the host links
         result["host_e2e"] = host_e2e(args, cfg, eng, ks, recs, lens, d_pt, d_aad, aad_len)
@@ -450,11 +611,16 @@ def main():
     if os.path.exists(lfile) and "lds_issue_ceiling" in result["roofline"]:  # LDS-array occupancy of the same kernel from its PMC pass (the bound that binds)
         with open(lfile) as f:
             result["roofline"]["lds_issue_ceiling"]["lds_array_busy_measured"] = json.load(f)["lds_array_busy_frac"]
+    for o in (seal_b, open_b):
+        o.close()
+    del d_pt, d_ct, d_out, d_aad, d_res
+    if rank == 0 and world == 1 and not args.no_plugin:
+        result["plugin_ptlsbench"] = plugin_ptlsbench()
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(args.config, cfg)
     if rank == 0:
         print(json.dumps(result), flush=True)
-    for o in (seal_b, open_b, ks, eng):
+    for o in (ks, eng):
         o.close()
     if world > 1:
         dist.destroy_process_group()

@@ -70,6 +70,10 @@ __host__ __device__ constexpr uint32_t lds_bytes(int log2g)
 #ifndef PURE_BLOCKS
 #define PURE_BLOCKS 2 /* data blocks per lane per iteration of the branch-free loop */
 #endif
+#ifndef DEAL_MUTANT
+#define DEAL_MUTANT 0 /* TEST-ONLY broken builds (tools/build_mutants.sh, tests/test_gpu_dealing.py): 1 = the task a wave
+                         drew past one chunk is dropped at the next chunk of the key run, 2 = cbase is not advanced */
+#endif
 
 struct V4 {
     uint32_t w0, w1, w2, w3;
@@ -786,16 +790,37 @@ __device__ __forceinline__ void store_bytes(uint8_t *p, int n, V4 v)
 
 __device__ __forceinline__ V4 mask_block(V4 v, int n);
 
-/* ALIGNED: p is 16-byte aligned, so the 16-byte chunk holding a partial block never crosses a page;
- * load it whole and keep the first n bytes.  Otherwise read exactly n bytes. */
+/* n (0..15) bytes at a 16-byte aligned p as dword loads of the whole dwords, then single bytes: nothing past
+ * p + n is read (fusion over-reads within the page, lib/fusion.c:345-388; a caller's allocation may end at
+ * the record's last byte) */
+__device__ __forceinline__ V4 load_partial_aligned(const uint8_t *p, int n)
+{
+    const uint32_t *q = reinterpret_cast<const uint32_t *>(p);
+    uint32_t w[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int k = n - 4 * i;
+        uint32_t v = 0;
+        if (k >= 4) {
+            v = q[i];
+        } else if (k > 0) {
+#pragma unroll 1
+            for (int j = k - 1; j >= 0; --j)
+                v = (v << 8) | p[4 * i + j];
+        }
+        w[i] = v;
+    }
+    return V4{w[0], w[1], w[2], w[3]};
+}
+
+/* a (possibly partial) block of n bytes: whole blocks as one 16-byte load; partial ones exactly n bytes
+ * (ALIGNED: whole dwords + bytes, otherwise byte by byte) */
 template <bool ALIGNED>
 __device__ __forceinline__ V4 load_block(const uint8_t *p, int n)
 {
-    if (ALIGNED) {
-        const V4 r = load_full(p);
-        return n == 16 ? r : mask_block(r, n);
-    }
-    return n == 16 ? load_full(p) : load_bytes(p, n);
+    if (n == 16)
+        return load_full(p);
+    return ALIGNED ? load_partial_aligned(p, n) : load_bytes(p, n);
 }
 
 template <bool ALIGNED>
@@ -929,6 +954,8 @@ __global__ void __launch_bounds__(WGT)
             cbase = 0;
             have_g = false; /* a task drawn past the old key's run belongs to no chunk */
         }
+        if (DEAL_MUTANT == 1)
+            have_g = false;
         const KeySlot *__restrict__ slot = slots + ch.key;
         const uint32_t *__restrict__ rk = slot->rk;
         const int ntasks = (int)((ch.count + R - 1) / R);
@@ -1228,7 +1255,8 @@ __global__ void __launch_bounds__(WGT)
                 }
             }
         }
-        cbase += (uint32_t)ntasks;
+        if (DEAL_MUTANT != 2)
+            cbase += (uint32_t)ntasks;
     }
 }
 

@@ -126,7 +126,15 @@ struct st_ptls_hip_batch_t {
     int auto_lanes; /* chosen from the record lengths */
     bool forced;
     uint32_t max_key; /* largest key slot any record names (checked against the keyset at seal/open) */
+    unsigned max_wg;  /* 0, or a cap on the workgroups of a launch (planning then sizes chunks for that many) */
 };
+
+/* CUs a batch is planned and launched for: the device's, or fewer when the batch caps its grid */
+static unsigned batch_cus(const st_ptls_hip_batch_t *b)
+{
+    const unsigned ncu = (unsigned)b->eng->ncu;
+    return b->max_wg != 0 && b->max_wg < ncu ? b->max_wg : ncu;
+}
 
 class DeviceGuard {
   public:
@@ -291,8 +299,9 @@ extern "C" int ptls_hip_keyset_set(ptls_hip_keyset_t *ks, size_t first, size_t c
         else if (hipStreamSynchronize(s) != hipSuccess)
             rc = fail(PTLS_HIP_ENODEV, "keyset_set: key setup failed");
     }
-    /* raw keys do not stay in device memory outside the expanded slots */
-    (void)hipMemset(d_tmp, 0, kbytes + ibytes);
+    /* raw keys do not stay in device memory outside the expanded slots: the scrub is ordered after the
+     * uploads and the key setup on the same stream, whatever path got here */
+    (void)hipMemsetAsync(d_tmp, 0, kbytes + ibytes, s);
     (void)hipStreamSynchronize(s);
     (void)hipFree(d_tmp);
     if (rc == 0)
@@ -441,13 +450,27 @@ static int plan_wg(const std::vector<Chunk> &ch, int lanes)
 static void build_chunks(const ptls_hip_record_t *recs, size_t n, int lanes, unsigned ncu, std::vector<Chunk> &ch,
                          std::vector<uint32_t> &order, bool &all_aligned)
 {
-    const uint32_t per_task = lanes >= 64 ? 1u : 64u / (uint32_t)lanes;
-    const size_t tasks = (n + per_task - 1) / per_task;
-    const size_t spread = (tasks + (ncu ? ncu : 1) - 1) / (ncu ? ncu : 1); /* tasks per chunk for >= ncu chunks */
-    const uint32_t max_chunk = per_task * (uint32_t)std::max<size_t>(1, std::min<size_t>((WG_MAX / 64) * 2, spread));
     ch.clear();
     order.resize(n);
     all_aligned = true;
+    if (lanes == SPARSE_LANES) {
+        /* the sparse kernel keeps no per-key workgroup state and its waves take records grid-stride: in
+         * decreasing length over the whole batch every wave gets a similar share of bytes.  One chunk holds
+         * the record count (the kernel reads nothing else from it); its key field names no slot. */
+        for (size_t i = 0; i < n; ++i) {
+            order[i] = (uint32_t)i;
+            if (((recs[i].in_off | recs[i].out_off | recs[i].aad_off) & 15) != 0)
+                all_aligned = false;
+        }
+        std::stable_sort(order.begin(), order.end(), [&](uint32_t x, uint32_t y) { return recs[x].len > recs[y].len; });
+        if (n != 0)
+            ch.push_back(Chunk{0, (uint32_t)n, 0xffffffffu, all_aligned ? 1u : 0u});
+        return;
+    }
+    const uint32_t per_task = 64u / (uint32_t)lanes;
+    const size_t tasks = (n + per_task - 1) / per_task;
+    const size_t spread = (tasks + (ncu ? ncu : 1) - 1) / (ncu ? ncu : 1); /* tasks per chunk for >= ncu chunks */
+    const uint32_t max_chunk = per_task * (uint32_t)std::max<size_t>(1, std::min<size_t>((WG_MAX / 64) * 2, spread));
     size_t i = 0;
     while (i < n) {
         Chunk c;
@@ -471,17 +494,13 @@ static void build_chunks(const ptls_hip_record_t *recs, size_t n, int lanes, uns
         all_aligned = all_aligned && (c.flags & 1u);
         ch.push_back(c);
     }
-    /* the sparse kernel's waves take records grid-stride: in decreasing length over the whole batch, every
-     * wave gets a similar share of bytes (the chunks then only give it the record count) */
-    if (lanes == SPARSE_LANES)
-        std::stable_sort(order.begin(), order.end(), [&](uint32_t x, uint32_t y) { return recs[x].len > recs[y].len; });
 }
 
 static int plan_chunks(ptls_hip_batch_t *b)
 {
     std::vector<Chunk> ch;
     std::vector<uint32_t> order;
-    build_chunks(b->h_recs.data(), b->n, b->lanes, (unsigned)b->eng->ncu, ch, order, b->all_aligned);
+    build_chunks(b->h_recs.data(), b->n, b->lanes, batch_cus(b), ch, order, b->all_aligned);
     b->wg = b->forced_wg ? b->forced_wg : plan_wg(ch, b->lanes);
     if (b->d_chunks != nullptr)
         (void)hipFree(b->d_chunks);
@@ -587,6 +606,15 @@ extern "C" int ptls_hip_batch_workgroup(ptls_hip_batch_t *b)
     return b->wg;
 }
 
+extern "C" int ptls_hip_batch_set_max_workgroups(ptls_hip_batch_t *b, int n)
+{
+    if (b == nullptr || n < 0)
+        return fail(PTLS_HIP_EINVAL, "batch_set_max_workgroups: n must be >= 0");
+    DeviceGuard g(b->eng->device);
+    b->max_wg = (unsigned)n;
+    return plan_chunks(b);
+}
+
 static int run_batch(ptls_hip_batch_t *b, ptls_hip_keyset_t *ks, const void *in, const void *aad, void *out, uint64_t *result,
                      void *stream, bool open, ptls_hip_keyset_t *hp_ks = nullptr, const ptls_hip_supp_t *supp = nullptr,
                      void *mask = nullptr)
@@ -623,7 +651,7 @@ static int run_batch(ptls_hip_batch_t *b, ptls_hip_keyset_t *ks, const void *in,
     const bool base_aligned = ((reinterpret_cast<uintptr_t>(in) | reinterpret_cast<uintptr_t>(a.aad) |
                                 reinterpret_cast<uintptr_t>(out)) & 15) == 0;
     const bool aligned = base_aligned && b->all_aligned;
-    const unsigned grid = plan_grid(b->n, b->nchunks, b->lanes, (unsigned)b->eng->ncu);
+    const unsigned grid = plan_grid(b->n, b->nchunks, b->lanes, batch_cus(b));
     const int rounds = ks->key_size == 16 ? 10 : 14;
     int e = launch_batch(b->lanes, rounds, open, b->wg, grid, stream, a, aligned);
     if (e != 0)
@@ -1175,7 +1203,8 @@ struct hip_aead_state {
 
 struct hip_aead_context {
     ptls_aead_context_t super;
-    hip_aead_state *st;
+    hip_aead_state *st; /* nullptr after an IV-only setup of a fresh context */
+    uint8_t iv[12];     /* the static IV of such a context (fusion keeps it in static_iv, lib/fusion.c:1188-1189) */
 };
 
 [[noreturn]] static void plugin_die(const char *what)
@@ -1218,24 +1247,31 @@ static const hip_ctr_state *ctr_state_of(const ptls_cipher_context_t *c)
     return reinterpret_cast<const hip_ctr_context *>(c)->st;
 }
 
-/* do_init: the keystream block AES-ECB(key, iv) on the device (fusion: aesecb_encrypt, :1057-1062) */
-static void ctr_init(ptls_cipher_context_t *_ctx, const void *iv)
+/* one AES-ECB block on the device with the state's key (fusion: aesecb_encrypt, lib/fusion.c:322-334) */
+static void ecb_block(hip_ctr_state *st, const void *src, uint8_t dst[16])
 {
-    hip_ctr_state *st = reinterpret_cast<hip_ctr_context *>(_ctx)->st;
     DeviceGuard g(st->eng->device);
     const ptls_hip_supp_t sp{32, 48, 0, PTLS_HIP_SUPP_ENABLE};
     std::memcpy(st->h_stage, &sp, sizeof(sp));
-    std::memcpy(st->h_stage + 32, iv, 16);
-    plugin_check(hipMemcpyAsync(st->d_buf, st->h_stage, 48, hipMemcpyHostToDevice, st->stream), "ctr upload");
+    std::memcpy(st->h_stage + 32, src, 16);
+    plugin_check(hipMemcpyAsync(st->d_buf, st->h_stage, 48, hipMemcpyHostToDevice, st->stream), "ecb upload");
     const int e = launch_aesecb(st->ks->key_size == 16 ? 10 : 14, reinterpret_cast<const ptls_hip_supp_t *>(st->d_buf), 1,
                                 st->d_buf, st->d_buf, st->ks->d_slots, 1, st->eng->d_t0, 1, st->stream);
     if (e != 0) {
         g_err = hipGetErrorString((hipError_t)e);
-        plugin_die("ctr launch");
+        plugin_die("ecb launch");
     }
-    plugin_check(hipMemcpyAsync(st->h_stage + 48, st->d_buf + 48, 16, hipMemcpyDeviceToHost, st->stream), "ctr download");
-    plugin_check(hipStreamSynchronize(st->stream), "ctr sync");
-    std::memcpy(st->bits, st->h_stage + 48, 16);
+    plugin_check(hipMemcpyAsync(st->h_stage + 48, st->d_buf + 48, 16, hipMemcpyDeviceToHost, st->stream), "ecb download");
+    plugin_check(hipStreamSynchronize(st->stream), "ecb sync");
+    std::memcpy(dst, st->h_stage + 48, 16);
+    std::memset(st->h_stage + 32, 0, 32);
+}
+
+/* do_init: the keystream block AES-ECB(key, iv) on the device (fusion: aesecb_encrypt, :1057-1062) */
+static void ctr_init(ptls_cipher_context_t *_ctx, const void *iv)
+{
+    hip_ctr_state *st = reinterpret_cast<hip_ctr_context *>(_ctx)->st;
+    ecb_block(st, iv, st->bits);
     st->ready = true;
 }
 
@@ -1252,44 +1288,18 @@ static void ctr_transform(ptls_cipher_context_t *_ctx, void *output, const void 
         static_cast<uint8_t *>(output)[i] = static_cast<const uint8_t *>(input)[i] ^ st->bits[i];
 }
 
-static void ctr_dispose(ptls_cipher_context_t *_ctx)
+/* a one-key ECB state on the plugin engine's device: expanded key slot + 64 B of device / pinned staging */
+static hip_ctr_state *ecb_state_new(const void *key, size_t key_size)
 {
-    auto *ctx = reinterpret_cast<hip_ctr_context *>(_ctx);
-    hip_ctr_state *st = ctx->st;
-    if (st == nullptr)
-        return;
-    {
-        DeviceGuard g(st->eng->device);
-        ptls_hip_keyset_free(st->ks);
-        if (st->d_buf != nullptr) {
-            (void)hipMemset(st->d_buf, 0, 64);
-            (void)hipStreamSynchronize(st->stream);
-        }
-        (void)hipFree(st->d_buf);
-        if (st->h_stage != nullptr)
-            std::memset(st->h_stage, 0, 64);
-        (void)hipHostFree(st->h_stage);
-        (void)hipStreamDestroy(st->stream);
-    }
-    std::memset(st->bits, 0, sizeof(st->bits));
-    delete st;
-    ctx->st = nullptr;
-}
-
-static int aesctr_setup(ptls_cipher_context_t *_ctx, int is_enc, const void *key, size_t key_size)
-{
-    (void)is_enc; /* CTR: same operation both ways */
-    auto *ctx = reinterpret_cast<hip_ctr_context *>(_ctx);
-    ctx->st = nullptr;
     ptls_hip_engine_t *eng = plugin_engine();
     if (eng == nullptr || key == nullptr)
-        return -1;
+        return nullptr;
     DeviceGuard g(eng->device);
     auto *st = new hip_ctr_state();
     st->eng = eng;
     if (hipStreamCreateWithFlags(&st->stream, hipStreamNonBlocking) != hipSuccess) {
         delete st;
-        return -1;
+        return nullptr;
     }
     st->ks = ptls_hip_keyset_new(eng, key_size, 1);
     const bool ok = st->ks != nullptr && hipMalloc(&st->d_buf, 64) == hipSuccess &&
@@ -1302,13 +1312,91 @@ static int aesctr_setup(ptls_cipher_context_t *_ctx, int is_enc, const void *key
         (void)hipHostFree(st->h_stage);
         (void)hipStreamDestroy(st->stream);
         delete st;
-        return -1;
+        return nullptr;
     }
-    ctx->st = st;
+    return st;
+}
+
+static void ecb_state_free(hip_ctr_state *st)
+{
+    {
+        DeviceGuard g(st->eng->device);
+        ptls_hip_keyset_free(st->ks);
+        if (st->d_buf != nullptr) {
+            (void)hipMemsetAsync(st->d_buf, 0, 64, st->stream);
+            (void)hipStreamSynchronize(st->stream);
+        }
+        (void)hipFree(st->d_buf);
+        if (st->h_stage != nullptr)
+            std::memset(st->h_stage, 0, 64);
+        (void)hipHostFree(st->h_stage);
+        (void)hipStreamDestroy(st->stream);
+    }
+    std::memset(st->bits, 0, sizeof(st->bits));
+    delete st;
+}
+
+static void ctr_dispose(ptls_cipher_context_t *_ctx)
+{
+    auto *ctx = reinterpret_cast<hip_ctr_context *>(_ctx);
+    if (ctx->st == nullptr)
+        return;
+    ecb_state_free(ctx->st);
+    ctx->st = nullptr;
+}
+
+static int aesctr_setup(ptls_cipher_context_t *_ctx, int is_enc, const void *key, size_t key_size)
+{
+    (void)is_enc; /* CTR: same operation both ways */
+    auto *ctx = reinterpret_cast<hip_ctr_context *>(_ctx);
+    ctx->st = ecb_state_new(key, key_size);
+    if (ctx->st == nullptr)
+        return -1;
     ctx->super.do_dispose = ctr_dispose;
     ctx->super.do_init = ctr_init;
     ctx->super.do_transform = ctr_transform;
     return 0;
+}
+
+/* ---- fusion's public one-block ECB API (include/picotls/fusion.h:52-54, lib/fusion.c:857-928) ---- */
+
+extern "C" int ptls_hip_aesecb_init(ptls_hip_aesecb_context_t *ctx, int is_enc, const void *key, size_t key_size, int aesni256)
+{
+    (void)aesni256; /* an x86 code-path choice in fusion; accepted so call sites stay the same */
+    if (ctx == nullptr)
+        return fail(PTLS_HIP_EINVAL, "aesecb_init: ctx is NULL");
+    ctx->state = nullptr;
+    ctx->rounds = 0;
+    /* fusion asserts encryption-only and a 16- or 32-byte key (lib/fusion.c:859-873) */
+    if (!is_enc || key == nullptr || (key_size != PTLS_AES128_KEY_SIZE && key_size != PTLS_AES256_KEY_SIZE))
+        return fail(PTLS_HIP_EINVAL, "aesecb_init: encryption with a 16- or 32-byte key only");
+    hip_ctr_state *st = ecb_state_new(key, key_size);
+    if (st == nullptr)
+        return fail(PTLS_HIP_ENODEV, "aesecb_init: %s", g_err.empty() ? "no usable gfx950 device" : g_err.c_str());
+    ctx->state = st;
+    ctx->rounds = key_size == PTLS_AES128_KEY_SIZE ? 10 : 14;
+    return 0;
+}
+
+extern "C" void ptls_hip_aesecb_dispose(ptls_hip_aesecb_context_t *ctx)
+{
+    if (ctx == nullptr || ctx->state == nullptr)
+        return;
+    ecb_state_free(static_cast<hip_ctr_state *>(ctx->state));
+    ctx->state = nullptr;
+    ctx->rounds = 0;
+}
+
+extern "C" void ptls_hip_aesecb_encrypt(ptls_hip_aesecb_context_t *ctx, void *dst, const void *src)
+{
+    if (ctx == nullptr || ctx->state == nullptr) {
+        fprintf(stderr, "ptls_hip: aesecb_encrypt on a context that init did not set up\n");
+        abort();
+    }
+    uint8_t block[16];
+    ecb_block(static_cast<hip_ctr_state *>(ctx->state), src, block);
+    std::memcpy(dst, block, 16);
+    std::memset(block, 0, sizeof(block));
 }
 
 static int aes128ctr_setup(ptls_cipher_context_t *ctx, int is_enc, const void *key)
@@ -1464,14 +1552,19 @@ static void aead_dispose(ptls_aead_context_t *_ctx)
 
 static void aead_get_iv(ptls_aead_context_t *_ctx, void *iv)
 {
-    std::memcpy(iv, reinterpret_cast<hip_aead_context *>(_ctx)->st->iv, 12);
+    auto *ctx = reinterpret_cast<hip_aead_context *>(_ctx);
+    std::memcpy(iv, ctx->st != nullptr ? ctx->st->iv : ctx->iv, 12);
 }
 
 static void aead_set_iv(ptls_aead_context_t *_ctx, const void *iv)
 {
-    hip_aead_state *st = reinterpret_cast<hip_aead_context *>(_ctx)->st;
-    std::memcpy(st->iv, iv, 12);
-    st->iv_dirty = true;
+    auto *ctx = reinterpret_cast<hip_aead_context *>(_ctx);
+    if (ctx->st == nullptr) {
+        std::memcpy(ctx->iv, iv, 12);
+        return;
+    }
+    std::memcpy(ctx->st->iv, iv, 12);
+    ctx->st->iv_dirty = true;
 }
 
 static void aead_encrypt_init(ptls_aead_context_t *, uint64_t, const void *, size_t)
@@ -1585,12 +1678,25 @@ static int aesgcm_setup(ptls_aead_context_t *_ctx, int is_enc, const void *key, 
 {
     (void)is_enc; /* one context seals and opens, as fusion's (lib/fusion.c:1184-1206) */
     auto *ctx = reinterpret_cast<hip_aead_context *>(_ctx);
-    if (key == nullptr) { /* IV-only re-setup (lib/fusion.c:1190-1191) */
-        if (ctx->st == nullptr)
-            return -1;
+    if (key == nullptr) {
+        /* IV-only setup: fusion stores the IV and returns 0, on a fresh context as on a keyed one
+         * (lib/fusion.c:1188-1191).  ptls_aead_new_direct zeroes only `super` (lib/picotls.c:6465), so a
+         * fresh context is recognised by its unset dispose_crypto, never by reading the uninitialised tail.
+         * Unlike fusion's, the fresh context also gets dispose / get_iv / set_iv, so ptls_aead_free and
+         * ptls_aead_xor_iv work on it; encrypt / decrypt stay NULL as in fusion. */
+        if (_ctx->dispose_crypto == nullptr) {
+            ctx->st = nullptr;
+            std::memcpy(ctx->iv, iv, 12);
+            ctx->super.dispose_crypto = aead_dispose;
+            ctx->super.do_get_iv = aead_get_iv;
+            ctx->super.do_set_iv = aead_set_iv;
+            return 0;
+        }
         aead_set_iv(_ctx, iv);
         return 0;
     }
+    if (_ctx->dispose_crypto != nullptr && ctx->st != nullptr) /* re-keying a keyed context: release the old key first */
+        aead_dispose(_ctx);
     ctx->st = state_new(key, iv, key_size);
     if (ctx->st == nullptr)
         return -1;

@@ -8,13 +8,15 @@
  * in the workgroup's LDS, so each key switch costs a table build and two workgroup barriers, and a key
  * run of one record leaves 11 of 12 waves waiting (20 GiB/s at 65 536 records over 65 536 keys).
  * Here every wave works alone on one record at a time:
- *   - 64 lanes per record: lane l takes GHASH elements e = l, l + 64, ... (Horner with P = H^64), then
- *     a 6-level shuffle tree multiplies lane l's sum by H^(q+1), q = (N - 1 - l) mod 64;
- *   - each wave owns an 8 KiB 4-bit-window table in LDS ([nibble position p][value v] = v at p times P),
- *     rebuilt from the key's basis P * x^e (keysetup: H^(2^t) * x^e, t = 0..6) for P = H^64 before the
- *     record and for H, H^2, ..., H^32 during the tree: 8 ds_write_b128 per lane per build, no barrier
- *     (a wave's LDS operations complete in order);
- *   - a multiply is 32 ds_read_b128 (gh_mul_nibble); AES-CTR uses the batch kernel's 32x-replicated
+ *   - 64 lanes per record: lane l takes GHASH elements e = l, l + 64, ... (Horner with P = H^64);
+ *   - each wave owns an 8 KiB 4-bit-window table of H^64 in LDS ([nibble position p][value v] = v at p
+ *     times H^64), rebuilt per record from the key's basis H^64 * x^e (keysetup): 4 basis loads and 8
+ *     ds_write_b128 per lane, no barrier (a wave's LDS operations complete in order).  A record of at most
+ *     64 GHASH elements (one per lane) needs no Horner step and skips the build;
+ *   - the combination needs no table: lane l multiplies its sum by its own power H^(q+1),
+ *     q = (N - 1 - l) mod 64, read from keysetup's per-key H^1..H^64 list, on the VALU (gf_mul_valu), and an
+ *     XOR butterfly over the 64 lanes leaves the GHASH in every lane;
+ *   - a Horner multiply is 32 ds_read_b128 (gh_mul_nibble); AES-CTR uses the batch kernel's 32x-replicated
  *     T-tables (64 KiB) and round keys through the scalar unit.  64 KiB + 12 x 8 KiB = the CU's 160 KiB.
  */
 #include "batch_kernel.h"
@@ -139,7 +141,7 @@ __global__ void __launch_bounds__(SPARSE_WG)
                        n2 = slot->iv[2] ^ bswap32((uint32_t)rec.seq);
         const CtrConst cc = ctr_const(lds, lb_aes, rk, n0, n1, n2);
         const int iters = (N + 63) >> 6;
-        wave_lds_sync(); /* the previous record's tree reads are done */
+        wave_lds_sync(); /* the previous record's Horner reads of the table are done */
         if (SPARSE_ABLATE != 3 && iters > 1) { /* N <= 64: one element per lane, no Horner step */
             V4 b[4];
             load_wave_basis(bs + 6 * 128, lane, b); /* H^64 */
@@ -183,9 +185,8 @@ __global__ void __launch_bounds__(SPARSE_WG)
             }
         }
 
-        /* lane l's sum times H^(q+1), q = distance of its last element from the end: times H, then a shuffle
-         * tree over q (level d: lanes with q = 0 mod 2d absorb the lane holding q + d, i.e. lane l - d, times H^d) */
-        /* q = distance of the lane's last element from the end of the GHASH input */
+        /* lane l's sum times H^(q+1), q = distance of its last element from the end of the GHASH input, on the
+         * VALU; the XOR butterfly then sums the 64 lanes (ghash_combine) */
         const int q = (N - 1 - lane) & 63;
         if (SPARSE_ABLATE != 1)
             y = ghash_combine(bs, q, y);

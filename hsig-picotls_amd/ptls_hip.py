@@ -55,6 +55,10 @@ SIGNATURES = {
     "ptls_hip_batch_lanes": (_i, [_vp]),
     "ptls_hip_batch_set_workgroup": (_i, [_vp, _i]),
     "ptls_hip_batch_workgroup": (_i, [_vp]),
+    "ptls_hip_batch_set_max_workgroups": (_i, [_vp, _i]),
+    "ptls_hip_aesecb_init": (_i, [_vp, _i, _vp, _sz, _i]),
+    "ptls_hip_aesecb_dispose": (None, [_vp]),
+    "ptls_hip_aesecb_encrypt": (None, [_vp, _vp, _vp]),
     "ptls_hip_aesgcm_seal_batch": (_i, [_vp, _vp, _vp, _vp, _vp, _vp]),
     "ptls_hip_aesgcm_open_batch": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "ptls_hip_aesgcm_seal_batch_supp": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
@@ -234,6 +238,10 @@ class Batch:
     def set_workgroup(self, threads):
         _check(lib().ptls_hip_batch_set_workgroup(self.ptr, threads), "batch_set_workgroup")
 
+    def set_max_workgroups(self, n):
+        """cap the launch grid at n workgroups (0 = one per CU); chunks are then planned for n CUs"""
+        _check(lib().ptls_hip_batch_set_max_workgroups(self.ptr, n), "batch_set_max_workgroups")
+
     def seal(self, keyset, inp, aad, out, stream=None):
         _check(lib().ptls_hip_aesgcm_seal_batch(self.ptr, keyset.ptr, _ptr(inp), _ptr(aad), _ptr(out), _stream(stream)),
                "seal_batch")
@@ -308,6 +316,31 @@ class AesGcm:
         if self.ptr:
             lib().ptls_hip_aesgcm_free(self.ptr)
             self.ptr = None
+
+
+class AesEcb:
+    """fusion's one-block ECB API (ptls_hip_aesecb_*, ~ ptls_fusion_aesecb_*, include/picotls/fusion.h:52-54)"""
+
+    class Ctx(ctypes.Structure):  # ptls_hip_aesecb_context_t
+        _fields_ = [("state", ctypes.c_void_p), ("rounds", ctypes.c_uint)]
+
+    def __init__(self, key, is_enc=1):
+        self.ctx = self.Ctx()
+        _check(lib().ptls_hip_aesecb_init(ctypes.addressof(self.ctx), is_enc, bytes(key), len(key), 0), "aesecb_init")
+
+    @property
+    def rounds(self):
+        return self.ctx.rounds
+
+    def encrypt(self, block):
+        assert len(block) == 16
+        out = ctypes.create_string_buffer(16)
+        lib().ptls_hip_aesecb_encrypt(ctypes.addressof(self.ctx), out, bytes(block))
+        return out.raw
+
+    def close(self):
+        if self.ctx.state:
+            lib().ptls_hip_aesecb_dispose(ctypes.addressof(self.ctx))
 
 
 class Pipeline:

@@ -92,6 +92,22 @@ void ptls_hip_aesgcm_encrypt(ptls_hip_aesgcm_context_t *ctx, void *output, const
 int ptls_hip_aesgcm_decrypt(ptls_hip_aesgcm_context_t *ctx, void *output, const void *input, size_t inlen, const void *nonce,
                             const void *aad, size_t aadlen, const void *tag);
 
+/* Fusion's public one-block AES-ECB API (ptls_fusion_aesecb_init / _dispose / _encrypt,
+ * include/picotls/fusion.h:52-54, lib/fusion.c:857-928): an encryption-only AES-128/256 key schedule and
+ * single-block encryption, here with the key expanded into a device key slot and each block encrypted by
+ * one kernel launch (synchronous, host buffers).  Same arguments as fusion's, including the trailing
+ * `aesni256` (an x86 code-path switch there, ignored here).  Fusion's init returns void and asserts on
+ * decryption or a key size other than 16 / 32; this one returns 0, or PTLS_HIP_EINVAL for those cases and
+ * PTLS_HIP_ENODEV without a usable gfx950 device (ctx->state is then NULL and dispose is a no-op).
+ * dispose zeroizes and releases the device key slot. */
+typedef struct st_ptls_hip_aesecb_context_t {
+    void *state;     /* engine-owned: key slot, staging, stream */
+    unsigned rounds; /* 10 or 14, as fusion's ctx->rounds */
+} ptls_hip_aesecb_context_t;
+int ptls_hip_aesecb_init(ptls_hip_aesecb_context_t *ctx, int is_enc, const void *key, size_t key_size, int aesni256);
+void ptls_hip_aesecb_dispose(ptls_hip_aesecb_context_t *ctx);
+void ptls_hip_aesecb_encrypt(ptls_hip_aesecb_context_t *ctx, void *dst, const void *src);
+
 /* ------------------------------------------------------------------------------------------ *
  * 2. batch extension                                                                          *
  * ------------------------------------------------------------------------------------------ */
@@ -144,7 +160,9 @@ int ptls_hip_keyset_update_secrets(ptls_hip_keyset_t *ks, size_t first, size_t c
  *         ptls_aead_decrypt, lib/fusion.c:1151-1166).
  * The nonce is slot.iv with bytes 4..11 XORed with big-endian seq (ptls_aead__build_iv,
  * lib/picotls.c:6492-6506).  in == out (in place) is allowed.  For full speed keep in_off, out_off
- * 16-byte aligned and put records of the same key next to each other. */
+ * 16-byte aligned and put records of the same key next to each other.  The kernels read exactly the
+ * record's input (+ tag on open) and AAD bytes and write exactly its output bytes: buffers need no padding
+ * past the last record (partial blocks are loaded as whole dwords + single bytes). */
 typedef struct st_ptls_hip_record_t {
     uint64_t in_off;
     uint64_t out_off;
@@ -171,6 +189,10 @@ int ptls_hip_batch_lanes(ptls_hip_batch_t *batch);
 /* threads per workgroup of the batch kernel (512 or 768); 0 = automatic (default).  For tuning. */
 int ptls_hip_batch_set_workgroup(ptls_hip_batch_t *batch, int threads);
 int ptls_hip_batch_workgroup(ptls_hip_batch_t *batch);
+/* at most `n` workgroups per launch, and chunks planned as for a device of n CUs (0 = the device's CU
+ * count, the default).  For tests of the work distribution (a workgroup then takes several chunks of one
+ * key run) and for sharing a device with other work. */
+int ptls_hip_batch_set_max_workgroups(ptls_hip_batch_t *batch, int n);
 
 /* Asynchronous on `stream`; all pointers are device (or device-accessible) memory.  Fails with
  * PTLS_HIP_EINVAL (nothing launched) when a record names a key slot outside `ks`. */

@@ -19,6 +19,14 @@
 #include <time.h>
 #include "picotls.h"
 #include "picotls/fusion.h"
+#include "picotls/minicrypto.h"
+
+static double now(void)
+{
+    struct timespec t;
+    clock_gettime(CLOCK_MONOTONIC, &t);
+    return (double)t.tv_sec + 1e-9 * (double)t.tv_nsec;
+}
 
 static ptls_aead_algorithm_t *pick(int bits)
 {
@@ -79,6 +87,101 @@ size_t ref_seal_iv96(int bits, const void *key, const void *iv, const void *xor_
     return r;
 }
 
+/* ---- IV-only setup (setup_crypto with key == NULL; fusion: lib/fusion.c:1188-1191) ---- */
+
+/* the context ptls_aead_new_direct makes for key == NULL (lib/picotls.c:6458-6473): fusion stores the IV and
+ * returns 0, leaving the vtable unset, so the caller may only release it with ref_ctx_free_raw */
+void *ref_aead_new_iv_only(const ptls_aead_algorithm_t *algo, int is_enc, const void *iv)
+{
+    return ptls_aead_new_direct((ptls_aead_algorithm_t *)algo, is_enc, NULL, iv);
+}
+
+void ref_ctx_free_raw(void *ctx)
+{
+    free(ctx);
+}
+
+/* algo->setup_crypto(ctx, is_enc, NULL, iv) on a live context: IV-only re-setup */
+int ref_aead_setup_iv_only(ptls_aead_context_t *ctx, int is_enc, const void *iv)
+{
+    return ctx->algo->setup_crypto(ctx, is_enc, NULL, iv);
+}
+
+/* lib/fusion.c: keyed context with iv, then an IV-only re-setup to iv2, then one seal */
+size_t ref_seal_reiv(int bits, const void *key, const void *iv, const void *iv2, uint64_t seq, const void *aad, size_t aadlen,
+                     const void *in, size_t inlen, void *out)
+{
+    ptls_aead_context_t *ctx = ptls_aead_new_direct(pick(bits), 1, key, iv);
+    if (ref_aead_setup_iv_only(ctx, 1, iv2) != 0)
+        return SIZE_MAX;
+    size_t r = ptls_aead_encrypt(ctx, out, in, inlen, seq, aad, aadlen);
+    ptls_aead_free(ctx);
+    return r;
+}
+
+/* ---- t/ptlsbench.c bench_run_one (:88-173) over any AEAD object ----
+ * The same loop: batches of up to 1000 ptls_aead_encrypt of one cache-hot zero input into 1000 distinct
+ * outputs, AAD = uint64_t h[4] with h[0] = seq starting at 1, then the same records ptls_aead_decrypt-ed.
+ * Contexts come from ptls_aead_new(aead, sha256, is_enc, 'z' x 64, NULL) as in bench_run_aead (:218-225).
+ * Times are wall clock (CLOCK_MONOTONIC) and, like ptlsbench, process CPU time; both in microseconds. */
+#define REF_BENCH_BATCH 1000
+int ref_ptlsbench(const ptls_aead_algorithm_t *aead, size_t n, size_t l, double *wall_enc, double *wall_dec, double *cpu_enc,
+                  double *cpu_dec)
+{
+    uint8_t secret[PTLS_MAX_SECRET_SIZE];
+    memset(secret, 'z', sizeof(secret));
+    ptls_aead_context_t *e = ptls_aead_new((ptls_aead_algorithm_t *)aead, &ptls_minicrypto_sha256, 1, secret, NULL);
+    ptls_aead_context_t *d = ptls_aead_new((ptls_aead_algorithm_t *)aead, &ptls_minicrypto_sha256, 0, secret, NULL);
+    uint8_t *v_in = calloc(1, l + 1), *v_dec = malloc(l + 1), *v_enc[REF_BENCH_BATCH];
+    uint64_t h[4] = {0};
+    int ret = 0;
+    *wall_enc = *wall_dec = *cpu_enc = *cpu_dec = 0;
+    for (size_t i = 0; i < REF_BENCH_BATCH; ++i)
+        v_enc[i] = malloc(l + PTLS_MAX_DIGEST_SIZE);
+    if (e == NULL || d == NULL) {
+        ret = -1;
+        goto Exit;
+    }
+    for (size_t k = 0; k < n;) {
+        size_t e_len = 0, i_max = n - k > REF_BENCH_BATCH ? REF_BENCH_BATCH : n - k;
+        uint64_t old_h = h[0];
+        struct timespec c0, c1, c2;
+        clock_gettime(CLOCK_PROCESS_CPUTIME_ID, &c0);
+        double t0 = now();
+        for (size_t i = 0; i < i_max; ++i) {
+            h[0]++;
+            e_len = ptls_aead_encrypt(e, v_enc[i], v_in, l, h[0], h, sizeof(h));
+        }
+        double t1 = now();
+        clock_gettime(CLOCK_PROCESS_CPUTIME_ID, &c1);
+        h[0] = old_h;
+        for (size_t i = 0; i < i_max; ++i) {
+            h[0]++;
+            if (ptls_aead_decrypt(d, v_dec, v_enc[i], e_len, h[0], h, sizeof(h)) != l) {
+                ret = -2;
+                goto Exit;
+            }
+        }
+        double t2 = now();
+        clock_gettime(CLOCK_PROCESS_CPUTIME_ID, &c2);
+        *wall_enc += (t1 - t0) * 1e6;
+        *wall_dec += (t2 - t1) * 1e6;
+        *cpu_enc += ((double)(c1.tv_sec - c0.tv_sec) * 1e9 + (double)(c1.tv_nsec - c0.tv_nsec)) * 1e-3;
+        *cpu_dec += ((double)(c2.tv_sec - c1.tv_sec) * 1e9 + (double)(c2.tv_nsec - c1.tv_nsec)) * 1e-3;
+        k += i_max;
+    }
+Exit:
+    if (e != NULL)
+        ptls_aead_free(e);
+    if (d != NULL)
+        ptls_aead_free(d);
+    for (size_t i = 0; i < REF_BENCH_BATCH; ++i)
+        free(v_enc[i]);
+    free(v_in);
+    free(v_dec);
+    return ret;
+}
+
 /* ---- CPU baseline: lib/fusion.c over a batch of distinct record buffers, 1..N pinned threads ---- */
 
 struct bench_job {
@@ -89,15 +192,9 @@ struct bench_job {
     size_t first, count, len, stride, aadlen;
     const uint8_t *aad; /* nrec * aadlen */
     pthread_barrier_t *bar;
+    int passes;
     double secs;
 };
-
-static double now(void)
-{
-    struct timespec t;
-    clock_gettime(CLOCK_MONOTONIC, &t);
-    return (double)t.tv_sec + 1e-9 * (double)t.tv_nsec;
-}
 
 static void *bench_worker(void *p)
 {
@@ -112,12 +209,14 @@ static void *bench_worker(void *p)
     ptls_aead_context_t *ctx = ptls_aead_new_direct(pick(j->bits), !j->do_open, j->key, j->iv);
     pthread_barrier_wait(j->bar);
     double t0 = now();
-    for (size_t i = j->first; i < j->first + j->count; ++i) {
-        const uint8_t *aad = j->aad + i * j->aadlen;
-        if (j->do_open)
-            (void)ptls_aead_decrypt(ctx, j->out + i * j->stride, j->in + i * j->stride, j->len + 16, i, aad, j->aadlen);
-        else
-            ptls_aead_encrypt(ctx, j->out + i * j->stride, j->in + i * j->stride, j->len, i, aad, j->aadlen);
+    for (int pass = 0; pass < j->passes; ++pass) {
+        for (size_t i = j->first; i < j->first + j->count; ++i) {
+            const uint8_t *aad = j->aad + i * j->aadlen;
+            if (j->do_open)
+                (void)ptls_aead_decrypt(ctx, j->out + i * j->stride, j->in + i * j->stride, j->len + 16, i, aad, j->aadlen);
+            else
+                ptls_aead_encrypt(ctx, j->out + i * j->stride, j->in + i * j->stride, j->len, i, aad, j->aadlen);
+        }
     }
     j->secs = now() - t0;
     ptls_aead_free(ctx);
@@ -125,10 +224,10 @@ static void *bench_worker(void *p)
 }
 
 /* Seals (do_open = 0) or opens (do_open = 1) records i = 0..nrec-1 held at in + i*stride, writing to
- * out + i*stride; record i uses seq = i and aad + i*aadlen.  Returns the wall time of the slowest
- * thread (all threads start behind a barrier).  cpus: list of cpu ids to pin to (NULL = no pinning). */
+ * out + i*stride, `passes` times over; record i uses seq = i and aad + i*aadlen.  Returns the wall time of
+ * the slowest thread (all threads start behind a barrier).  cpus: cpu ids to pin to (NULL = no pinning). */
 double ref_bench(int bits, int do_open, const void *key, const void *iv, void *in, void *out, size_t nrec, size_t len,
-                 size_t stride, const void *aad, size_t aadlen, int threads, const int *cpus)
+                 size_t stride, const void *aad, size_t aadlen, int threads, const int *cpus, int passes)
 {
     pthread_t th[512];
     struct bench_job jobs[512];
@@ -141,7 +240,7 @@ double ref_bench(int bits, int do_open, const void *key, const void *iv, void *i
     for (int t = 0; t < threads; ++t) {
         size_t a = nrec * (size_t)t / (size_t)threads, b = nrec * (size_t)(t + 1) / (size_t)threads;
         jobs[t] = (struct bench_job){bits, cpus != NULL ? cpus[t] : -1, do_open, key, iv, in, out, a, b - a, len, stride, aadlen,
-                                     aad, &bar, 0};
+                                     aad, &bar, passes < 1 ? 1 : passes, 0};
         pthread_create(&th[t], NULL, bench_worker, &jobs[t]);
     }
     double mx = 0;
@@ -161,7 +260,6 @@ double ref_bench(int bits, int do_open, const void *key, const void *iv, void *i
  * the caller passes (the HIP engine's, for the drop-in test); the hash is minicrypto's SHA-256/384 *
  * (lib/cifra/aes128.c, aes256.c), compiled unmodified.                                            *
  * ---------------------------------------------------------------------------------------------- */
-#include "picotls/minicrypto.h"
 
 struct ref_tls13 {
     ptls_context_t ctx;
@@ -228,6 +326,37 @@ void *ref_tls13_import(int bits, const void *aead, int is_server, const void *en
     uint8_t *q = params;
     put16(&q, (uint16_t)(p - params - 2));
     if (ptls_import(&r->ctx, &r->tls, ptls_iovec_init(params, p - params)) != 0) {
+        free(r);
+        return NULL;
+    }
+    return r;
+}
+
+/* A post-handshake TLS 1.2 connection of the reference: ptls_build_tls12_export_params derives the key block
+ * from a master secret and the hello randoms with the reference's PRF (lib/picotls.c:5217-5255), ptls_import
+ * instantiates the AEADs through import_tls12_traffic_protection (:5291-5312), and ptls_send / ptls_receive
+ * then run the TLS 1.2 record layer (buffer_push_encrypted_records :747-794 with build_tls12_aad :730-739,
+ * handle_input_tls12 :5927-5990).  aead NULL -> fusion's ptls_non_temporal_aes{128,256}gcm, the objects
+ * whose tls12 fields are {4, 8} (lib/fusion.c:2154-2179). */
+void *ref_tls12_import(int bits, const void *aead, int is_server, const void *master_secret, const void *hello_randoms,
+                       uint64_t next_send_record_iv)
+{
+    struct ref_tls13 *r = calloc(1, sizeof(*r));
+    r->suite.id = bits == 256 ? PTLS_CIPHER_SUITE_ECDHE_RSA_WITH_AES_256_GCM_SHA384 : PTLS_CIPHER_SUITE_ECDHE_RSA_WITH_AES_128_GCM_SHA256;
+    r->suite.aead = aead != NULL ? (ptls_aead_algorithm_t *)aead : (bits == 256 ? &ptls_non_temporal_aes256gcm : &ptls_non_temporal_aes128gcm);
+    r->suite.hash = bits == 256 ? &ptls_minicrypto_sha384 : &ptls_minicrypto_sha256;
+    r->suite.name = "ref12";
+    r->suites[0] = &r->suite;
+    r->ctx.random_bytes = ref_random_bytes;
+    r->ctx.get_time = &ptls_get_time;
+    r->ctx.tls12_cipher_suites = r->suites;
+    ptls_buffer_t buf;
+    ptls_buffer_init(&buf, "", 0);
+    int ok = ptls_build_tls12_export_params(&r->ctx, &buf, is_server, 0, &r->suite, master_secret, hello_randoms, next_send_record_iv,
+                                            NULL, ptls_iovec_init(NULL, 0)) == 0 &&
+             ptls_import(&r->ctx, &r->tls, ptls_iovec_init(buf.base, buf.off)) == 0;
+    ptls_buffer_dispose(&buf);
+    if (!ok) {
         free(r);
         return NULL;
     }

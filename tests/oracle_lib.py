@@ -132,7 +132,14 @@ class Ref:
                                     _c.c_size_t, _u8p]
         L.ref_bench.restype = _c.c_double
         L.ref_bench.argtypes = [_c.c_int, _c.c_int, _u8p, _u8p, _u8p, _u8p, _c.c_size_t, _c.c_size_t, _c.c_size_t,
-                                _u8p, _c.c_size_t, _c.c_int, _c.c_void_p]
+                                _u8p, _c.c_size_t, _c.c_int, _c.c_void_p, _c.c_int]
+        L.ref_seal_reiv.restype = _c.c_size_t
+        L.ref_seal_reiv.argtypes = [_c.c_int, _u8p, _u8p, _u8p, _c.c_uint64, _u8p, _c.c_size_t, _u8p, _c.c_size_t, _u8p]
+        L.ref_aead_new_iv_only.restype = _c.c_void_p
+        L.ref_aead_new_iv_only.argtypes = [_c.c_void_p, _c.c_int, _u8p]
+        L.ref_aead_setup_iv_only.restype = _c.c_int
+        L.ref_aead_setup_iv_only.argtypes = [_c.c_void_p, _c.c_int, _u8p]
+        L.ref_ctx_free_raw.argtypes = [_c.c_void_p]
         L.ref_fusion_supported.restype = _c.c_int
         L.ref_fusion_can_aesni256.restype = _c.c_int
         self.supported = bool(L.ref_fusion_supported())
@@ -155,6 +162,17 @@ class Ref:
         self.lib.ref_seal_iv96(len(key) * 8, _buf(key), _buf(iv), _buf(xor_bytes), len(xor_bytes), seq, _buf(aad),
                                len(aad), _buf(pt), len(pt), out)
         return out.raw
+
+    def seal_reiv(self, key, iv, iv2, seq, aad, pt):
+        """keyed with iv, IV-only re-setup to iv2 (setup_crypto(ctx, 1, NULL, iv2)), then seal"""
+        out = _c.create_string_buffer(len(pt) + 16)
+        n = self.lib.ref_seal_reiv(len(key) * 8, _buf(key), _buf(iv), _buf(iv2), seq, _buf(aad), len(aad), _buf(pt), len(pt),
+                                   out)
+        assert n == len(pt) + 16
+        return out.raw
+
+    def algo(self, name):
+        return _c.addressof(_c.c_char.in_dll(self.lib, name))
 
     def open(self, key, iv, seq, aad, ct):
         out = _c.create_string_buffer(max(len(ct), 16))
@@ -211,6 +229,42 @@ class RefTLS:
         if self.h:
             self.lib.ref_tls13_free(self.h)
             self.h = None
+
+
+class RefTLS12(RefTLS):
+    """A post-handshake TLS 1.2 connection of the REFERENCE: ptls_build_tls12_export_params (the reference's PRF
+    key block from master_secret and the hello randoms) + ptls_import, then its TLS 1.2 record layer
+    (build_tls12_aad, lib/picotls.c:730-739).  `aead` = address of a ptls_aead_algorithm_t (None = fusion's
+    ptls_non_temporal_aes{128,256}gcm, lib/fusion.c:2154-2179)."""
+
+    def __init__(self, bits, master_secret, hello_randoms, next_send_record_iv=0, aead=None, is_server=1):
+        L = self.lib = _c.CDLL(REF_SO)
+        L.ref_tls12_import.restype = _c.c_void_p
+        L.ref_tls12_import.argtypes = [_c.c_int, _c.c_void_p, _c.c_int, _u8p, _u8p, _c.c_uint64]
+        L.ref_tls13_free.argtypes = [_c.c_void_p]
+        L.ref_tls13_send.restype = _c.c_long
+        L.ref_tls13_send.argtypes = [_c.c_void_p, _u8p, _c.c_size_t, _u8p, _c.c_size_t]
+        L.ref_tls13_receive.restype = _c.c_int
+        L.ref_tls13_receive.argtypes = [_c.c_void_p, _u8p, _c.c_size_t, _c.POINTER(_c.c_size_t), _u8p, _c.c_size_t,
+                                        _c.POINTER(_c.c_size_t)]
+        assert len(master_secret) == 48 and len(hello_randoms) == 64
+        self.h = L.ref_tls12_import(bits, aead, is_server, _buf(master_secret), _buf(hello_randoms), next_send_record_iv)
+        assert self.h, "ptls_build_tls12_export_params / ptls_import failed"
+
+
+def ref_ptlsbench(aead_addr, n=1000, l=1500):
+    """t/ptlsbench.c bench_run_one (:88-173) on the AEAD object at aead_addr: dict of encrypt / decrypt Mbps
+    (ptlsbench's unit) and microseconds per call, wall clock and process CPU time"""
+    L = _c.CDLL(REF_SO)
+    L.ref_ptlsbench.restype = _c.c_int
+    L.ref_ptlsbench.argtypes = [_c.c_void_p, _c.c_size_t, _c.c_size_t] + [_c.POINTER(_c.c_double)] * 4
+    v = [_c.c_double() for _ in range(4)]
+    rc = L.ref_ptlsbench(aead_addr, n, l, *[_c.byref(x) for x in v])
+    assert rc == 0, f"ref_ptlsbench failed ({rc})"
+    we, wd, ce, cd = (x.value for x in v)
+    mbps = lambda us: round(n * l * 8 / us, 1)  # noqa: E731  (bits per microsecond = Mbps, t/ptlsbench.c:175-183)
+    return dict(n=n, l=l, enc_mbps_wall=mbps(we), dec_mbps_wall=mbps(wd), enc_mbps_cpu=mbps(ce), dec_mbps_cpu=mbps(cd),
+                enc_us_per_call=round(we / n, 3), dec_us_per_call=round(wd / n, 3))
 
 
 def ref_hkdf_expand_label(bits, secret, label, outlen):

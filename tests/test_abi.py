@@ -147,3 +147,53 @@ def test_fails_loudly_without_device():
         ref.ptls_aead_new_direct.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
         algo = ctypes.addressof(ctypes.c_char.in_dll(L, "ptls_hip_aes128gcm"))
         assert not ref.ptls_aead_new_direct(algo, 1, bytes(16), bytes(12))
+
+
+def test_iv_only_setup_of_a_fresh_context():
+    """setup_crypto(key == NULL) on the context ptls_aead_new_direct just made (lib/picotls.c:6458-6473): fusion
+    stores the IV and returns 0 (lib/fusion.c:1188-1191) without touching the vtable; so does ptls_hip_aes*gcm,
+    recognising the fresh context by its zeroed `super` (no device needed, none touched).  Ours additionally
+    gives it get_iv / set_iv / dispose, so the IV reads back and ptls_aead_free releases it."""
+    from oracle_lib import Ref
+    if not Ref.available:
+        pytest.skip("oracle/_ref not built")
+    import plugin_driver
+    ref = Ref()
+    L = ptls_hip.lib()
+    iv = bytes(range(40, 52))
+    for bits in (128, 256):
+        fus = ref.lib.ref_aead_new_iv_only(ref.algo(f"ptls_fusion_aes{bits}gcm"), 1, iv)
+        assert fus, "fusion's IV-only setup returns 0"
+        f = plugin_driver.AeadContext.from_address(fus)
+        assert not (f.do_encrypt or f.do_decrypt or f.dispose_crypto)
+        ref.lib.ref_ctx_free_raw(fus)
+        for name in (f"ptls_hip_aes{bits}gcm", f"ptls_hip_non_temporal_aes{bits}gcm"):
+            algo = ctypes.addressof(ctypes.c_char.in_dll(L, name))
+            for is_enc in (0, 1):
+                ctx = ref.lib.ref_aead_new_iv_only(algo, is_enc, iv)
+                assert ctx, name
+                v = plugin_driver.AeadContext.from_address(ctx)
+                assert v.algo == algo and not (v.do_encrypt or v.do_encrypt_v or v.do_decrypt)
+                got = ctypes.create_string_buffer(12)
+                ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_void_p)(v.do_get_iv)(ctx, got)
+                assert got.raw == iv
+                drv = plugin_driver.PluginDriver()  # the reference's lifecycle functions; no device touched
+                drv.xor_iv(ctx, b"\x01\x02")  # the reference's ptls_aead_xor_iv over our get_iv / set_iv
+                ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_void_p)(v.do_get_iv)(ctx, got)
+                assert got.raw == bytes([iv[0] ^ 1, iv[1] ^ 2]) + iv[2:]
+                assert ref.lib.ref_aead_setup_iv_only(ctx, is_enc, iv) == 0  # again, now on the IV-only context
+                drv.free(ctx)  # ptls_aead_free -> our dispose_crypto
+
+
+def test_aesecb_api_argument_checks():
+    """ptls_hip_aesecb_init rejects what fusion's asserts reject (decryption, key sizes other than 16 / 32,
+    lib/fusion.c:859-873) with EINVAL, and, without a device, fails with ENODEV leaving the context empty"""
+    L = ptls_hip.lib()
+    ctx = ptls_hip.AesEcb.Ctx()
+    assert L.ptls_hip_aesecb_init(ctypes.addressof(ctx), 0, bytes(16), 16, 0) == -1
+    assert L.ptls_hip_aesecb_init(ctypes.addressof(ctx), 1, bytes(24), 24, 0) == -1
+    assert not ctx.state
+    if not _gpu_present():
+        assert L.ptls_hip_aesecb_init(ctypes.addressof(ctx), 1, bytes(16), 16, 0) == -2
+        assert not ctx.state and ctx.rounds == 0
+        L.ptls_hip_aesecb_dispose(ctypes.addressof(ctx))  # no-op on an empty context

@@ -643,3 +643,94 @@ def test_host_pipeline_seal_open(engine, oracle, slice_kib):
         assert hout[rec["out_off"]: rec["out_off"] + len(r[4])].tobytes() == r[4]
     pipe.close()
     ks.close()
+
+
+def test_iv_only_resetup_of_a_keyed_context(engine, oracle):
+    """setup_crypto(ctx, is_enc, NULL, iv2) on a keyed context only replaces the static IV (lib/fusion.c:1188-1191):
+    the next seal equals lib/fusion.c's after the same IV-only re-setup, and a keyed seal under iv2"""
+    from oracle_lib import Ref
+    if not Ref.available:
+        pytest.skip("oracle/_ref not built")
+    import plugin_driver
+    drv = plugin_driver.PluginDriver()
+    ref = Ref()
+    rng = np.random.default_rng(77)
+    for bits in (128, 256):
+        key = rng.integers(0, 256, bits // 8, dtype=np.uint8).tobytes()
+        iv, iv2 = (rng.integers(0, 256, 12, dtype=np.uint8).tobytes() for _ in range(2))
+        text = rng.integers(0, 256, 1000, dtype=np.uint8).tobytes()
+        aad = b"hdr"
+        for non_temporal in (False, True):
+            ctx = drv.new(bits, key, iv, is_enc=1, non_temporal=non_temporal)
+            assert drv.encrypt(ctx, text, 5, aad) == ref.seal(key, iv, 5, aad, text)
+            assert ref.lib.ref_aead_setup_iv_only(ctx, 1, iv2) == 0
+            assert drv.encrypt(ctx, text, 5, aad) == ref.seal_reiv(key, iv, iv2, 5, aad, text) == ref.seal(key, iv2, 5, aad, text)
+            drv.free(ctx)
+
+
+def test_aesecb_api_fusion_kats(engine, oracle, golden):
+    """ptls_hip_aesecb_init / _encrypt / _dispose replay t/fusion.c test_ecb (:71-85: all-zero AES-128 and AES-256
+    keys on "hello world!!!!!"), then random keys and blocks against the oracle"""
+    for v in golden["kats"]["ecb"]:
+        ecb = ptls_hip.AesEcb(bytes.fromhex(v["key"]))
+        assert ecb.rounds == (10 if len(v["key"]) == 32 else 14)
+        assert ecb.encrypt(bytes.fromhex(v["pt"])).hex() == v["ct"]
+        ecb.close()
+    rng = np.random.default_rng(5)
+    for key_len in (16, 32):
+        key = rng.integers(0, 256, key_len, dtype=np.uint8).tobytes()
+        ecb = ptls_hip.AesEcb(key)
+        for _ in range(8):
+            blk = rng.integers(0, 256, 16, dtype=np.uint8).tobytes()
+            assert ecb.encrypt(blk) == oracle.aes_ecb(key, blk)
+        ecb.close()
+    with pytest.raises(ptls_hip.HipError):
+        ptls_hip.AesEcb(bytes(16), is_enc=0)  # fusion: assert(is_enc) (lib/fusion.c:859)
+
+
+@pytest.mark.parametrize("bits", [128, 256])
+def test_tls12_record_layer_over_non_temporal_objects(engine, bits):
+    """The tls12 = {4, 8} fields ptls_hip_non_temporal_aes*gcm advertise, exercised by the reference's TLS 1.2
+    record layer: two post-handshake TLS 1.2 connections made by ptls_build_tls12_export_params + ptls_import
+    from one master secret, one on lib/fusion.c's ptls_non_temporal_aes*gcm and one on ours.  ptls_send
+    (8-byte explicit record IV from the counter, 13-byte AAD of build_tls12_aad, lib/picotls.c:730-794) emits
+    the same wire bytes; each side's ptls_receive (handle_input_tls12, :5927-5990) decrypts the other's; a
+    flipped byte is rejected the same way by both."""
+    from oracle_lib import Ref, RefTLS12
+    if not Ref.available:
+        pytest.skip("oracle/_ref not built")
+    import plugin_driver
+    drv = plugin_driver.PluginDriver()
+    rng = np.random.default_rng(bits)
+    master = rng.integers(0, 256, 48, dtype=np.uint8).tobytes()
+    randoms = rng.integers(0, 256, 64, dtype=np.uint8).tobytes()
+    rec_iv = int(rng.integers(0, 2 ** 62))
+    ours = drv.nt_algos[bits]
+    f_srv = RefTLS12(bits, master, randoms, rec_iv, None, is_server=1)
+    h_srv = RefTLS12(bits, master, randoms, rec_iv, ours, is_server=1)
+    f_cli = RefTLS12(bits, master, randoms, 0, None, is_server=0)
+    h_cli = RefTLS12(bits, master, randoms, 0, ours, is_server=0)
+
+    def receive_all(conn, wire):
+        got, pos = b"", 0
+        while pos < len(wire):
+            ret, used, pt = conn.receive(wire[pos:])
+            assert ret == 0 and used > 0, (ret, used)
+            got += pt
+            pos += used
+        return got
+
+    for L in (1, 15, 16, 17, 1350, 16384, 16385, 40000):
+        payload = rng.integers(0, 256, L, dtype=np.uint8).tobytes()
+        wire_f, wire_h = f_srv.send(payload), h_srv.send(payload)
+        assert wire_h == wire_f, L
+        assert receive_all(h_cli, wire_f) == payload
+        assert receive_all(f_cli, wire_h) == payload
+    # tamper: the same response from both record layers (fusion's NT decrypt vs ours)
+    payload = rng.integers(0, 256, 500, dtype=np.uint8).tobytes()
+    wire = bytearray(f_srv.send(payload))
+    assert bytes(wire) == h_srv.send(payload)
+    wire[40] ^= 0x10
+    assert h_cli.receive(bytes(wire)) == f_cli.receive(bytes(wire))
+    for c in (f_srv, h_srv, f_cli, h_cli):
+        c.close()

@@ -67,3 +67,38 @@ def test_multi_key_shards_key_major():
         assert np.array_equal(seq, idx // K)                       # per-key sequence number
         assert np.all(np.diff(key.astype(np.int64)) >= 0)          # same-key records adjacent
         assert lens.min() >= 64 and lens.max() <= 16384
+
+
+def _bench(*extra, env=None):
+    import json
+    import subprocess
+    e = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        e.pop(k, None)
+    e.update(env or {})
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--dry-run", "--config", "c3", "--records", "2048",
+                          "--steps", "3", "--warmup", "1", *extra], env=e, capture_output=True, text=True, timeout=240)
+    lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
+    return out.returncode, [json.loads(ln) for ln in lines], out.stderr
+
+
+def test_bench_launches_its_own_ranks():
+    """`bench.py --gpus 2` with no launcher around it starts 2 ranks itself (torch.distributed.run, 127.0.0.1), as the
+    driver's plain `bench.py --gpus N` would on an 8-GPU node; rank 0 alone prints one line with n_gpus 2, both
+    ranks' own rates, and a whole-node rate of the ranks' bytes over the slowest rank's time"""
+    rc, lines, err = _bench("--gpus", "2")
+    assert rc == 0, err[-3000:]
+    assert len(lines) == 1, lines
+    r = lines[0]
+    assert r["n_gpus"] == 2 and len(r["per_rank"]) == 2
+    assert [x[0] for x in r["first_index_per_rank"]] == [0.0, 2048.0]  # disjoint record ranges
+    slow = max(x["seconds"] for x in r["per_rank"])
+    assert r["per_rank"][1]["seconds"] > r["per_rank"][0]["seconds"]  # rank 1 sleeps twice as long
+    total = 2 * 2 * 2048 * 1350 * 3 / (1 << 30)  # ranks x (seal + open) x bytes x steps
+    assert abs(r["value"] - total / (r["ms_per_step"] * 3 / 1e3)) / r["value"] < 0.02
+    assert r["ms_per_step"] * 3 / 1e3 >= slow
+
+
+def test_bench_rejects_a_world_size_mismatch():
+    rc, lines, err = _bench("--gpus", "2", env={"WORLD_SIZE": "3", "RANK": "0", "LOCAL_RANK": "0"})
+    assert rc == 2 and not lines and "WORLD_SIZE=3" in err
