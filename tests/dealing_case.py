@@ -54,6 +54,10 @@ def mismatches(engine, oracle, key_len, lanes):
 
 def main():
     lanes, key_len = int(sys.argv[1]), int(sys.argv[2])
+    import torch
+    # torch first: its HIP runtime must be the process's one before libptls_hip.so loads (the same order as
+    # tests/conftest.py's engine fixture and bench.py; the other order leaves torch with "No HIP GPUs")
+    assert torch.cuda.is_available()
     import ptls_hip
     from oracle_lib import Oracle
     eng = ptls_hip.Engine(0)
