@@ -848,6 +848,8 @@ struct PipeSlot {
 struct st_ptls_hip_pipeline_t {
     ptls_hip_engine_t *eng;
     size_t slice_bytes, max_recs;
+    int transport;      /* PTLS_HIP_TRANSPORT_*: what the caller asked for */
+    int last_transport; /* what the last seal/open used */
     PipeSlot slot[NSLOT];
 };
 
@@ -920,6 +922,20 @@ extern "C" void ptls_hip_pipeline_free(ptls_hip_pipeline_t *p)
     delete p;
 }
 
+extern "C" int ptls_hip_pipeline_set_transport(ptls_hip_pipeline_t *p, int transport)
+{
+    if (p == nullptr ||
+        !(transport == PTLS_HIP_TRANSPORT_AUTO || transport == PTLS_HIP_TRANSPORT_COPY || transport == PTLS_HIP_TRANSPORT_MAPPED))
+        return fail(PTLS_HIP_EINVAL, "pipeline_set_transport: bad arguments");
+    p->transport = transport;
+    return 0;
+}
+
+extern "C" int ptls_hip_pipeline_last_transport(ptls_hip_pipeline_t *p)
+{
+    return p->last_transport;
+}
+
 extern "C" int ptls_hip_host_register(void *ptr, size_t len)
 {
     HIP_TRY(hipHostRegister(ptr, len, hipHostRegisterDefault), PTLS_HIP_ENODEV);
@@ -943,6 +959,112 @@ struct Span {
  * is parsed after the open, like ptls_hip_tls13_open_batch) */
 enum PipeMode { PIPE_SEAL, PIPE_OPEN, PIPE_TLS13_SEAL, PIPE_TLS13_OPEN };
 
+/* the device address of pinned (hipHostMalloc'd) or registered host memory, or nullptr if it is not mapped */
+static void *mapped_ptr(const void *h)
+{
+    if (h == nullptr)
+        return nullptr;
+    void *d = nullptr;
+    if (hipHostGetDevicePointer(&d, const_cast<void *>(h), 0) != hipSuccess) {
+        (void)hipGetLastError(); /* not an error of the pipeline: the copy transport is used */
+        return nullptr;
+    }
+    return d;
+}
+
+/* PTLS_HIP_TRANSPORT_MAPPED: the batch kernel reads the records from, and writes them to, the caller's pinned host
+ * buffers over PCIe itself (their device addresses); no staging copies, no copy engines.  Only the descriptors,
+ * the launch plan and the header-protection descriptors go through the slots' pinned staging.  Slices of at
+ * most max_recs records rotate over the slots' streams.  (tools/hostmem_probe.py, DESIGN.md §6.3: the copy
+ * engines carry ~57 GB/s in both directions together, the kernel's own PCIe reads + writes ~80 GB/s.) */
+static int pipeline_run_mapped(ptls_hip_pipeline_t *p, ptls_hip_keyset_t *ks, const ptls_hip_record_t *recs, size_t n,
+                               const uint8_t *d_in, const uint8_t *d_aad, uint8_t *d_out, uint64_t *h_result, uint64_t *d_res,
+                               PipeMode mode, ptls_hip_keyset_t *hp_ks, const ptls_hip_supp_t *supp, uint8_t *d_mask)
+{
+    const bool open = mode == PIPE_OPEN || mode == PIPE_TLS13_OPEN;
+    const bool aad_in_out = mode == PIPE_TLS13_SEAL, aad_in_in = mode == PIPE_TLS13_OPEN;
+    const int rounds = ks->key_size == 16 ? 10 : 14;
+    std::vector<Chunk> ch;
+    std::vector<uint32_t> order;
+    int k = 0;
+    for (size_t i = 0; i < n; ++k) {
+        const size_t cnt = std::min(n - i, p->max_recs - 1);
+        PipeSlot &s = p->slot[k % NSLOT];
+        if (s.busy)
+            HIP_TRY(hipEventSynchronize(s.done), PTLS_HIP_ENODEV);
+        std::memcpy(s.h_recs, recs + i, cnt * sizeof(ptls_hip_record_t));
+        const int lanes = choose_lanes(std::vector<ptls_hip_record_t>(s.h_recs, s.h_recs + cnt));
+        bool aligned;
+        build_chunks(s.h_recs, cnt, lanes, (unsigned)p->eng->ncu, ch, order, aligned);
+        std::memcpy(s.h_chunks, ch.data(), ch.size() * sizeof(Chunk));
+        std::memcpy(s.h_order, order.data(), cnt * sizeof(uint32_t));
+        for (size_t t = 0; t < cnt; ++t)
+            s.h_recs_ord[t] = s.h_recs[order[t]];
+        HIP_TRY(hipMemcpyAsync(s.d_recs_ord, s.h_recs_ord, cnt * sizeof(ptls_hip_record_t), hipMemcpyHostToDevice, s.stream),
+                PTLS_HIP_ENODEV);
+        HIP_TRY(hipMemcpyAsync(s.d_order, s.h_order, cnt * sizeof(uint32_t), hipMemcpyHostToDevice, s.stream), PTLS_HIP_ENODEV);
+        HIP_TRY(hipMemcpyAsync(s.d_recs, s.h_recs, cnt * sizeof(ptls_hip_record_t), hipMemcpyHostToDevice, s.stream),
+                PTLS_HIP_ENODEV);
+        HIP_TRY(hipMemcpyAsync(s.d_chunks, s.h_chunks, ch.size() * sizeof(Chunk), hipMemcpyHostToDevice, s.stream), PTLS_HIP_ENODEV);
+        if (supp != nullptr) {
+            std::memcpy(s.h_supp, supp + i, cnt * sizeof(ptls_hip_supp_t));
+            HIP_TRY(hipMemcpyAsync(s.d_supp, s.h_supp, cnt * sizeof(ptls_hip_supp_t), hipMemcpyHostToDevice, s.stream),
+                    PTLS_HIP_ENODEV);
+        }
+        const unsigned egrid = (unsigned)std::min<size_t>((cnt + 255) / 256, (size_t)p->eng->ncu * 4);
+        if (aad_in_out) {
+            const int eh = launch_tls13_headers(s.d_recs, (uint32_t)cnt, d_out, egrid, s.stream);
+            if (eh != 0)
+                return fail(PTLS_HIP_ELAUNCH, "pipeline: header kernel launch failed: %s", hipGetErrorString((hipError_t)eh));
+        }
+        uint64_t *res = d_res != nullptr ? d_res + i : s.d_result;
+        KernelArgs a{};
+        a.recs = s.d_recs;
+        a.recs_ord = s.d_recs_ord;
+        a.order = s.d_order;
+        a.chunks = s.d_chunks;
+        a.nchunks = (uint32_t)ch.size();
+        a.in = d_in;
+        a.aad = aad_in_out ? d_out : aad_in_in ? d_in : d_aad;
+        a.out = d_out;
+        a.result = res;
+        a.slots = ks->d_slots;
+        a.basis = ks->d_basis;
+        a.t0 = p->eng->d_t0;
+        if (supp != nullptr) {
+            a.supp = s.d_supp;
+            a.hp_slots = hp_ks->d_slots;
+            a.hp_nslots = (uint32_t)hp_ks->nslots;
+            a.mask = d_mask;
+        }
+        const bool base_aligned =
+            ((reinterpret_cast<uintptr_t>(a.in) | reinterpret_cast<uintptr_t>(a.aad) | reinterpret_cast<uintptr_t>(a.out)) & 15) == 0;
+        const unsigned grid = plan_grid(cnt, ch.size(), lanes, (unsigned)p->eng->ncu);
+        const int e = launch_batch(lanes, rounds, open, plan_wg(ch, lanes), grid, s.stream, a, aligned && base_aligned);
+        if (e != 0)
+            return fail(PTLS_HIP_ELAUNCH, "pipeline: kernel launch failed: %s", hipGetErrorString((hipError_t)e));
+        if (mode == PIPE_TLS13_OPEN) {
+            const int ei = launch_tls13_inner(s.d_recs, (uint32_t)cnt, d_out, res, egrid, s.stream);
+            if (ei != 0)
+                return fail(PTLS_HIP_ELAUNCH, "pipeline: inner-plaintext kernel launch failed: %s", hipGetErrorString((hipError_t)ei));
+        }
+        if (open && d_res == nullptr)
+            HIP_TRY(hipMemcpyAsync(h_result + i, s.d_result, cnt * sizeof(uint64_t), hipMemcpyDeviceToHost, s.stream),
+                    PTLS_HIP_ENODEV);
+        HIP_TRY(hipEventRecord(s.done, s.stream), PTLS_HIP_ENODEV);
+        s.busy = true;
+        i += cnt;
+    }
+    for (auto &s : p->slot) {
+        if (s.busy)
+            HIP_TRY(hipEventSynchronize(s.done), PTLS_HIP_ENODEV);
+        s.busy = false;
+    }
+    /* the kernel's stores to host memory are complete once its stream event has been waited for */
+    p->last_transport = PTLS_HIP_TRANSPORT_MAPPED;
+    return 0;
+}
+
 static int pipeline_run(ptls_hip_pipeline_t *p, ptls_hip_keyset_t *ks, const ptls_hip_record_t *recs, size_t n, const void *h_in,
                         const void *h_aad, void *h_out, uint64_t *h_result, PipeMode mode, ptls_hip_keyset_t *hp_ks = nullptr,
                         const ptls_hip_supp_t *supp = nullptr, void *h_mask = nullptr)
@@ -961,6 +1083,19 @@ static int pipeline_run(ptls_hip_pipeline_t *p, ptls_hip_keyset_t *ks, const ptl
         if (recs[i].key >= ks->nslots)
             return fail(PTLS_HIP_EINVAL, "pipeline: record %zu names key slot %u, the keyset has %zu", i, recs[i].key, ks->nslots);
     DeviceGuard g(p->eng->device);
+    if (p->transport != PTLS_HIP_TRANSPORT_COPY && n != 0) {
+        const uint8_t *d_in = static_cast<const uint8_t *>(mapped_ptr(h_in));
+        uint8_t *d_out = static_cast<uint8_t *>(mapped_ptr(h_out));
+        const uint8_t *d_aad = static_cast<const uint8_t *>(mapped_ptr(h_aad));
+        uint8_t *d_mask = static_cast<uint8_t *>(mapped_ptr(h_mask));
+        uint64_t *d_res = open ? static_cast<uint64_t *>(mapped_ptr(h_result)) : nullptr;
+        const bool ok = d_in != nullptr && d_out != nullptr && (h_aad == nullptr || d_aad != nullptr) && (h_mask == nullptr || d_mask != nullptr);
+        if (ok)
+            return pipeline_run_mapped(p, ks, recs, n, d_in, d_aad, d_out, h_result, d_res, mode, hp_ks, supp, d_mask);
+        if (p->transport == PTLS_HIP_TRANSPORT_MAPPED)
+            return fail(PTLS_HIP_EINVAL, "pipeline: transport MAPPED needs pinned or registered host buffers (in, out, aad, mask)");
+    }
+    p->last_transport = PTLS_HIP_TRANSPORT_COPY;
     const int rounds = ks->key_size == 16 ? 10 : 14;
     const size_t tag_in = open ? 16 : 0, tag_out = open ? 0 : 16;
     const uint8_t *hin = static_cast<const uint8_t *>(h_in), *haad = static_cast<const uint8_t *>(h_aad);

@@ -25,6 +25,7 @@ assert TLS13_MESSAGE_DTYPE.itemsize == 40
 TLS13_BAD_RECORD_MAC = (1 << 64) - 1
 TLS13_NO_CONTENT_TYPE = (1 << 64) - 2
 TLS13_DECODE_ERROR = -50
+TRANSPORT_AUTO, TRANSPORT_COPY, TRANSPORT_MAPPED = 0, 1, 2
 
 
 def record_tls13_type(t):
@@ -83,6 +84,8 @@ SIGNATURES = {
     "ptls_hip_pipeline_tls13_seal": (_i, [_vp, _vp, _vp, _sz, _vp, _vp]),
     "ptls_hip_pipeline_seal_supp": (_i, [_vp, _vp, _vp, _vp, _vp, _sz, _vp, _vp, _vp, _vp]),
     "ptls_hip_pipeline_tls13_open": (_i, [_vp, _vp, _vp, _sz, _vp, _vp, _vp]),
+    "ptls_hip_pipeline_set_transport": (_i, [_vp, _i]),
+    "ptls_hip_pipeline_last_transport": (_i, [_vp]),
     "ptls_hip_host_register": (_i, [_vp, _sz]),
     "ptls_hip_host_unregister": (_i, [_vp]),
 }
@@ -346,11 +349,21 @@ class AesEcb:
 class Pipeline:
     """host-resident seal/open: pinned H2D -> kernel -> D2H overlapped over three streams"""
 
-    def __init__(self, engine, slice_bytes=64 << 20):
+    def __init__(self, engine, slice_bytes=64 << 20, transport=None):
         self.engine = engine
         self.ptr = lib().ptls_hip_pipeline_new(engine.ptr, slice_bytes)
         if not self.ptr:
             raise HipError(f"ptls_hip_pipeline_new: {last_error()}")
+        if transport is not None:
+            self.set_transport(transport)
+
+    def set_transport(self, transport):
+        """TRANSPORT_AUTO / TRANSPORT_COPY (copy engines + device staging) / TRANSPORT_MAPPED (kernels on the pinned host buffers)"""
+        _check(lib().ptls_hip_pipeline_set_transport(self.ptr, transport), "pipeline_set_transport")
+
+    @property
+    def last_transport(self):
+        return lib().ptls_hip_pipeline_last_transport(self.ptr)
 
     def seal(self, keyset, recs, h_in, h_aad, h_out):
         recs = np.ascontiguousarray(recs, dtype=RECORD_DTYPE)

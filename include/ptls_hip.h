@@ -307,6 +307,17 @@ int ptls_hip_pipeline_tls13_seal(ptls_hip_pipeline_t *p, ptls_hip_keyset_t *ks, 
                                  const void *h_in, void *h_wire);
 int ptls_hip_pipeline_tls13_open(ptls_hip_pipeline_t *p, ptls_hip_keyset_t *ks, const ptls_hip_record_t *recs, size_t n,
                                  const void *h_wire, void *h_out, uint64_t *h_result);
+/* How a pipeline moves the bytes.  AUTO (the default): MAPPED when every host buffer of the call (in, out, aad,
+ * mask) is pinned or registered, COPY otherwise.  COPY: the staging described above (copy engines).  MAPPED: no
+ * staging -- the kernels read the records from and write them to the host buffers over PCIe themselves (their
+ * device mappings, hipHostGetDevicePointer), one launch per max-records slice; bytes between records in the
+ * output are then left untouched, as by the device-resident batch calls.  A call in MAPPED mode with an unmapped
+ * buffer fails with PTLS_HIP_EINVAL.  last_transport: what the last seal/open of the pipeline used. */
+#define PTLS_HIP_TRANSPORT_AUTO 0
+#define PTLS_HIP_TRANSPORT_COPY 1
+#define PTLS_HIP_TRANSPORT_MAPPED 2
+int ptls_hip_pipeline_set_transport(ptls_hip_pipeline_t *p, int transport);
+int ptls_hip_pipeline_last_transport(ptls_hip_pipeline_t *p);
 int ptls_hip_host_register(void *ptr, size_t len);
 int ptls_hip_host_unregister(void *ptr);
 

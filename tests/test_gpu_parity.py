@@ -20,6 +20,8 @@ pytestmark = pytest.mark.gpu
 
 torch = pytest.importorskip("torch")
 import ptls_hip  # noqa: E402
+
+TRANSPORTS = {"copy": ptls_hip.TRANSPORT_COPY, "mapped": ptls_hip.TRANSPORT_MAPPED}  # host pipeline transports
 from hip_helpers import HostBatch  # noqa: E402
 from make_golden import CONFIGS, config_record, sweep_inputs  # noqa: E402
 from oracle_lib import tls_aad  # noqa: E402
@@ -459,7 +461,7 @@ def _supp_array(rows):
 
 
 @pytest.mark.parametrize("keys", ["3", "per_packet"])
-@pytest.mark.parametrize("path", ["device", "pipeline"])
+@pytest.mark.parametrize("path", ["device", "copy", "mapped"])
 @pytest.mark.parametrize("key_len", [16, 32])
 def test_seal_batch_quic_header_protection(engine, oracle, key_len, path, keys):
     """QUIC header protection fused into the seal launch (fusion's supp,
@@ -504,9 +506,10 @@ def test_seal_batch_quic_header_protection(engine, oracle, key_len, path, keys):
             supp[i] = row
         p_out = torch.zeros(hb.out_total + 32, dtype=torch.uint8).pin_memory()
         p_mask = torch.zeros(16 * len(recs), dtype=torch.uint8).pin_memory()
-        pipe = ptls_hip.Pipeline(engine, 64 << 10)
+        pipe = ptls_hip.Pipeline(engine, 64 << 10, transport=TRANSPORTS.get(path))
         pipe.seal_supp(hb.keyset, hp, hb.recs, supp, torch.from_numpy(h_in).pin_memory(), torch.from_numpy(h_aad).pin_memory(),
                        p_out, p_mask)
+        assert pipe.last_transport == TRANSPORTS[path]
         pipe.close()
         out, mask = p_out.numpy(), p_mask.numpy()
     for j, (r, rec, (off, k, enabled)) in enumerate(zip(recs, hb.recs, expect)):
@@ -594,10 +597,12 @@ def test_plugin_ctr_cipher_and_fused_supp(engine, oracle):
         drv.cipher_free(cctx)
 
 
+@pytest.mark.parametrize("transport", ["copy", "mapped"])
 @pytest.mark.parametrize("slice_kib", [64, 1024])
-def test_host_pipeline_seal_open(engine, oracle, slice_kib):
-    """host-resident path: records in pinned host memory, sliced, H2D -> kernel -> D2H over 3 streams;
-    mixed lengths, two keys, TLS and QUIC-sized records; bit-exact vs the oracle, then opened back"""
+def test_host_pipeline_seal_open(engine, oracle, slice_kib, transport):
+    """host-resident path: records in pinned host memory, sliced; transport copy = H2D -> kernel -> D2H over 3
+    streams, mapped = the kernels on the host buffers directly; mixed lengths, two keys, TLS and QUIC-sized
+    records; bit-exact vs the oracle, then opened back"""
     rng = np.random.default_rng(3)
     recs_in = []
     for i in range(700):
@@ -618,8 +623,9 @@ def test_host_pipeline_seal_open(engine, oracle, slice_kib):
     for r, rec in zip(recs_in, recs):
         hin[rec["in_off"]: rec["in_off"] + len(r[4])] = np.frombuffer(r[4], np.uint8)
         haad[rec["aad_off"]: rec["aad_off"] + 5] = np.frombuffer(r[3], np.uint8)
-    pipe = ptls_hip.Pipeline(engine, slice_kib << 10)
+    pipe = ptls_hip.Pipeline(engine, slice_kib << 10, transport=TRANSPORTS[transport])
     pipe.seal(ks, recs, h_in, h_aad, h_out)
+    assert pipe.last_transport == TRANSPORTS[transport]
     hout = h_out.numpy()
     sealed = []
     for r, rec in zip(recs_in, recs):

@@ -14,8 +14,10 @@ pytestmark = pytest.mark.gpu
 
 torch = pytest.importorskip("torch")
 import ptls_hip  # noqa: E402
+
 from oracle_lib import Ref, RefTLS, ref_traffic_keys, tls13_wire  # noqa: E402
 
+TRANSPORTS = {"copy": ptls_hip.TRANSPORT_COPY, "mapped": ptls_hip.TRANSPORT_MAPPED}  # host pipeline transports
 needs_ref = pytest.mark.skipif(not Ref.available, reason="oracle/_ref (reference build) not present")
 
 
@@ -27,7 +29,7 @@ def conn_secrets(bits, n, seed):
 
 
 @needs_ref
-@pytest.mark.parametrize("path", ["device", "pipeline"])
+@pytest.mark.parametrize("path", ["device", "copy", "mapped"])
 @pytest.mark.parametrize("bits", [128, 256])
 def test_tls13_seal_batch_equals_ptls_send(engine, oracle, bits, path):
     """many connections x messages of 0..40000 bytes and three content types, framed + sealed in one
@@ -76,8 +78,9 @@ def test_tls13_seal_batch_equals_ptls_send(engine, oracle, bits, path):
     else:  # host-resident: pinned message buffer -> pinned wire buffer, 64 KiB slices (many slices, 3 streams)
         p_in = torch.from_numpy(h_in).pin_memory()
         p_out = torch.zeros(out_off + 3 * len(msgs) + 16, dtype=torch.uint8).pin_memory()
-        pipe = ptls_hip.Pipeline(engine, 64 << 10)
+        pipe = ptls_hip.Pipeline(engine, 64 << 10, transport=TRANSPORTS.get(path))
         pipe.tls13_seal(ks, recs, p_in, p_out)
+        assert pipe.last_transport == TRANSPORTS[path]
         pipe.close()
         out = p_out.numpy()
     for i, (m, wire) in enumerate(zip(marr, expect)):
@@ -91,7 +94,7 @@ def test_tls13_seal_batch_equals_ptls_send(engine, oracle, bits, path):
 
 
 @needs_ref
-@pytest.mark.parametrize("path", ["device", "pipeline"])
+@pytest.mark.parametrize("path", ["device", "copy", "mapped"])
 @pytest.mark.parametrize("bits", [128, 256])
 def test_tls13_open_batch_equals_ptls_receive(engine, oracle, bits, path):
     """a received byte stream (ptls_send output, plus records with TLSInnerPlaintext padding, an all-zero
@@ -140,8 +143,9 @@ def test_tls13_open_batch_equals_ptls_receive(engine, oracle, bits, path):
         p_in = torch.from_numpy(np.frombuffer(stream + bytes(16), np.uint8).copy()).pin_memory()
         p_out = torch.zeros(out_size, dtype=torch.uint8).pin_memory()
         p_res = torch.zeros(len(recs), dtype=torch.int64).pin_memory()
-        pipe = ptls_hip.Pipeline(engine, 64 << 10)
+        pipe = ptls_hip.Pipeline(engine, 64 << 10, transport=TRANSPORTS.get(path))
         pipe.tls13_open(ks, recs, p_in, p_out, p_res)
+        assert pipe.last_transport == TRANSPORTS[path]
         pipe.close()
         out = p_out.numpy()
         res = [int(x) & ((1 << 64) - 1) for x in p_res.numpy()]

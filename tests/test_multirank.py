@@ -96,7 +96,7 @@ def test_bench_launches_its_own_ranks():
     assert r["per_rank"][1]["seconds"] > r["per_rank"][0]["seconds"]  # rank 1 sleeps twice as long
     total = 2 * 2 * 2048 * 1350 * 3 / (1 << 30)  # ranks x (seal + open) x bytes x steps
     assert abs(r["value"] - total / (r["ms_per_step"] * 3 / 1e3)) / r["value"] < 0.02
-    assert r["ms_per_step"] * 3 / 1e3 >= slow
+    assert r["ms_per_step"] * 3 / 1e3 >= slow - 1e-3  # the max over ranks (JSON fields are rounded)
 
 
 def test_bench_rejects_a_world_size_mismatch():

@@ -1,15 +1,24 @@
 #!/bin/bash
-# build a tuning variant of the engine with extra defines:
+# build a tuning / ablation variant of the engine with extra defines:
 #   EXTRA="-DWG_ALT=768 -DPURE_BLOCKS=2" tools/build_variant.sh <name>  ->  hsig-picotls_amd/variants/libptls_hip_<name>.so
+# SRCS (optional) = the kernel sources that get EXTRA (default: all); the others reuse the product build's objects.
 set -e
 cd "$(dirname "$0")/../hsig-picotls_amd"
+make -s -j8 libptls_hip.so >/dev/null
 name=$1; out=variants/libptls_hip_${name}.so
+ALL="aesgcm_kernels sparse_kernel batch_g1 batch_g2 batch_g4 batch_g8 batch_g16"
+SRCS=${SRCS:-$ALL}
 mkdir -p variants/build_${name}
-for src in aesgcm_kernels sparse_kernel batch_g1 batch_g2 batch_g4 batch_g8 batch_g16; do
-  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC $EXTRA -I../include -Icsrc -c csrc/$src.hip -o variants/build_${name}/$src.o &
+objs=""
+for src in $ALL; do
+  if [[ " $SRCS " == *" $src "* ]]; then
+    /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC $EXTRA -I../include -Icsrc -c csrc/$src.hip -o variants/build_${name}/$src.o &
+    objs="$objs variants/build_${name}/$src.o"
+  else
+    objs="$objs build/$src.o"
+  fi
 done
 wait
 g++ -std=c++17 -O2 -fPIC -D__HIP_PLATFORM_AMD__ $EXTRA -I/opt/rocm/include -I../include -Icsrc -c csrc/engine.cpp -o variants/build_${name}/e.o
-[ -f build/keyschedule.o ] || make -s build/keyschedule.o
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $out variants/build_${name}/aesgcm_kernels.o variants/build_${name}/batch_g*.o variants/build_${name}/sparse_kernel.o build/keyschedule.o variants/build_${name}/e.o -L/opt/rocm/lib -lamdhip64 -Wl,-rpath,/opt/rocm/lib
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $out $objs build/keyschedule.o variants/build_${name}/e.o -L/opt/rocm/lib -lamdhip64 -Wl,-rpath,/opt/rocm/lib
 echo "built $out"
