@@ -326,8 +326,8 @@ __device__ __forceinline__ V4 last_finish(const RoundLoads &r, const uint32_t *_
 /* forward declarations of the GHASH pieces (defined below) */
 struct GhLane;
 __device__ __forceinline__ V4 gh_rot(const GhLane &g, V4 y);
-template <int T0, int NT>
-__device__ __forceinline__ void gh_issue(const uint8_t *lds, const GhLane &g, const V4 &xr, V4 (&G)[8]);
+template <int T0, int NT, int NG>
+__device__ __forceinline__ void gh_issue(const uint8_t *lds, const GhLane &g, const V4 &xr, V4 (&G)[NG]);
 
 /* Keystream of KP counter blocks (counter-mode shortcut for rounds 1-2, as aes_ctr_n) and, when HASH,
  * y <- (...(y * P ^ hx[0]) * P ^ ...) ^ hx[KP-1]: multiply j spread over phases 4j+1 .. 4j+4. */
@@ -423,22 +423,25 @@ __device__ __forceinline__ void ctr_ghash_phased(const uint8_t *lds, uint32_t lb
 /* SKEWED=1 variant of ctr_ghash_phased: the lane's KP blocks run 1/KP of a round apart, so a wave always
  * has lookups in flight while it XORs.  Segment s issues a quarter GHASH multiply (s < 4 KP) and round
  * s/KP+1 of block s%KP, then finishes the round that block (s-KP+1)%KP issued KP-1 segments earlier and
- * folds in the quarter multiply (its lookups go out first, so the fold does not wait for the AES ones). */
-template <int ROUNDS, int KP, bool HASH>
+ * folds in the quarter multiply (its lookups go out first, so the fold does not wait for the AES ones).
+ * GH = the multiply's table, issued in GH::PARTS parts of 4 lookups: GhMain (the batch kernel's 8-bit windows,
+ * 4 parts) or GhNibble (the sparse kernel's per-wave 4-bit windows, 8 parts), defined with the GHASH helpers. */
+template <int ROUNDS, int KP, bool HASH, class GH>
 __device__ __forceinline__ void ctr_ghash_skewed(const uint8_t *lds, uint32_t lb, const uint32_t *__restrict__ rk, const CtrConst &cc,
-                                                 const uint32_t (&cw)[KP], V4 (&ks)[KP], V4 &y, const V4 (&hx)[KP], const GhLane &g)
+                                                 const uint32_t (&cw)[KP], V4 (&ks)[KP], V4 &y, const V4 (&hx)[KP], const GH &gm)
 {
-    static_assert(4 * KP <= KP * ROUNDS, "GHASH quarters must fit in the segments");
+    constexpr int P = GH::PARTS; /* issue parts (4 lookups each) per GHASH multiply */
+    static_assert(P * KP <= KP * ROUNDS, "GHASH parts must fit in the segments");
     V4 s[KP];
     uint32_t t0[KP], t1[KP];
     RoundLoads R[KP];
     uint32_t M[KP][8];
-    V4 G[8];
+    V4 G[4];
     V4 acc = V4{0, 0, 0, 0}, xr = V4{0, 0, 0, 0};
     constexpr int NSEG = KP * ROUNDS + KP - 1;
 #pragma unroll
     for (int seg = 0; seg < NSEG; ++seg) {
-        const int gj = seg >> 2, gq = seg & 3;
+        const int gj = seg / P, gq = seg % P;
         const bool gh = HASH && gj < KP;
 #if SETPRIO
         __builtin_amdgcn_s_setprio(SETPRIO); /* a wave about to issue lookups goes first */
@@ -446,14 +449,18 @@ __device__ __forceinline__ void ctr_ghash_skewed(const uint8_t *lds, uint32_t lb
         /* ---- issue: GHASH quarter first, then the AES lookups (so the fold below need not wait for them) ---- */
         if (gh) {
             if (gq == 0) {
-                xr = gh_rot(g, y);
+                xr = gm.prep(y);
                 acc = hx[gj];
             }
-            switch (gq) {
-            case 0: gh_issue<0, 4>(lds, g, xr, G); break;
-            case 1: gh_issue<4, 4>(lds, g, xr, G); break;
-            case 2: gh_issue<8, 4>(lds, g, xr, G); break;
-            default: gh_issue<12, 4>(lds, g, xr, G); break;
+            switch (gq) { /* gq is a constant once the segment loop is unrolled */
+            case 0: gm.template issue<0>(lds, xr, G); break;
+            case 1: gm.template issue<1>(lds, xr, G); break;
+            case 2: gm.template issue<2>(lds, xr, G); break;
+            case 3: gm.template issue<3 % P>(lds, xr, G); break;
+            case 4: gm.template issue<4 % P>(lds, xr, G); break;
+            case 5: gm.template issue<5 % P>(lds, xr, G); break;
+            case 6: gm.template issue<6 % P>(lds, xr, G); break;
+            default: gm.template issue<7 % P>(lds, xr, G); break;
             }
         }
         __builtin_amdgcn_sched_barrier(0);
@@ -503,21 +510,11 @@ __device__ __forceinline__ void ctr_ghash_skewed(const uint8_t *lds, uint32_t lb
         if (gh) {
             acc = v4xor3(acc, G[0], G[1]);
             acc = v4xor3(acc, G[2], G[3]);
-            if (gq == 3)
+            if (gq == P - 1)
                 y = acc;
         }
         __builtin_amdgcn_sched_barrier(0);
     }
-}
-
-template <int ROUNDS, int KP, bool HASH>
-__device__ __forceinline__ void ctr_ghash(const uint8_t *lds, uint32_t lb, const uint32_t *__restrict__ rk, const CtrConst &cc,
-                                          const uint32_t (&cw)[KP], V4 (&ks)[KP], V4 &y, const V4 (&hx)[KP], const GhLane &g)
-{
-    if constexpr (SKEWED)
-        ctr_ghash_skewed<ROUNDS, KP, HASH>(lds, lb, rk, cc, cw, ks, y, hx, g);
-    else
-        ctr_ghash_phased<ROUNDS, KP, HASH>(lds, lb, rk, cc, cw, ks, y, hx, g);
 }
 
 /* K independent blocks, round-interleaved */
@@ -628,9 +625,10 @@ __device__ __forceinline__ V4 gh_rot(const GhLane &g, V4 y)
               __builtin_amdgcn_alignbit(r3, r2, g.shift), __builtin_amdgcn_alignbit(r0, r3, g.shift)};
 }
 
-template <int T0, int NT>
-__device__ __forceinline__ void gh_issue(const uint8_t *lds, const GhLane &g, const V4 &xr, V4 (&G)[8])
+template <int T0, int NT, int NG>
+__device__ __forceinline__ void gh_issue(const uint8_t *lds, const GhLane &g, const V4 &xr, V4 (&G)[NG])
 {
+    static_assert(NT <= NG, "lookups must fit the result array");
 #pragma unroll
     for (int i = 0; i < NT; ++i) {
         const int t = T0 + i, q = t >> 2;
@@ -639,6 +637,44 @@ __device__ __forceinline__ void gh_issue(const uint8_t *lds, const GhLane &g, co
         const uint32_t addr = __builtin_amdgcn_perm(xw, lbw, 0x0c0c0000u | ((4u + (t & 3)) << 8) | (t & 3));
         G[i] = lds128(lds, LDS_GMAIN + addr);
     }
+}
+
+/* GHASH-multiply policies of ctr_ghash_skewed: the issue of part Q (4 ds_read_b128) of one multiply of y */
+struct GhMain { /* the batch kernel's 8-bit-window table of P at LDS_GMAIN: 16 lookups = 4 parts (one word of rotated y each) */
+    const GhLane &g;
+    static constexpr int PARTS = 4;
+    __device__ __forceinline__ V4 prep(V4 y) const { return gh_rot(g, y); }
+    template <int Q>
+    __device__ __forceinline__ void issue(const uint8_t *lds, const V4 &xr, V4 (&G)[4]) const
+    {
+        gh_issue<4 * Q, 4>(lds, g, xr, G);
+    }
+};
+
+struct GhNibble { /* a 4-bit-window table [p = 8w + j][v] at LDS offset tab (gh_mul_nibble's layout): 32 lookups = 8 parts */
+    uint32_t tab;
+    static constexpr int PARTS = 8;
+    __device__ __forceinline__ V4 prep(V4 y) const { return y; }
+    template <int Q>
+    __device__ __forceinline__ void issue(const uint8_t *lds, const V4 &xr, V4 (&G)[4]) const
+    {
+        const uint32_t w = (Q >> 1) == 0 ? xr.w0 : (Q >> 1) == 1 ? xr.w1 : (Q >> 1) == 2 ? xr.w2 : xr.w3;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int j = 4 * (Q & 1) + i; /* nibble j of word Q / 2 */
+            G[i] = lds128(lds, tab + (uint32_t)(8 * (Q >> 1) + j) * 256u + ((w >> (4 * j)) & 15u) * 16u);
+        }
+    }
+};
+
+template <int ROUNDS, int KP, bool HASH>
+__device__ __forceinline__ void ctr_ghash(const uint8_t *lds, uint32_t lb, const uint32_t *__restrict__ rk, const CtrConst &cc,
+                                          const uint32_t (&cw)[KP], V4 (&ks)[KP], V4 &y, const V4 (&hx)[KP], const GhLane &g)
+{
+    if constexpr (SKEWED)
+        ctr_ghash_skewed<ROUNDS, KP, HASH>(lds, lb, rk, cc, cw, ks, y, hx, GhMain{g});
+    else
+        ctr_ghash_phased<ROUNDS, KP, HASH>(lds, lb, rk, cc, cw, ks, y, hx, g);
 }
 
 /* y * P with a nibble table [p = 8w + j][v] (used only in the per-record reduction tree).  One word

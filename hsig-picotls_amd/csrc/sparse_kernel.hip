@@ -19,6 +19,8 @@
  *   - a Horner multiply is 32 ds_read_b128 (gh_mul_nibble); AES-CTR uses the batch kernel's 32x-replicated
  *     T-tables (64 KiB) and round keys through the scalar unit.  64 KiB + 12 x 8 KiB = the CU's 160 KiB.
  */
+#include <type_traits>
+
 #include "batch_kernel.h"
 
 namespace ptls_hip {
@@ -28,6 +30,12 @@ namespace ptls_hip {
 #endif
 #ifndef SPARSE_ABLATE
 #define SPARSE_ABLATE 0 /* timing ablation only (wrong output): 1 = no final lane combination, 2 = no main-loop multiply, 3 = no H^64 table build */
+#endif
+#ifndef SPARSE_GEN_SKEW
+#define SPARSE_GEN_SKEW 1 /* generic elements through the skewed counter-mode AES (1: c4s seal +1.5 %, open +4 %) or aes_ctr_n (0) */
+#endif
+#ifndef SPARSE_PURE
+#define SPARSE_PURE 1 /* the branch-free skewed stretch over full blocks (0: every element on the generic path) */
 #endif
 #ifndef SPARSE_PE
 #define SPARSE_PE 2 /* GHASH elements (AES blocks) per lane per main-loop iteration */
@@ -73,12 +81,25 @@ __device__ __forceinline__ void store_wave_table(uint8_t *lds, uint32_t tab, con
     const int p = lane >> 1;
     const V4 hi = (lane & 1) ? b[3] : V4{0, 0, 0, 0};
     const uint32_t row = tab + (uint32_t)p * 256u + (uint32_t)(lane & 1) * 128u;
-    const V4 b01 = v4xor(b[0], b[1]);
+    /* the 8 lanes of a ds_write_b128 group write rows 128 B apart, i.e. the same banks: each lane walks its eight
+     * entries from its own start ((k + lane) & 7), so the group's eight addresses fall in eight distinct 16-B bank
+     * quads (conflict-free); the entry's basis combination follows its low three value bits as masks */
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
-        const V4 lo = (k & 3) == 0 ? V4{0, 0, 0, 0} : (k & 3) == 1 ? b[0] : (k & 3) == 2 ? b[1] : b01;
-        const V4 e = (k & 4) ? v4xor3(hi, lo, b[2]) : v4xor(hi, lo);
-        lds128_store(lds, row + (uint32_t)k * 16u, e);
+        const uint32_t v = (uint32_t)(k + lane) & 7u;
+        const uint32_t m0 = 0u - (v & 1u), m1 = 0u - ((v >> 1) & 1u), m2 = 0u - (v >> 2);
+        const uint32_t hw[4] = {hi.w0, hi.w1, hi.w2, hi.w3};
+        uint32_t e[4];
+#pragma unroll
+        for (int w = 0; w < 4; ++w) {
+            const uint32_t b0 = w == 0 ? b[0].w0 : w == 1 ? b[0].w1 : w == 2 ? b[0].w2 : b[0].w3;
+            const uint32_t b1 = w == 0 ? b[1].w0 : w == 1 ? b[1].w1 : w == 2 ? b[1].w2 : b[1].w3;
+            const uint32_t b2 = w == 0 ? b[2].w0 : w == 1 ? b[2].w1 : w == 2 ? b[2].w2 : b[2].w3;
+            uint32_t z = __builtin_amdgcn_bitop3_b32(hw[w], m0, b0, 0x78); /* z ^ (m & b) */
+            z = __builtin_amdgcn_bitop3_b32(z, m1, b1, 0x78);
+            e[w] = __builtin_amdgcn_bitop3_b32(z, m2, b2, 0x78);
+        }
+        lds128_store(lds, row + v * 16u, V4{e[0], e[1], e[2], e[3]});
     }
 }
 
@@ -110,7 +131,7 @@ __global__ void __launch_bounds__(SPARSE_WG)
     static_assert(SP_TAB + (SPARSE_WG / 64) * 8192 <= 163840, "AES tables + per-wave GHASH tables must fit the CU's 160 KiB");
     const int lane = threadIdx.x & 63;
     const uint32_t lb_aes = (uint32_t)(lane & 31) * 4u; /* table base 0: byte 2 of the address is 0 */
-    const uint32_t tab = SP_TAB + (uint32_t)(threadIdx.x >> 6) * 8192u;
+    const uint32_t tab = __builtin_amdgcn_readfirstlane(SP_TAB + (uint32_t)(threadIdx.x >> 6) * 8192u); /* wave-uniform */
     build_aes_tables_at0(lds, t0);
     __syncthreads();
     if (nchunks == 0)
@@ -137,12 +158,22 @@ __global__ void __launch_bounds__(SPARSE_WG)
         const uint8_t *in_p = in + rec.in_off;
         uint8_t *out_p = out + rec.out_off;
         const uint8_t *aad_p = aad + rec.aad_off;
-        const uint32_t n0 = slot->iv[0], n1 = slot->iv[1] ^ bswap32((uint32_t)(rec.seq >> 32)),
-                       n2 = slot->iv[2] ^ bswap32((uint32_t)rec.seq);
-        const CtrConst cc = ctr_const(lds, lb_aes, rk, n0, n1, n2);
+        const uint32_t n0 = __builtin_amdgcn_readfirstlane(slot->iv[0]),
+                       n1 = __builtin_amdgcn_readfirstlane(slot->iv[1] ^ bswap32((uint32_t)(rec.seq >> 32))),
+                       n2 = __builtin_amdgcn_readfirstlane(slot->iv[2] ^ bswap32((uint32_t)rec.seq));
+        /* the record (and so its counter-mode constants) is the wave's alone: keep them in SGPRs */
+        CtrConst cc = ctr_const(lds, lb_aes, rk, n0, n1, n2);
+        cc.k10 = __builtin_amdgcn_readfirstlane(cc.k10);
+        cc.k11 = __builtin_amdgcn_readfirstlane(cc.k11);
+        cc.k20 = __builtin_amdgcn_readfirstlane(cc.k20);
+        cc.k21 = __builtin_amdgcn_readfirstlane(cc.k21);
+        cc.k22 = __builtin_amdgcn_readfirstlane(cc.k22);
+        cc.k23 = __builtin_amdgcn_readfirstlane(cc.k23);
+        cc.r03 = __builtin_amdgcn_readfirstlane(cc.r03);
         const int iters = (N + 63) >> 6;
         wave_lds_sync(); /* the previous record's Horner reads of the table are done */
         if (SPARSE_ABLATE != 3 && iters > 1) { /* N <= 64: one element per lane, no Horner step */
+            /* (loading these during the previous record's VALU combine measured no faster: other waves hide it) */
             V4 b[4];
             load_wave_basis(bs + 6 * 128, lane, b); /* H^64 */
             store_wave_table(lds, tab, b, lane);
@@ -150,15 +181,17 @@ __global__ void __launch_bounds__(SPARSE_WG)
         wave_lds_sync();
 
         V4 y = V4{0, 0, 0, 0}, ek0 = V4{0, 0, 0, 0};
-        /* elements m .. m + SPARSE_PE - 1 of the lane (past `iters`: inactive), their AES blocks interleaved */
-        for (int m = 0; m < iters; m += SPARSE_PE) {
-            Elem e[SPARSE_PE];
-            V4 inb[SPARSE_PE], ks[SPARSE_PE];
-            uint32_t cw[SPARSE_PE];
+        /* generic elements m .. m + NE - 1 of the lane (past `mend`: skipped): partial / AAD / length blocks and
+         * counters >= 2^16, their AES blocks interleaved (counter-mode shortcut unless a counter is that large) */
+        auto generic = [&](auto ne_tag, int m, int mend) __attribute__((always_inline)) {
+            constexpr int NE = decltype(ne_tag)::value;
+            Elem e[NE];
+            V4 inb[NE], ks[NE];
+            uint32_t cw[NE];
             int big = 0;
 #pragma unroll
-            for (int b = 0; b < SPARSE_PE; ++b) {
-                e[b] = elem_of(lane + (m + b) * 64, N, na, nc, L);
+            for (int b = 0; b < NE; ++b) {
+                e[b] = elem_of(m + b < mend ? lane + (m + b) * 64 : N, N, na, nc, L);
                 inb[b] = V4{0, 0, 0, 0};
                 if (e[b].is_c) {
                     const bool tb = tflag && e[b].c == nc - 1; /* the block holding the content-type byte */
@@ -171,19 +204,113 @@ __global__ void __launch_bounds__(SPARSE_WG)
                 ks[b] = V4{n0, n1, n2, cw[b]};
                 big |= (e[b].is_c && e[b].c >= 65534) ? 1 : 0;
             }
-            if (wave_max(big))
-                aes_encrypt_n<ROUNDS, SPARSE_PE>(lds, lb_aes, rk, ks);
-            else
-                aes_ctr_n<ROUNDS, SPARSE_PE>(lds, lb_aes, rk, cc, cw, ks);
+            if (wave_max(big)) {
+                aes_encrypt_n<ROUNDS, NE>(lds, lb_aes, rk, ks);
+            } else if (!SPARSE_GEN_SKEW) {
+                aes_ctr_n<ROUNDS, NE>(lds, lb_aes, rk, cc, cw, ks);
+            } else {
+                const V4 nohash[NE] = {};
+                V4 ydummy = V4{0, 0, 0, 0};
+                ctr_ghash_skewed<ROUNDS, NE, false>(lds, lb_aes, rk, cc, cw, ks, ydummy, nohash, GhNibble{tab});
+            }
 #pragma unroll
-            for (int b = 0; b < SPARSE_PE; ++b) {
+            for (int b = 0; b < NE; ++b) {
                 const V4 x = finish_elem<OPEN, ALIGNED>(e[b], inb[b], ks[b], aad_p, A, L, out_p, ek0);
                 if (m + b == 0)
                     y = x; /* 0 * P ^ x */
                 else if (SPARSE_ABLATE != 2 && e[b].active)
                     y = v4xor(gh_mul_nibble(lds, tab, y), x); /* y * H^64 ^ x */
             }
+        };
+        auto generic_range = [&](int m0, int m1) __attribute__((always_inline)) {
+            int m = m0;
+            for (; m + 1 < m1; m += 2)
+                generic(std::integral_constant<int, 2>{}, m, m1);
+            if (m < m1)
+                generic(std::integral_constant<int, 1>{}, m, m1);
+        };
+
+        /* the wave's "pure" elements m in [pm0, pm1): every lane's element is a full data block with a counter below
+         * 2^16 (lane l, element m = data block 64 m + l - na).  There the body is branch-free, KP blocks per lane per
+         * iteration, the counter-mode AES of the blocks skewed against the H^64 multiplies of the previous iteration's
+         * ciphertext (seal) or of the input ciphertext (open), the next iteration's plaintext prefetched. */
+        constexpr int KP = SPARSE_PE;
+        const int nf = (L - (tflag ? 1 : 0)) >> 4;              /* full blocks that are all input bytes */
+        const int lastc = min(nf, 65534) - 1;                   /* last data block allowed in the stretch */
+        const int pm0 = (na + 63) >> 6;                         /* first m whose element is data on lane 0 */
+        const int mhi = lastc + na - 63 >= 0 ? ((lastc + na - 63) >> 6) + 1 : 0; /* m < mhi: lane 63's block <= lastc */
+        const int npure = SPARSE_PURE && mhi > pm0 ? (mhi - pm0) / KP : 0;
+        const int pm1 = pm0 + npure * KP;
+        generic_range(0, pm0);
+        if (npure) {
+            const int c0 = 64 * pm0 + lane - na; /* the lane's first data block of the stretch */
+            const uint8_t *src = in_p + 16 * (size_t)c0;
+            uint8_t *dst = out_p + 16 * (size_t)c0;
+            V4 pend[KP], bufA[KP], bufB[KP];
+            /* open hashes its input in the iteration that loads it: the next iteration's blocks are prefetched into the
+             * other buffer.  Seal uses its plaintext only after the iteration's AES, so it loads at the top of the
+             * iteration into one buffer (8 VGPRs fewer: the seal instantiations stay within 168 without scratch). */
+#pragma unroll
+            for (int b = 0; b < KP; ++b)
+                bufA[b] = load_full(src + 1024 * b);
+            auto pure_iter = [&](int it, bool hash_pending, V4(&d)[KP], V4(&dn)[KP]) __attribute__((always_inline)) {
+                const size_t o = (size_t)it * KP * 1024;
+                const size_t on = (size_t)min(it + 1, npure - 1) * KP * 1024;
+                V4 k[KP];
+                uint32_t cw[KP];
+#pragma unroll
+                for (int b = 0; b < KP; ++b) {
+                    if (OPEN)
+                        dn[b] = load_full(src + on + 1024 * b);
+                    else if (it != 0)
+                        d[b] = load_full(src + o + 1024 * b);
+                    cw[b] = bswap32((uint32_t)(c0 + 2 + (it * KP + b) * 64));
+                    k[b] = V4{n0, n1, n2, cw[b]};
+                }
+                __builtin_amdgcn_sched_barrier(0); /* keep the loads at the top of the iteration */
+                if (SPARSE_ABLATE == 2) {
+                    ctr_ghash_skewed<ROUNDS, KP, false>(lds, lb_aes, rk, cc, cw, k, y, d, GhNibble{tab});
+#pragma unroll
+                    for (int b = 0; b < KP; ++b) {
+                        pend[b] = v4xor(d[b], k[b]);
+                        store_full(dst + o + 1024 * b, pend[b]);
+                    }
+                } else if (OPEN) {
+                    ctr_ghash_skewed<ROUNDS, KP, true>(lds, lb_aes, rk, cc, cw, k, y, d, GhNibble{tab});
+#pragma unroll
+                    for (int b = 0; b < KP; ++b)
+                        store_full(dst + o + 1024 * b, v4xor(d[b], k[b]));
+                } else {
+                    if (hash_pending)
+                        ctr_ghash_skewed<ROUNDS, KP, true>(lds, lb_aes, rk, cc, cw, k, y, pend, GhNibble{tab});
+                    else
+                        ctr_ghash_skewed<ROUNDS, KP, false>(lds, lb_aes, rk, cc, cw, k, y, pend, GhNibble{tab});
+#pragma unroll
+                    for (int b = 0; b < KP; ++b) {
+                        pend[b] = v4xor(d[b], k[b]);
+                        store_full(dst + o + 1024 * b, pend[b]);
+                    }
+                }
+            };
+            if (OPEN) {
+                pure_iter(0, false, bufA, bufB);
+                int it = 1;
+                for (; it + 1 < npure; it += 2) {
+                    pure_iter(it, true, bufB, bufA);
+                    pure_iter(it + 1, true, bufA, bufB);
+                }
+                if (it < npure)
+                    pure_iter(it, true, bufB, bufA);
+            } else {
+                pure_iter(0, false, bufA, bufA);
+                for (int it = 1; it < npure; ++it)
+                    pure_iter(it, true, bufA, bufA);
+#pragma unroll
+                for (int b = 0; b < KP; ++b)
+                    y = v4xor(gh_mul_nibble(lds, tab, y), pend[b]);
+            }
         }
+        generic_range(pm1, iters);
 
         /* lane l's sum times H^(q+1), q = distance of its last element from the end of the GHASH input, on the
          * VALU; the XOR butterfly then sums the 64 lanes (ghash_combine) */
