@@ -276,6 +276,8 @@ int launch_batch(int lanes, int rounds, bool open, int wg, unsigned grid, void *
         return launch_batch_g8(rounds, open, wg, grid, stream, a, aligned);
     case 16:
         return launch_batch_g16(rounds, open, wg, grid, stream, a, aligned);
+    case 32:
+        return launch_batch_g32(rounds, open, wg, grid, stream, a, aligned);
     case SPARSE_LANES:
         return launch_batch_sparse(rounds, open, grid, stream, a, aligned);
     default:

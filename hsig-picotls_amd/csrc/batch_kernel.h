@@ -67,6 +67,9 @@ __host__ __device__ constexpr uint32_t lds_bytes(int log2g)
                        power table) and an XOR butterfly instead of the log2(G)-level LDS nibble-table tree.
                        Parity-green, measured c2 / c4 equal and c3 -4 %; the sparse kernel uses it. */
 #endif
+#ifndef GEN_MASK
+#define GEN_MASK 0 /* 1: a generic element's AES runs under the exec mask of the lanes whose element is in the record */
+#endif
 #ifndef PURE_BLOCKS
 #define PURE_BLOCKS 2 /* data blocks per lane per iteration of the branch-free loop */
 #endif
@@ -741,22 +744,42 @@ __device__ void build_aes_tables(uint8_t *lds, const uint32_t *__restrict__ t0)
 }
 
 /* GHASH tables of one key slot.  basis = uint4[NPOW][128], basis[t][e] = H^(2^t) * x^e (GCM bit
- * index e: byte e/8, bit 7 - e%8).  Raw byte p, bit t  <->  e = 8p + 7 - t. */
-__device__ void build_ghash_tables(uint8_t *lds, const uint32_t *__restrict__ basis, int log2g)
+ * index e: byte e/8, bit 7 - e%8).  Raw byte p, bit t  <->  e = 8p + 7 - t.  tree: also the nibble tables of
+ * the shuffle-tree combination (not needed when the lanes combine on the VALU).
+ * Main table: thread (p = tid & 15, hv = tid >> 4) of the first 256 writes the 16 entries v = 16 hv + lv of
+ * position p: 4 + popcount(hv) basis loads, the 16 low-nibble combinations in Gray-code order, and
+ * stores whose 8-lane groups hold 8 different positions p, i.e. 8 different bank quads (conflict-free).
+ * (Per entry from up to 8 basis loads with lanes 256 B apart cost a key switch 8x the loads and 8-way store
+ * conflicts.)  The other threads build the tree tables meanwhile. */
+__device__ void build_ghash_tables(uint8_t *lds, const uint32_t *__restrict__ basis, int log2g, bool tree = true)
 {
     const uint32_t *bm = basis + log2g * 128 * 4;
-    for (int e = threadIdx.x; e < 16 * 256; e += blockDim.x) {
-        const int p = e >> 8, v = e & 255;
-        V4 acc = V4{0, 0, 0, 0};
+    const int tid = (int)threadIdx.x;
+    if (tid < 256) {
+        const int p = tid & 15, hv = tid >> 4;
+        V4 lb[4];
+        V4 hi = V4{0, 0, 0, 0};
 #pragma unroll
-        for (int t = 0; t < 8; ++t)
-            if ((v >> t) & 1)
-                acc = v4xor(acc, ld_basis(bm, 8 * p + 7 - t));
-        lds128_store(lds, LDS_GMAIN + v * 256 + p * 16, acc);
+        for (int t = 0; t < 4; ++t)
+            lb[t] = ld_basis(bm, 8 * p + 7 - t);
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+            if ((hv >> t) & 1)
+                hi = v4xor(hi, ld_basis(bm, 8 * p + 7 - (4 + t)));
+        /* low nibble in Gray-code order: each entry is the previous one with one basis vector toggled */
+        V4 cur = hi;
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            if (k != 0)
+                cur = v4xor(cur, lb[__builtin_ctz(k)]); /* bit that flips between Gray codes k - 1 and k */
+            const int lv = k ^ (k >> 1);
+            lds128_store(lds, LDS_GMAIN + (uint32_t)(16 * hv + lv) * 256u + (uint32_t)p * 16u, cur);
+        }
     }
     /* H^(2^d) for the tree levels d < log2 G (at most H^4); d = 0 (H) always */
-    const int ntree = log2g < 1 ? 1 : log2g > TREE_TABLES ? TREE_TABLES : log2g;
-    for (int e = threadIdx.x; e < ntree * 512; e += blockDim.x) {
+    const int ntree = !tree ? 0 : log2g < 1 ? 1 : log2g > TREE_TABLES ? TREE_TABLES : log2g;
+    const int t0 = (int)blockDim.x > 256 ? 256 : 0, nt = (int)blockDim.x - t0;
+    for (int e = tid - t0; e >= 0 && e < ntree * 512; e += nt) {
         const int d = e >> 9, p = (e >> 4) & 31, v = e & 15;
         const int w = p >> 3, j = p & 7;
         const uint32_t *bt = basis + d * 128 * 4;
@@ -956,7 +979,8 @@ __global__ void __launch_bounds__(WGT)
                         const ptls_hip_supp_t *__restrict__ supp, const KeySlot *__restrict__ hp_slots, uint32_t hp_nslots,
                         uint8_t *mask)
 {
-    constexpr int LOG2G = G == 1 ? 0 : G == 2 ? 1 : G == 4 ? 2 : G == 8 ? 3 : 4;
+    constexpr int LOG2G = G == 1 ? 0 : G == 2 ? 1 : G == 4 ? 2 : G == 8 ? 3 : G == 16 ? 4 : 5;
+    static_assert(G >= 1 && G <= 32 && (G & (G - 1)) == 0, "lanes per record: 1, 2, 4, 8, 16 or 32");
     /* DYN_DEAL: the task counter sits after the tables */
     constexpr bool DYN = DYN_DEAL != 0 && SPLIT_PROBE != 1; /* the counter is reset at key switches, which SPLIT_PROBE 1 skips */
     static_assert(lds_bytes(LOG2G) + 16 <= 163840, "tables + task counter must fit the CU's 160 KiB");
@@ -982,7 +1006,7 @@ __global__ void __launch_bounds__(WGT)
         const Chunk ch = chunks[ci];
         if (SPLIT_PROBE != 1 && ch.key != cur_key) {
             __syncthreads();
-            build_ghash_tables(lds, basis + (size_t)ch.key * (BASIS_VECS * 4), LOG2G);
+            build_ghash_tables(lds, basis + (size_t)ch.key * (BASIS_VECS * 4), LOG2G, !(VALU_TREE != 0 || G >= 32));
             if (DYN && threadIdx.x == 0)
                 *task_ctr = 0;
             __syncthreads();
@@ -1072,8 +1096,10 @@ __global__ void __launch_bounds__(WGT)
                     ks[b] = V4{n0, n1, n2, cw[b]};
                     big |= (e[b].is_c && e[b].c >= 65534) ? 1 : 0;
                 }
-                if (SPLIT_PROBE == 2) {
-                } else if (wave_max(big))
+                const bool bigw = wave_max(big) != 0; /* wave-wide, before any lane branches off */
+                const bool act = !GEN_MASK || e[0].active || e[1].active;
+                if (SPLIT_PROBE == 2 || !act) {
+                } else if (bigw)
                     aes_encrypt_n<ROUNDS, 2>(lds, lb_aes, rk, ks);
                 else
 #if GEN_SKEWED
@@ -1106,8 +1132,9 @@ __global__ void __launch_bounds__(WGT)
                 const uint32_t cw0[1] = {e0.is_c ? bswap32((uint32_t)e0.c + 2u) : 0x01000000u};
                 V4 ks0[1] = {V4{n0, n1, n2, cw0[0]}};
 #if GEN_SKEWED
-                if (SPLIT_PROBE == 2) {
-                } else if (!wave_max((e0.is_c && e0.c >= 65534) ? 1 : 0)) {
+                const bool big0 = wave_max((e0.is_c && e0.c >= 65534) ? 1 : 0) != 0;
+                if (SPLIT_PROBE == 2 || (GEN_MASK && !e0.active)) {
+                } else if (!big0) {
                     const V4 nohash[1] = {V4{0, 0, 0, 0}};
                     V4 ydummy = V4{0, 0, 0, 0};
                     ctr_ghash<ROUNDS, 1, false>(lds, lb_aes, rk, cc, cw0, ks0, ydummy, nohash, gl);
@@ -1225,46 +1252,49 @@ __global__ void __launch_bounds__(WGT)
             }
 
             /* combine the G partial sums of each record: position q = distance of a lane's last element
-             * from the end of the GHASH input; sum_q y_q * H^(q+1) by a shuffle tree */
+             * from the end of the GHASH input; sum_q y_q * H^(q+1).  G <= 16: a log2(G)-level shuffle tree over
+             * nibble tables of H, H^2, H^4 in LDS; G = 32 (or VALU_TREE): one VALU multiply per lane by its own
+             * power H^(q+1) (keysetup's list) and an XOR butterfly over the record's lanes */
+            constexpr bool VCOMB = VALU_TREE != 0 || G >= 32;
             const int q = (nc - r) & (G - 1);
-#if VALU_TREE
-            V4 s = V4{0, 0, 0, 0};
-            if (SPLIT_PROBE != 1) {
-                const uint4 hp = reinterpret_cast<const uint4 *>(basis)[(size_t)ch.key * BASIS_VECS + NPOW * 128 + q]; /* H^(q+1) */
-                s = gf_mul_valu(y, V4{hp.x, hp.y, hp.z, hp.w});
+            V4 s; /* the record's GHASH (VCOMB: in every lane; tree: computed below in lane q == 0) */
+            if constexpr (VCOMB) {
+                s = V4{0, 0, 0, 0};
+                if (SPLIT_PROBE != 1) {
+                    const uint4 hp = reinterpret_cast<const uint4 *>(basis)[(size_t)ch.key * BASIS_VECS + NPOW * 128 + q]; /* H^(q+1) */
+                    s = gf_mul_valu(y, V4{hp.x, hp.y, hp.z, hp.w});
 #pragma unroll
-                for (int o = G / 2; o > 0; o >>= 1) {
-                    s.w0 ^= __shfl_xor(s.w0, o, 64);
-                    s.w1 ^= __shfl_xor(s.w1, o, 64);
-                    s.w2 ^= __shfl_xor(s.w2, o, 64);
-                    s.w3 ^= __shfl_xor(s.w3, o, 64);
+                    for (int o = G / 2; o > 0; o >>= 1) {
+                        s.w0 ^= __shfl_xor(s.w0, o, 64);
+                        s.w1 ^= __shfl_xor(s.w1, o, 64);
+                        s.w2 ^= __shfl_xor(s.w2, o, 64);
+                        s.w3 ^= __shfl_xor(s.w3, o, 64);
+                    }
+                }
+            } else {
+#pragma unroll
+                for (int lvl = 0; lvl < (SPLIT_PROBE == 1 ? 0 : LOG2G); ++lvl) {
+                    const int d = 1 << lvl;
+                    const int src = (lane & ~(G - 1)) | ((r - d) & (G - 1));
+                    V4 v;
+                    v.w0 = __shfl(y.w0, src, 64);
+                    v.w1 = __shfl(y.w1, src, 64);
+                    v.w2 = __shfl(y.w2, src, 64);
+                    v.w3 = __shfl(y.w3, src, 64);
+                    V4 w;
+                    if (lvl < TREE_TABLES) {
+                        w = gh_mul_nibble(lds, LDS_GTREE + lvl * LDS_TREE_STRIDE, v);
+                    } else { /* H^8 = H^4 * H^4 */
+                        const uint32_t t4 = LDS_GTREE + (TREE_TABLES - 1) * LDS_TREE_STRIDE;
+                        w = gh_mul_nibble(lds, t4, gh_mul_nibble(lds, t4, v));
+                    }
+                    if ((q & (2 * d - 1)) == 0)
+                        y = v4xor(y, w);
                 }
             }
-#else
-#pragma unroll
-            for (int lvl = 0; lvl < (SPLIT_PROBE == 1 ? 0 : LOG2G); ++lvl) {
-                const int d = 1 << lvl;
-                const int src = (lane & ~(G - 1)) | ((r - d) & (G - 1));
-                V4 v;
-                v.w0 = __shfl(y.w0, src, 64);
-                v.w1 = __shfl(y.w1, src, 64);
-                v.w2 = __shfl(y.w2, src, 64);
-                v.w3 = __shfl(y.w3, src, 64);
-                V4 w;
-                if (lvl < TREE_TABLES) {
-                    w = gh_mul_nibble(lds, LDS_GTREE + lvl * LDS_TREE_STRIDE, v);
-                } else { /* H^8 = H^4 * H^4 */
-                    const uint32_t t4 = LDS_GTREE + (TREE_TABLES - 1) * LDS_TREE_STRIDE;
-                    w = gh_mul_nibble(lds, t4, gh_mul_nibble(lds, t4, v));
-                }
-                if ((q & (2 * d - 1)) == 0)
-                    y = v4xor(y, w);
-            }
-#endif
             if (valid && q == 0) {
-#if !VALU_TREE
-                const V4 s = gh_mul_nibble(lds, LDS_GTREE, y); /* * H */
-#endif
+                if constexpr (!VCOMB)
+                    s = gh_mul_nibble(lds, LDS_GTREE, y); /* * H */
                 const V4 tag = v4xor(s, ek0);
                 if (OPEN) {
                     const V4 rt = load_full(in_p + L);

@@ -577,8 +577,9 @@ extern "C" size_t ptls_hip_batch_count(ptls_hip_batch_t *b)
 
 extern "C" int ptls_hip_batch_set_lanes(ptls_hip_batch_t *b, int lanes)
 {
-    if (b == nullptr || !(lanes == 0 || lanes == 1 || lanes == 2 || lanes == 4 || lanes == 8 || lanes == 16 || lanes == SPARSE_LANES))
-        return fail(PTLS_HIP_EINVAL, "batch_set_lanes: lanes must be 0, 1, 2, 4, 8, 16 or 64");
+    if (b == nullptr ||
+        !(lanes == 0 || lanes == 1 || lanes == 2 || lanes == 4 || lanes == 8 || lanes == 16 || lanes == 32 || lanes == SPARSE_LANES))
+        return fail(PTLS_HIP_EINVAL, "batch_set_lanes: lanes must be 0, 1, 2, 4, 8, 16, 32 or 64");
     DeviceGuard g(b->eng->device);
     const int want = lanes == 0 ? b->auto_lanes : lanes;
     if (want == b->lanes)

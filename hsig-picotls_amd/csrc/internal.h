@@ -20,7 +20,7 @@ constexpr int NPOW = 7;          /* H^1, H^2, H^4, H^8, H^16 (batch kernel table
 /* GHASH basis slot: NPOW x 128 vectors P * x^e, then H^1 .. H^64 (the sparse kernel's per-lane final powers) */
 constexpr int LANE_POWS = 64;
 constexpr int BASIS_VECS = NPOW * 128 + LANE_POWS; /* uint4 per key slot (15 KiB) */
-constexpr int MAX_LANES = 16;    /* lanes per record (G) of the batch kernel: 1, 2, 4, 8, 16 */
+constexpr int MAX_LANES = 32;    /* lanes per record (G) of the batch kernel: 1, 2, 4, 8, 16, 32 */
 constexpr int SPARSE_LANES = 64; /* "lanes" value of the wave-per-record kernel (sparse_kernel.hip) */
 /* the planner picks that kernel when a batch's key runs hold fewer records than this on average */
 #ifndef SPARSE_MAX_PER_RUN
@@ -78,6 +78,7 @@ int launch_batch_g2(int rounds, bool open, int wg, unsigned grid, void *stream, 
 int launch_batch_g4(int rounds, bool open, int wg, unsigned grid, void *stream, const KernelArgs &a, bool aligned);
 int launch_batch_g8(int rounds, bool open, int wg, unsigned grid, void *stream, const KernelArgs &a, bool aligned);
 int launch_batch_g16(int rounds, bool open, int wg, unsigned grid, void *stream, const KernelArgs &a, bool aligned);
+int launch_batch_g32(int rounds, bool open, int wg, unsigned grid, void *stream, const KernelArgs &a, bool aligned);
 int launch_batch_sparse(int rounds, bool open, unsigned grid, void *stream, const KernelArgs &a, bool aligned);
 int launch_batch(int lanes, int rounds, bool open, int wg, unsigned grid, void *stream, const KernelArgs &a, bool aligned);
 int launch_keysetup(KeySlot *slots, uint32_t *basis, const uint8_t *keys, const uint8_t *ivs, uint32_t first, uint32_t count,

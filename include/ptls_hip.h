@@ -182,7 +182,7 @@ typedef struct st_ptls_hip_record_t {
 ptls_hip_batch_t *ptls_hip_batch_new(ptls_hip_engine_t *engine, const ptls_hip_record_t *recs, size_t n, void *stream);
 void ptls_hip_batch_free(ptls_hip_batch_t *batch);
 size_t ptls_hip_batch_count(ptls_hip_batch_t *batch);
-/* lanes cooperating on one record (1, 2, 4, 8 or 16), or 64: one wave per record with key-independent
+/* lanes cooperating on one record (1, 2, 4, 8, 16 or 32), or 64: one wave per record with key-independent
  * LDS (the kernel chosen for batches of many keys with few records each); 0 = automatic (default). */
 int ptls_hip_batch_set_lanes(ptls_hip_batch_t *batch, int lanes);
 int ptls_hip_batch_lanes(ptls_hip_batch_t *batch);

@@ -27,7 +27,7 @@ from make_golden import CONFIGS, config_record, sweep_inputs  # noqa: E402
 from oracle_lib import tls_aad  # noqa: E402
 
 UINT64_MAX = (1 << 64) - 1
-LANES = (1, 2, 4, 8, 16, 64)  # 64: the wave-per-record sparse-key kernel
+LANES = (1, 2, 4, 8, 16, 32, 64)  # 64: the wave-per-record sparse-key kernel
 
 
 def kat_records(golden):
@@ -253,7 +253,7 @@ def test_unaligned_layout(engine, oracle, align):
 
 
 @pytest.mark.parametrize("wg", [512, 768])
-@pytest.mark.parametrize("lanes", [2, 4, 8, 16, 64])
+@pytest.mark.parametrize("lanes", [2, 4, 8, 16, 32, 64])
 def test_key_runs_mixed_lengths(engine, oracle, wg, lanes):
     """BASELINE configs[3] shape in miniature: AES-256, several keys with runs of 150-400 records of
     random 0..6000-byte lengths (the planner reorders each key chunk by length), every workgroup size"""
@@ -308,7 +308,7 @@ def test_differential_random(engine, oracle):
         hb.close()
 
 
-@pytest.mark.parametrize("lanes", [0, 2, 16, 64])
+@pytest.mark.parametrize("lanes", [0, 2, 16, 32, 64])
 @pytest.mark.parametrize("key_len", [16, 32])
 def test_large_records_counter_past_16_bits(engine, oracle, key_len, lanes):
     """records past 2^16 blocks (1 MiB): the counter-mode shortcut holds only while the 32-bit block

@@ -6,7 +6,7 @@ set -e
 cd "$(dirname "$0")/../hsig-picotls_amd"
 make -s -j8 libptls_hip.so >/dev/null
 name=$1; out=variants/libptls_hip_${name}.so
-ALL="aesgcm_kernels sparse_kernel batch_g1 batch_g2 batch_g4 batch_g8 batch_g16"
+ALL="aesgcm_kernels sparse_kernel batch_g1 batch_g2 batch_g4 batch_g8 batch_g16 batch_g32"
 SRCS=${SRCS:-$ALL}
 mkdir -p variants/build_${name}
 objs=""

@@ -11,12 +11,21 @@ ap.add_argument("libs", nargs="+")
 ap.add_argument("--config", default="c4")
 ap.add_argument("--lanes", type=int, default=0)
 ap.add_argument("--records", type=int, default=0, help="override the config's record count")
+ap.add_argument("--key-len", type=int, default=0, help="override the key size (16 / 32)")
+ap.add_argument("--fixed-len", type=int, default=0, help="every record this many bytes (instead of the config's lengths)")
+ap.add_argument("--keys", type=int, default=0, help="override the number of keys")
 args = ap.parse_args()
 import torch
 import bench
 cfg = dict(bench.CONFIGS[args.config])
 if args.records:
     cfg["n"] = args.records
+if args.key_len:
+    cfg["key_len"] = args.key_len
+if args.fixed_len:
+    cfg["L"] = args.fixed_len
+if args.keys:
+    cfg["keys"] = args.keys
 for lib in args.libs:
     os.environ["PTLS_HIP_LIB"] = lib
     import ptls_hip
