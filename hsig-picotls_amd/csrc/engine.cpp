@@ -418,6 +418,12 @@ static int choose_lanes(const std::vector<ptls_hip_record_t> &recs)
     /* key runs too short to amortise the per-key GHASH tables: the key-independent wave-per-record kernel */
     if (per_run < SPARSE_MAX_PER_RUN)
         return SPARSE_LANES;
+    /* long records, short key runs: more lanes per record give a key run more wave tasks for the workgroup's 12
+     * waves.  Measured on configs[3]'s shape (AES-256, 64 B - 16 KiB, 64K keys; tools/time_cfg.py),
+     * seal GiB/s at 16 / 32 lanes (sparse kernel): 8 records per key 126 / 258 (503), 16: 260 / 499 (516),
+     * 24: 394 / 681 (525), 32: 518 / 715, 48: 717 / 734, 64: 786 / 776. */
+    if (g == 8 && mean >= 256 && per_run < 56)
+        return 32;
     if (g == 8 && mean >= 256 && per_run < (double)(WG_ALT / 64) * (64 / 8))
         return 16;
     return g;
@@ -973,10 +979,27 @@ static void *mapped_ptr(const void *h)
     return d;
 }
 
+/* lanes per record when the kernel reads and writes host memory: the launch is PCIe-bound, not LDS-bound, and wider
+ * lane groups turn each load / store instruction into longer contiguous runs per record, i.e. fewer, larger PCIe
+ * requests.  Measured (tools/hostmem_probe.py, seal+open GiB/s at 4 / 8 / 16 / 32 lanes): 1350-B records 31.7 /
+ * 34.8 / 36.7 / 39.5; 16-KiB records - / 36.6 / 40.2 / 41.5; 64 B - 16 KiB over 64K keys at 16 / 32: 28.6 / 36.2.
+ * Batches for the sparse-key kernel keep it. */
+static int mapped_lanes(const std::vector<ptls_hip_record_t> &recs)
+{
+    const int lanes = choose_lanes(recs);
+    if (lanes == SPARSE_LANES || recs.empty())
+        return lanes;
+    double sum = 0;
+    for (const auto &r : recs)
+        sum += (double)((r.aad_len + 15) / 16 + (r.len + 15) / 16 + 1);
+    const double mean = sum / (double)recs.size();
+    return mean >= 32 ? 32 : mean >= 16 ? std::max(lanes, 16) : lanes;
+}
+
 /* PTLS_HIP_TRANSPORT_MAPPED: the batch kernel reads the records from, and writes them to, the caller's pinned host
  * buffers over PCIe itself (their device addresses); no staging copies, no copy engines.  Only the descriptors,
  * the launch plan and the header-protection descriptors go through the slots' pinned staging.  Slices of at
- * most max_recs records rotate over the slots' streams.  (tools/hostmem_probe.py, DESIGN.md §6.3: the copy
+ * most 4 x slice_bytes of payload rotate over the slots' streams, so planning overlaps the kernels.  (tools/hostmem_probe.py, DESIGN.md §6.3: the copy
  * engines carry ~57 GB/s in both directions together, the kernel's own PCIe reads + writes ~80 GB/s.) */
 static int pipeline_run_mapped(ptls_hip_pipeline_t *p, ptls_hip_keyset_t *ks, const ptls_hip_record_t *recs, size_t n,
                                const uint8_t *d_in, const uint8_t *d_aad, uint8_t *d_out, uint64_t *h_result, uint64_t *d_res,
@@ -989,12 +1012,19 @@ static int pipeline_run_mapped(ptls_hip_pipeline_t *p, ptls_hip_keyset_t *ks, co
     std::vector<uint32_t> order;
     int k = 0;
     for (size_t i = 0; i < n; ++k) {
-        const size_t cnt = std::min(n - i, p->max_recs - 1);
+        /* slices of at most slice_bytes of payload: the host plans and uploads slice k + 1 while the device runs k */
+        size_t cnt = 0, bytes = 0;
+        /* 4 x the staging slice: no staging is involved, and the measured best (seal+open GiB/s of 1 GiB, 64 / 128 /
+         * 256 / 512 / 2048 MiB slices: 16-KiB records 35.5 / 38.6 / 39.8 / 39.9 / 39.6, 1350-B records 32.9 / 33.3 /
+         * 33.4 / 30.7 / 21.9, configs[3] 34.7 / 36.3 / 37.2 / 35.8 / 33.9) */
+        const size_t mslice = 4 * p->slice_bytes;
+        while (i + cnt < n && cnt < p->max_recs - 1 && (cnt == 0 || bytes + recs[i + cnt].len <= mslice))
+            bytes += recs[i + cnt++].len;
         PipeSlot &s = p->slot[k % NSLOT];
         if (s.busy)
             HIP_TRY(hipEventSynchronize(s.done), PTLS_HIP_ENODEV);
         std::memcpy(s.h_recs, recs + i, cnt * sizeof(ptls_hip_record_t));
-        const int lanes = choose_lanes(std::vector<ptls_hip_record_t>(s.h_recs, s.h_recs + cnt));
+        const int lanes = mapped_lanes(std::vector<ptls_hip_record_t>(s.h_recs, s.h_recs + cnt));
         bool aligned;
         build_chunks(s.h_recs, cnt, lanes, (unsigned)p->eng->ncu, ch, order, aligned);
         std::memcpy(s.h_chunks, ch.data(), ch.size() * sizeof(Chunk));
@@ -1321,18 +1351,16 @@ static ptls_hip_engine_t *plugin_engine(void)
     return g_plugin_engine;
 }
 
-/* per-context state: one key slot plus device staging for one record */
+/* per-context state: one key slot plus pinned, device-mapped staging for one record.  A call copies the record in
+ * on the CPU, launches, and copies the output out: the kernel reads and writes the staging over PCIe itself (no
+ * copy-engine transfers, one launch + one stream synchronisation per call). */
 struct hip_aead_state {
     ptls_hip_engine_t *eng;
     ptls_hip_keyset_t *ks;
     hipStream_t stream;
-    uint8_t *d_buf; /* [in: cap][out: cap + 16][aad: aad_cap] */
+    uint8_t *h_io, *d_io; /* pinned [in: cap][out: cap + 16][aad: aad_cap] and its device address */
     size_t cap, aad_cap;
-    ptls_hip_record_t *d_rec;
-    Chunk *d_chunk;
-    uint32_t *d_order;
-    uint64_t *d_result;
-    uint8_t *h_stage; /* pinned: record + chunk + result */
+    uint8_t *h_stage, *d_stage; /* pinned 256 B: record, chunk, order, result, supp, mask (ST_*) and its device address */
     uint8_t iv[12];
     bool iv_dirty;
 };
@@ -1363,8 +1391,8 @@ struct hip_ctr_state {
     ptls_hip_engine_t *eng;
     ptls_hip_keyset_t *ks;
     hipStream_t stream;
-    uint8_t *d_buf;   /* [ptls_hip_supp_t @0][input block @32][mask @48] */
-    uint8_t *h_stage; /* pinned, same layout */
+    uint8_t *h_stage; /* pinned [ptls_hip_supp_t @0][input block @32][mask @48] */
+    uint8_t *d_stage; /* its device address: the kernel reads and writes it in place */
     uint8_t bits[16];
     bool ready;
 };
@@ -1390,14 +1418,12 @@ static void ecb_block(hip_ctr_state *st, const void *src, uint8_t dst[16])
     const ptls_hip_supp_t sp{32, 48, 0, PTLS_HIP_SUPP_ENABLE};
     std::memcpy(st->h_stage, &sp, sizeof(sp));
     std::memcpy(st->h_stage + 32, src, 16);
-    plugin_check(hipMemcpyAsync(st->d_buf, st->h_stage, 48, hipMemcpyHostToDevice, st->stream), "ecb upload");
-    const int e = launch_aesecb(st->ks->key_size == 16 ? 10 : 14, reinterpret_cast<const ptls_hip_supp_t *>(st->d_buf), 1,
-                                st->d_buf, st->d_buf, st->ks->d_slots, 1, st->eng->d_t0, 1, st->stream);
+    const int e = launch_aesecb(st->ks->key_size == 16 ? 10 : 14, reinterpret_cast<const ptls_hip_supp_t *>(st->d_stage), 1,
+                                st->d_stage, st->d_stage, st->ks->d_slots, 1, st->eng->d_t0, 1, st->stream);
     if (e != 0) {
         g_err = hipGetErrorString((hipError_t)e);
         plugin_die("ecb launch");
     }
-    plugin_check(hipMemcpyAsync(st->h_stage + 48, st->d_buf + 48, 16, hipMemcpyDeviceToHost, st->stream), "ecb download");
     plugin_check(hipStreamSynchronize(st->stream), "ecb sync");
     std::memcpy(dst, st->h_stage + 48, 16);
     std::memset(st->h_stage + 32, 0, 32);
@@ -1438,13 +1464,14 @@ static hip_ctr_state *ecb_state_new(const void *key, size_t key_size)
         return nullptr;
     }
     st->ks = ptls_hip_keyset_new(eng, key_size, 1);
-    const bool ok = st->ks != nullptr && hipMalloc(&st->d_buf, 64) == hipSuccess &&
-                    hipHostMalloc(&st->h_stage, 64, hipHostMallocDefault) == hipSuccess &&
+    void *d_stage = nullptr;
+    const bool ok = st->ks != nullptr && hipHostMalloc(&st->h_stage, 64, hipHostMallocDefault) == hipSuccess &&
+                    hipHostGetDevicePointer(&d_stage, st->h_stage, 0) == hipSuccess &&
                     ptls_hip_keyset_set(st->ks, 0, 1, key, nullptr, st->stream) == 0;
+    st->d_stage = static_cast<uint8_t *>(d_stage);
     if (!ok) {
         if (st->ks != nullptr)
             ptls_hip_keyset_free(st->ks);
-        (void)hipFree(st->d_buf);
         (void)hipHostFree(st->h_stage);
         (void)hipStreamDestroy(st->stream);
         delete st;
@@ -1458,11 +1485,7 @@ static void ecb_state_free(hip_ctr_state *st)
     {
         DeviceGuard g(st->eng->device);
         ptls_hip_keyset_free(st->ks);
-        if (st->d_buf != nullptr) {
-            (void)hipMemsetAsync(st->d_buf, 0, 64, st->stream);
-            (void)hipStreamSynchronize(st->stream);
-        }
-        (void)hipFree(st->d_buf);
+        (void)hipStreamSynchronize(st->stream);
         if (st->h_stage != nullptr)
             std::memset(st->h_stage, 0, 64);
         (void)hipHostFree(st->h_stage);
@@ -1545,6 +1568,13 @@ static int aes256ctr_setup(ptls_cipher_context_t *ctx, int is_enc, const void *k
     return aesctr_setup(ctx, is_enc, key, PTLS_AES256_KEY_SIZE);
 }
 
+static uint8_t *mapped_or_die(uint8_t *h)
+{
+    void *d = nullptr;
+    plugin_check(hipHostGetDevicePointer(&d, h, 0), "hipHostGetDevicePointer(staging)");
+    return static_cast<uint8_t *>(d);
+}
+
 static void state_reserve(hip_aead_state *st, size_t len, size_t aadlen)
 {
     if (len <= st->cap && aadlen <= st->aad_cap)
@@ -1556,9 +1586,13 @@ static void state_reserve(hip_aead_state *st, size_t len, size_t aadlen)
         aad_cap *= 2;
     cap = (cap + 15) & ~(size_t)15;
     aad_cap = (aad_cap + 15) & ~(size_t)15;
-    if (st->d_buf != nullptr)
-        plugin_check(hipFree(st->d_buf), "hipFree");
-    plugin_check(hipMalloc(&st->d_buf, cap + (cap + 16) + aad_cap), "hipMalloc(staging)");
+    if (st->h_io != nullptr) {
+        std::memset(st->h_io, 0, st->cap + st->cap + 16 + st->aad_cap);
+        plugin_check(hipHostFree(st->h_io), "hipHostFree");
+    }
+    st->h_io = nullptr;
+    plugin_check(hipHostMalloc(&st->h_io, cap + (cap + 16) + aad_cap, hipHostMallocDefault), "hipHostMalloc(staging)");
+    st->d_io = mapped_or_die(st->h_io);
     st->cap = cap;
     st->aad_cap = aad_cap;
 }
@@ -1574,7 +1608,9 @@ struct PluginSupp {
  * supp descriptor @160, header-protection mask @192 */
 static const size_t ST_REC = 0, ST_CHUNK = 64, ST_ORDER = 96, ST_RESULT = 128, ST_SUPP = 160, ST_MASK = 192;
 
-/* run one record through the batch kernel: in/out/aad are host buffers */
+/* run one record: in/out/aad are the caller's (unpinned) host buffers.  The sparse kernel (one wave per record,
+ * its own 8 KiB H^64 table, none for records of <= 64 GHASH elements) serves a single record without building
+ * a workgroup-wide 64 KiB table. */
 static uint64_t plugin_run(hip_aead_state *st, bool open, void *output, const void *input, size_t len, uint64_t seq,
                            const void *aad, size_t aadlen, const PluginSupp *ps = nullptr, const void *tag = nullptr)
 {
@@ -1586,76 +1622,66 @@ static uint64_t plugin_run(hip_aead_state *st, bool open, void *output, const vo
             plugin_die("set_iv");
         st->iv_dirty = false;
     }
-    uint8_t *d_in = st->d_buf, *d_out = st->d_buf + st->cap, *d_aad = st->d_buf + st->cap + st->cap + 16;
+    uint8_t *h_in = st->h_io, *h_out = st->h_io + st->cap, *h_aad = st->h_io + st->cap + st->cap + 16;
+    uint8_t *d_in = st->d_io, *d_out = st->d_io + st->cap, *d_aad = st->d_io + st->cap + st->cap + 16;
     ptls_hip_record_t rec{};
-    rec.in_off = 0;
-    rec.out_off = 0;
-    rec.aad_off = 0;
     rec.seq = seq;
     rec.len = (uint32_t)len;
     rec.aad_len = (uint32_t)aadlen;
-    rec.key = 0;
-    Chunk ch{0, 1, 0, 1};
+    const Chunk ch{0, 1, 0, 1};
     const uint32_t order0 = 0;
     const ptls_hip_supp_t sp{ps != nullptr ? ps->sample_off : 0, 0, 0, PTLS_HIP_SUPP_ENABLE};
     std::memcpy(st->h_stage + ST_REC, &rec, sizeof(rec));
     std::memcpy(st->h_stage + ST_CHUNK, &ch, sizeof(ch));
     std::memcpy(st->h_stage + ST_ORDER, &order0, sizeof(order0));
     std::memcpy(st->h_stage + ST_SUPP, &sp, sizeof(sp));
-    plugin_check(hipMemcpyAsync(st->d_rec, st->h_stage, ST_SUPP + sizeof(sp), hipMemcpyHostToDevice, st->stream), "upload(rec)");
     if (tag != nullptr) { /* open with a detached tag (ptls_fusion_aesgcm_decrypt, lib/fusion.c:660-661) */
         if (len != 0)
-            plugin_check(hipMemcpyAsync(d_in, input, len, hipMemcpyHostToDevice, st->stream), "upload(in)");
-        plugin_check(hipMemcpyAsync(d_in + len, tag, 16, hipMemcpyHostToDevice, st->stream), "upload(tag)");
+            std::memcpy(h_in, input, len);
+        std::memcpy(h_in + len, tag, 16);
     } else if (in_len != 0) {
-        plugin_check(hipMemcpyAsync(d_in, input, in_len, hipMemcpyHostToDevice, st->stream), "upload(in)");
+        std::memcpy(h_in, input, in_len);
     }
     if (aadlen != 0)
-        plugin_check(hipMemcpyAsync(d_aad, aad, aadlen, hipMemcpyHostToDevice, st->stream), "upload(aad)");
+        std::memcpy(h_aad, aad, aadlen);
     KernelArgs a{};
-    a.recs = st->d_rec;
-    a.recs_ord = st->d_rec; /* one record: chunk order is the caller's */
-    a.order = st->d_order;
-    a.chunks = st->d_chunk;
+    a.recs = reinterpret_cast<const ptls_hip_record_t *>(st->d_stage + ST_REC);
+    a.recs_ord = a.recs; /* one record: chunk order is the caller's */
+    a.order = reinterpret_cast<const uint32_t *>(st->d_stage + ST_ORDER);
+    a.chunks = reinterpret_cast<const Chunk *>(st->d_stage + ST_CHUNK);
     a.nchunks = 1;
     a.in = d_in;
     a.aad = d_aad;
     a.out = d_out;
-    a.result = st->d_result;
+    a.result = reinterpret_cast<uint64_t *>(st->d_stage + ST_RESULT);
     a.slots = st->ks->d_slots;
     a.basis = st->ks->d_basis;
     a.t0 = st->eng->d_t0;
     if (ps != nullptr) {
-        uint8_t *d_stage = reinterpret_cast<uint8_t *>(st->d_rec);
-        a.supp = reinterpret_cast<const ptls_hip_supp_t *>(d_stage + ST_SUPP);
+        a.supp = reinterpret_cast<const ptls_hip_supp_t *>(st->d_stage + ST_SUPP);
         a.hp_slots = ps->hp_slots;
         a.hp_nslots = 1;
-        a.mask = d_stage + ST_MASK;
+        a.mask = st->d_stage + ST_MASK;
     }
-    const size_t n = (aadlen + 15) / 16 + (len + 15) / 16 + 1;
-    const int lanes = n >= 128 ? 8 : n >= 48 ? 4 : n >= 16 ? 2 : 1;
-    int e = launch_batch(lanes, st->ks->key_size == 16 ? 10 : 14, open, 512, 1, st->stream, a, true);
+    const int e = launch_batch(SPARSE_LANES, st->ks->key_size == 16 ? 10 : 14, open, 0, 1, st->stream, a, true);
     if (e != 0) {
         g_err = hipGetErrorString((hipError_t)e);
         plugin_die("launch");
     }
+    plugin_check(hipStreamSynchronize(st->stream), "hipStreamSynchronize");
     uint64_t result = len;
     if (open) {
         if (len != 0)
-            plugin_check(hipMemcpyAsync(output, d_out, len, hipMemcpyDeviceToHost, st->stream), "download(out)");
-        plugin_check(hipMemcpyAsync(st->h_stage + ST_RESULT, st->d_result, 8, hipMemcpyDeviceToHost, st->stream), "download(result)");
-    } else {
-        plugin_check(hipMemcpyAsync(output, d_out, len + 16, hipMemcpyDeviceToHost, st->stream), "download(out)");
-        if (ps != nullptr)
-            plugin_check(hipMemcpyAsync(st->h_stage + ST_MASK, reinterpret_cast<uint8_t *>(st->d_rec) + ST_MASK, 16,
-                                        hipMemcpyDeviceToHost, st->stream),
-                         "download(mask)");
-    }
-    plugin_check(hipStreamSynchronize(st->stream), "hipStreamSynchronize");
-    if (open)
+            std::memcpy(output, h_out, len);
         std::memcpy(&result, st->h_stage + ST_RESULT, 8);
+    } else {
+        std::memcpy(output, h_out, len + 16);
+    }
     if (ps != nullptr)
         std::memcpy(ps->output, st->h_stage + ST_MASK, 16);
+    /* the record's bytes do not stay in the staging */
+    std::memset(h_in, 0, in_len);
+    std::memset(h_out, 0, open ? len : len + 16);
     return result;
 }
 
@@ -1664,13 +1690,15 @@ static void state_free(hip_aead_state *st)
     {
         DeviceGuard g(st->eng->device);
         ptls_hip_keyset_free(st->ks);
-        if (st->d_buf != nullptr) {
-            (void)hipMemset(st->d_buf, 0, st->cap + st->cap + 16 + st->aad_cap);
-            (void)hipStreamSynchronize(st->stream);
-            (void)hipFree(st->d_buf);
+        (void)hipStreamSynchronize(st->stream);
+        if (st->h_io != nullptr) {
+            std::memset(st->h_io, 0, st->cap + st->cap + 16 + st->aad_cap);
+            (void)hipHostFree(st->h_io);
         }
-        (void)hipFree(st->d_rec);
-        (void)hipHostFree(st->h_stage);
+        if (st->h_stage != nullptr) {
+            std::memset(st->h_stage, 0, 256);
+            (void)hipHostFree(st->h_stage);
+        }
         (void)hipStreamDestroy(st->stream);
     }
     std::memset(st->iv, 0, sizeof(st->iv));
@@ -1790,21 +1818,19 @@ static hip_aead_state *state_new(const void *key, const void *iv, size_t key_siz
         return nullptr;
     }
     st->ks = ptls_hip_keyset_new(eng, key_size, 1);
-    bool ok = st->ks != nullptr && hipMalloc(&st->d_rec, 256) == hipSuccess &&
-              hipHostMalloc(&st->h_stage, 256, hipHostMallocDefault) == hipSuccess &&
+    void *d_stage = nullptr;
+    bool ok = st->ks != nullptr && hipHostMalloc(&st->h_stage, 256, hipHostMallocDefault) == hipSuccess &&
+              hipHostGetDevicePointer(&d_stage, st->h_stage, 0) == hipSuccess &&
               ptls_hip_keyset_set(st->ks, 0, 1, key, iv, st->stream) == 0;
     if (!ok) {
         if (st->ks != nullptr)
             ptls_hip_keyset_free(st->ks);
-        (void)hipFree(st->d_rec);
         (void)hipHostFree(st->h_stage);
         (void)hipStreamDestroy(st->stream);
         delete st;
         return nullptr;
     }
-    st->d_chunk = reinterpret_cast<Chunk *>(reinterpret_cast<uint8_t *>(st->d_rec) + ST_CHUNK);
-    st->d_order = reinterpret_cast<uint32_t *>(reinterpret_cast<uint8_t *>(st->d_rec) + ST_ORDER);
-    st->d_result = reinterpret_cast<uint64_t *>(reinterpret_cast<uint8_t *>(st->d_rec) + ST_RESULT);
+    st->d_stage = static_cast<uint8_t *>(d_stage);
     std::memcpy(st->iv, iv, 12);
     st->iv_dirty = false;
     return st;
@@ -1959,12 +1985,21 @@ struct ptls_hip_aesgcm_context {
     hip_aead_state *st;
 };
 
-static void lowlevel_set_nonce(hip_aead_state *st, const void *nonce)
+/* the sequence number that turns the state's IV into `nonce` (bytes 4..11 = IV xor BE64(seq), ptls_aead__build_iv,
+ * lib/picotls.c:6492-6506) when bytes 0..3 agree, so a per-packet nonce needs no IV upload; otherwise the nonce
+ * becomes the IV (uploaded before the launch) and the sequence number is 0 */
+static uint64_t lowlevel_seq(hip_aead_state *st, const void *nonce)
 {
-    if (std::memcmp(st->iv, nonce, 12) != 0) {
-        std::memcpy(st->iv, nonce, 12);
+    const uint8_t *nb = static_cast<const uint8_t *>(nonce);
+    if (std::memcmp(st->iv, nb, 4) != 0) {
+        std::memcpy(st->iv, nb, 12);
         st->iv_dirty = true;
+        return 0;
     }
+    uint64_t seq = 0;
+    for (int i = 0; i < 8; ++i)
+        seq = (seq << 8) | (uint8_t)(nb[4 + i] ^ st->iv[4 + i]);
+    return seq;
 }
 
 extern "C" ptls_hip_aesgcm_context_t *ptls_hip_aesgcm_new(const void *key, size_t key_size, size_t capacity)
@@ -1999,13 +2034,12 @@ extern "C" void ptls_hip_aesgcm_encrypt(ptls_hip_aesgcm_context_t *ctx, void *ou
                                         const void *nonce, const void *aad, size_t aadlen,
                                         ptls_aead_supplementary_encryption_t *supp)
 {
-    lowlevel_set_nonce(ctx->st, nonce);
-    encrypt_supp(ctx->st, output, input, inlen, 0, aad, aadlen, supp);
+    encrypt_supp(ctx->st, output, input, inlen, lowlevel_seq(ctx->st, nonce), aad, aadlen, supp);
 }
 
 extern "C" int ptls_hip_aesgcm_decrypt(ptls_hip_aesgcm_context_t *ctx, void *output, const void *input, size_t inlen,
                                        const void *nonce, const void *aad, size_t aadlen, const void *tag)
 {
-    lowlevel_set_nonce(ctx->st, nonce);
-    return plugin_run(ctx->st, true, output, input, inlen, 0, aad, aadlen, nullptr, tag) != ~(uint64_t)0;
+    const uint64_t seq = lowlevel_seq(ctx->st, nonce);
+    return plugin_run(ctx->st, true, output, input, inlen, seq, aad, aadlen, nullptr, tag) != ~(uint64_t)0;
 }

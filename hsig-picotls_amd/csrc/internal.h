@@ -24,7 +24,7 @@ constexpr int MAX_LANES = 32;    /* lanes per record (G) of the batch kernel: 1,
 constexpr int SPARSE_LANES = 64; /* "lanes" value of the wave-per-record kernel (sparse_kernel.hip) */
 /* the planner picks that kernel when a batch's key runs hold fewer records than this on average */
 #ifndef SPARSE_MAX_PER_RUN
-#define SPARSE_MAX_PER_RUN 20 /* measured tie at ≈ 21 AES-256 records of 64 B-16 KiB per key */
+#define SPARSE_MAX_PER_RUN 16 /* measured tie with 32 lanes per record at 16 AES-256 records of 64 B-16 KiB per key */
 #endif
 /* one workgroup per CU (LDS-limited); 768 threads (3 waves per SIMD, 168 VGPRs) by default, 512 selectable
  * per batch (engine.cpp:plan_wg).  WG_MAX bounds the chunk size the planner cuts key runs into. */

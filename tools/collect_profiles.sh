@@ -2,8 +2,9 @@
 # Copy the summaries written by tools/refresh_profiles.sh from gpurun_out/ into profiles/ (committed).
 set -e
 cd "$(dirname "$0")/.."
-tag=${1:-r01}
-for c in c2 c3 c4; do
+tag=${1:-r02}; shift || true
+cfgs=${*:-c2 c3 c4 c4s}
+for c in $cfgs; do
   cp gpurun_out/prof_${tag}_$c/trace/run_kernel_stats.csv profiles/${tag}_${c}_kernel_stats.csv
   cp gpurun_out/prof_${tag}_$c/traffic_$c.json profiles/traffic_$c.json
   cp gpurun_out/pmc_$c/lds_$c.json profiles/lds_$c.json

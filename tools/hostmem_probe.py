@@ -55,14 +55,21 @@ def timed(f, reps=3):
 
 
 def main():
-    cfg = dict(bench.CONFIGS["c2"])
-    cfg["n"] = int(os.environ.get("PROBE_RECORDS", 65536))
-    out = {"records": cfg["n"], "record_bytes": cfg["L"]}
+    import argparse
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="c2")
+    ap.add_argument("--records", type=int, default=0)
+    ap.add_argument("--lanes", default="0", help="comma-separated lanes-per-record values for the zero-copy runs (0 = planner)")
+    ap.add_argument("--kinds", default="coherent,noncoherent")
+    args = ap.parse_args()
+    cfg = dict(bench.CONFIGS[args.config])
+    cfg["n"] = args.records or max(1, int((1 << 30) / (cfg["L"] or 8224)))
+    out = {"config": args.config, "records": cfg["n"], "record_bytes": cfg["L"]}
     eng = ptls_hip.Engine(0)
     idx, recs, in_total, out_total, lens = bench.make_workload(cfg, 0)
     sum_L = float(lens.sum())
     keys, ivs = bench.make_keys(cfg)
-    ks = ptls_hip.KeySet(eng, 16, 1)
+    ks = ptls_hip.KeySet(eng, cfg["key_len"], cfg["keys"])
     ks.set(0, keys, ivs)
     seal_b = ptls_hip.Batch(eng, recs)
     ro = recs.copy()
@@ -94,7 +101,10 @@ def main():
     seal_b.fill(d_in, bench.SEED_DATA)
 
     out["device_seal_gibps"] = round(sum_L / timed(lambda: seal_b.seal(ks, d_in, aad, d_out)) / GIB, 1)
-    for kind, fl in FLAGS.items():
+    runs = [(k, FLAGS[k], int(l)) for k in args.kinds.split(",") for l in args.lanes.split(",")]
+    for kind, fl, lanes in runs:
+        seal_b.set_lanes(lanes)
+        open_b.set_lanes(seal_b.lanes)
         hin, hin_d = host_alloc(in_total + 64, fl)
         hout, hout_d = host_alloc(out_total + 64, fl)
         hpt, hpt_d = host_alloc(in_total + 64, fl)
@@ -110,9 +120,10 @@ def main():
         r["seal_host_host_gibps"] = round(sum_L / t_s / GIB, 2)
         r["open_host_host_gibps"] = round(sum_L / t_o / GIB, 2)
         r["seal_open_host_host_gibps"] = round(2 * sum_L / (t_s + t_o) / GIB, 2)
-        r["open_all_ok"] = bool((res == int(cfg["L"])).all())
+        r["open_all_ok"] = bool((res == torch.from_numpy(lens.astype(np.int64)).cuda()).all())
         r["pcie_bytes_per_s_gbs"] = round((2 * sum_L + 16 * cfg["n"]) / t_s / 1e9, 1)
-        out[f"zero_copy_{kind}"] = r
+        r["lanes"] = seal_b.lanes
+        out[f"zero_copy_{kind}_lanes{seal_b.lanes}"] = r
         for p in (hin, hout, hpt):
             hip.hipHostFree(p)
     print(json.dumps(out), flush=True)
