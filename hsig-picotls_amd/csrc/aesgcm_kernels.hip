@@ -217,6 +217,10 @@ __global__ void keysetup_kernel(KeySlot *slots, uint32_t *basis, const uint8_t *
         bs[NPOW * 128 + q] = make_uint4(pr.w0, pr.w1, pr.w2, pr.w3);
         pk = gf_mul_slow(pk, hh);
     }
+#if HYBRID
+    /* round keys 1..rounds in the bit-sliced form of the batch kernel's hybrid waves (bs8_aes.h) */
+    bs8::slice_key(w, rounds, reinterpret_cast<uint32_t *>(bs + BS_KEY_OFF));
+#endif
 }
 
 /* ======================================================================================= *

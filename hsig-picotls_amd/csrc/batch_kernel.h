@@ -26,6 +26,7 @@
 
 #include <hip/hip_runtime.h>
 #include "internal.h"
+#include "bs8_aes.h"
 
 namespace ptls_hip {
 
@@ -619,6 +620,20 @@ __device__ __forceinline__ V4 gh_mul_main(const uint8_t *lds, const GhLane &g, V
     return acc;
 }
 
+/* gh_mul_main with its 16 lookups in two halves of 8 (32 VGPRs in flight instead of 64) */
+__device__ __forceinline__ V4 gh_mul_main_halves(const uint8_t *lds, const GhLane &g, V4 y, V4 x)
+{
+    const V4 xr = gh_rot(g, y);
+    V4 acc = x, G[8];
+    gh_issue<0, 8>(lds, g, xr, G);
+    acc = v4xor3(acc, G[0], G[1]), acc = v4xor3(acc, G[2], G[3]), acc = v4xor3(acc, G[4], G[5]), acc = v4xor3(acc, G[6], G[7]);
+    __builtin_amdgcn_sched_barrier(0);
+    gh_issue<8, 8>(lds, g, xr, G);
+    acc = v4xor3(acc, G[0], G[1]), acc = v4xor3(acc, G[2], G[3]), acc = v4xor3(acc, G[4], G[5]), acc = v4xor3(acc, G[6], G[7]);
+    __builtin_amdgcn_sched_barrier(0);
+    return acc;
+}
+
 /* gh_mul_main in pieces for the phased loop: the lane rotation of y, then the 4 lookups of word Q */
 __device__ __forceinline__ V4 gh_rot(const GhLane &g, V4 y)
 {
@@ -921,6 +936,38 @@ __device__ __forceinline__ int wave_max(int v)
     return v;
 }
 
+/* Bit-sliced AES-CTR keystream of 8 counter blocks c0 + k * stride of one lane (bs8_aes.h, all on the VALU); the
+ * lane's 8 data blocks src + k * src_stride are loaded during the last round, so they are not held through the group */
+template <int ROUNDS>
+__device__ __forceinline__ void bs8_ctr(const uint32_t *__restrict__ rk, const uint32_t *__restrict__ bk, uint32_t n0, uint32_t n1,
+                                        uint32_t n2, uint32_t c0, uint32_t stride, V4 (&ks)[8], const uint8_t *src, size_t src_stride,
+                                        V4 (&d)[8])
+{
+    uint32_t P[32];
+    bs8::ctr_planes(P, rk, n0, n1, n2, c0, stride);
+#pragma unroll
+    for (int r = 1; r <= ROUNDS; ++r) {
+        const uint32_t *Kr = bk + bs8::opaque_off(32 * (r - 1), P[0]);
+        bs8::sub_row<0>(P), bs8::sub_row<1>(P), bs8::sub_row<2>(P), bs8::sub_row<3>(P);
+        if (r == ROUNDS) {
+            asm volatile("" : "+v"(src) : "v"(P[0])); /* the loads go out after the last S-boxes, not earlier */
+#pragma unroll
+            for (int k = 0; k < 8; ++k)
+                d[k] = load_full(src + (size_t)k * src_stride);
+        }
+        bs8::shift_rows(P);
+        if (r < ROUNDS)
+            bs8::mix_columns_ark(P, Kr);
+        else
+            bs8::add_round_key(P, Kr);
+    }
+    uint32_t W[8][4];
+    bs8::from_planes(P, W);
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+        ks[k] = V4{W[k][0], W[k][1], W[k][2], W[k][3]};
+}
+
 /* ======================================================================================= *
  *  batch seal / open                                                                       *
  * ======================================================================================= */
@@ -1072,7 +1119,7 @@ __global__ void __launch_bounds__(WGT)
             /* Iterations handle two Horner elements (i and i + G) of a lane; their AES blocks are independent
              * and run interleaved.  y = y * P ^ x is exact from y = 0 (0 * P = 0), so no first-element case. */
             /* counter-mode shortcut constants of this lane's record (rounds 1-2 of every block with counter < 2^16) */
-            const CtrConst cc = ctr_const(lds, lb_aes, rk, n0, n1, n2);
+            CtrConst cc; /* computed after the stretch's bit-sliced part (not held through it) */
 
             /* elements m and m + 1 of the lane (AAD, partial or full data, length block), their two AES blocks
              * interleaved; the counter-mode shortcut unless some lane of the wave has a counter >= 2^16 */
@@ -1171,10 +1218,46 @@ __global__ void __launch_bounds__(WGT)
                     y = j == 0 ? x : gh_mul_main(lds, gl, y, x);
                 }
             }
-            if (npure) {
-                const uint8_t *src = in_p + 16 * (size_t)(i0 - na + pm0 * G);
-                uint8_t *dst = out_p + 16 * (size_t)(i0 - na + pm0 * G);
-                const uint32_t cbase = (uint32_t)(i0 - na + pm0 * G) + 2u;
+            /* HYBRID: a bit-slicing wave runs the first 8 * (npure * KP / 8) elements of the stretch on the VALU */
+            int vdone = 0;
+#if HYBRID
+            if (wave >= NW - HYBRID && SPLIT_PROBE == 0) {
+                static_assert(8 % KP == 0, "a sliced group covers whole iterations of the table loop");
+                const int ngr = npure * KP / 8;
+                if (ngr > 0) {
+                    const size_t o0 = 16 * (size_t)(i0 - na + pm0 * G);
+                    const uint32_t c0 = (uint32_t)(i0 - na + pm0 * G) + 2u;
+                    const uint32_t *__restrict__ bk = basis + ((size_t)ch.key * BASIS_VECS + BS_KEY_OFF) * 4;
+                    for (int gi = 0; gi < ngr; ++gi) {
+                        const size_t o = o0 + (size_t)(8 * gi * G) * 16;
+                        V4 d[8], ks[8];
+                        bs8_ctr<ROUNDS>(rk, bk, n0, n1, n2, c0 + (uint32_t)(8 * gi * G), (uint32_t)G, ks, in_p + o, 16 * (size_t)G, d);
+                        /* GHASH right away (Horner with the main table): its LDS latency is exposed to this wave, but nothing
+                         * has to be held through the next group's rounds */
+#pragma unroll
+                        for (int k = 0; k < 8; ++k) {
+                            /* (open hashes d, which does not depend on the keystream: keep its multiplies after it) */
+                            asm volatile("" : "+v"(d[k].w0), "+v"(d[k].w1), "+v"(d[k].w2), "+v"(d[k].w3) : "v"(ks[k].w0));
+                            const V4 x = v4xor(d[k], ks[k]);
+                            store_full(out_p + o + 16 * (size_t)(k * G), x);
+                            if (!OPEN)
+                                d[k] = x; /* d = the GHASH input from here on */
+                        }
+#pragma unroll
+                        for (int k = 0; k < 8; ++k)
+                            y = gh_mul_main_halves(lds, gl, y, d[k]);
+                    }
+                    vdone = 8 * ngr;
+                }
+            }
+#endif
+            cc = ctr_const(lds, lb_aes, rk, n0, n1, n2);
+            const int ntab = npure - vdone / KP; /* iterations left for the table loop */
+            if (ntab) {
+                const int pst = pm0 + vdone;
+                const uint8_t *src = in_p + 16 * (size_t)(i0 - na + pst * G);
+                uint8_t *dst = out_p + 16 * (size_t)(i0 - na + pst * G);
+                const uint32_t cbase = (uint32_t)(i0 - na + pst * G) + 2u;
                 V4 pend[KP], bufA[KP], bufB[KP];
                 /* ping-pong prefetch: iteration `it` consumes the buffer loaded one iteration earlier and refills
                  * the other one for it + 1 (clamped to the last iteration so the body stays branch-free).  Two
@@ -1185,7 +1268,7 @@ __global__ void __launch_bounds__(WGT)
                 /* one branch-free iteration; `hash_pending` is a literal at every call site */
                 auto pure_iter = [&](int it, bool hash_pending, V4(&d)[KP], V4(&dn)[KP]) {
                     const size_t o = (size_t)(it * KP * G) * 16;
-                    const size_t on = (size_t)(min(it + 1, npure - 1) * KP * G) * 16;
+                    const size_t on = (size_t)(min(it + 1, ntab - 1) * KP * G) * 16;
                     V4 k[KP];
                     uint32_t cw[KP];
 #if PFPRIO
@@ -1228,11 +1311,11 @@ __global__ void __launch_bounds__(WGT)
                 };
                 pure_iter(0, false, bufA, bufB);
                 int it = 1;
-                for (; it + 1 < npure; it += 2) {
+                for (; it + 1 < ntab; it += 2) {
                     pure_iter(it, true, bufB, bufA);
                     pure_iter(it + 1, true, bufA, bufB);
                 }
-                if (it < npure)
+                if (it < ntab)
                     pure_iter(it, true, bufB, bufA);
                 if (!OPEN && SPLIT_PROBE == 0) {
 #pragma unroll

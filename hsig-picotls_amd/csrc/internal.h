@@ -4,6 +4,7 @@
  * HBM layout:
  *   key slots    KeySlot[nslots]             512 B each: round keys, static IV, H powers
  *   GHASH basis  uint4[nslots][BASIS_VECS]   15 KiB per slot: P * x^e for P in {H, H^2, ..., H^64}, then H^1..H^64
+ *                                            (HYBRID builds: then the bit-sliced round keys, bs8_aes.h)
  *   records      ptls_hip_record_t[n]        48 B descriptors (caller's order)
  *   chunks       Chunk[nchunks]              runs of <= CHUNK_RECS records sharing one key slot
  *   payloads     caller's buffers, untouched layout (in / aad / out)
@@ -19,7 +20,16 @@ namespace ptls_hip {
 constexpr int NPOW = 7;          /* H^1, H^2, H^4, H^8, H^16 (batch kernel tables), H^32, H^64 (sparse kernel) */
 /* GHASH basis slot: NPOW x 128 vectors P * x^e, then H^1 .. H^64 (the sparse kernel's per-lane final powers) */
 constexpr int LANE_POWS = 64;
-constexpr int BASIS_VECS = NPOW * 128 + LANE_POWS; /* uint4 per key slot (15 KiB) */
+/* HYBRID (measurement switch): this many waves per batch-kernel workgroup (the last ones) run their
+ * full-block stretch as bit-sliced AES on the VALU (bs8_aes.h), the others with the LDS T-tables.  Parity-green, but
+ * no faster on MI355X (c2: +0-1 % at 4 of 12 waves, -5 % at 8, -20 % at 12), so off. */
+#ifndef HYBRID
+#define HYBRID 0
+#endif
+/* with HYBRID, the slot also holds the bit-sliced round keys 1..rounds (bs8::slice_key: 32 words per round) */
+constexpr int BS_KEY_OFF = NPOW * 128 + LANE_POWS; /* uint4 offset in the slot */
+constexpr int BS_KEY_VECS = HYBRID ? 14 * 32 / 4 : 0;
+constexpr int BASIS_VECS = BS_KEY_OFF + BS_KEY_VECS; /* uint4 per key slot (15 KiB; 16.75 KiB with HYBRID) */
 constexpr int MAX_LANES = 32;    /* lanes per record (G) of the batch kernel: 1, 2, 4, 8, 16, 32 */
 constexpr int SPARSE_LANES = 64; /* "lanes" value of the wave-per-record kernel (sparse_kernel.hip) */
 /* the planner picks that kernel when a batch's key runs hold fewer records than this on average */
