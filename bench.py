@@ -618,7 +618,13 @@ def main():
     lfile = os.path.join(ROOT, "profiles", f"lds_{args.config}.json")
     if os.path.exists(lfile) and "lds_issue_ceiling" in result["roofline"]:  # LDS-array occupancy of the same kernel from its PMC pass (the bound that binds)
         with open(lfile) as f:
-            result["roofline"]["lds_issue_ceiling"]["lds_array_busy_measured"] = json.load(f)["lds_array_busy_frac"]
+            lj = json.load(f)
+        ceil = result["roofline"]["lds_issue_ceiling"]
+        ceil["lds_array_busy_measured"] = lj["lds_array_busy_frac"]
+        if "valu_issue_busy_frac" in lj:  # the other issue port of the same loop
+            ceil["valu_issue_busy_measured"] = lj["valu_issue_busy_frac"]
+        if seal_ms:  # the clock the kernel actually ran at: PMC kernel cycles per XCD / this run's seal time
+            ceil["clock_ghz_measured"] = round(lj["kernel_cycles_per_xcd"] / (seal_ms * 1e-3) / 1e9, 3)
     for o in (seal_b, open_b):
         o.close()
     del d_pt, d_ct, d_out, d_aad, d_res

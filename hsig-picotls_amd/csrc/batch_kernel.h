@@ -74,6 +74,9 @@ __host__ __device__ constexpr uint32_t lds_bytes(int log2g)
 #ifndef PURE_BLOCKS
 #define PURE_BLOCKS 2 /* data blocks per lane per iteration of the branch-free loop */
 #endif
+#ifndef KEYSWITCH_PROBE
+#define KEYSWITCH_PROBE 0 /* timing ablation only: 1 = key switches keep their barriers but skip the table build (wrong output) */
+#endif
 #ifndef DEAL_MUTANT
 #define DEAL_MUTANT 0 /* TEST-ONLY broken builds (tools/build_mutants.sh, tests/test_gpu_dealing.py): 1 = the task a wave
                          drew past one chunk is dropped at the next chunk of the key run, 2 = cbase is not advanced */
@@ -1053,7 +1056,8 @@ __global__ void __launch_bounds__(WGT)
         const Chunk ch = chunks[ci];
         if (SPLIT_PROBE != 1 && ch.key != cur_key) {
             __syncthreads();
-            build_ghash_tables(lds, basis + (size_t)ch.key * (BASIS_VECS * 4), LOG2G, !(VALU_TREE != 0 || G >= 32));
+            if (KEYSWITCH_PROBE != 1 || cur_key == 0xffffffffu)
+                build_ghash_tables(lds, basis + (size_t)ch.key * (BASIS_VECS * 4), LOG2G, !(VALU_TREE != 0 || G >= 32));
             if (DYN && threadIdx.x == 0)
                 *task_ctr = 0;
             __syncthreads();
@@ -1063,6 +1067,7 @@ __global__ void __launch_bounds__(WGT)
         }
         if (DEAL_MUTANT == 1)
             have_g = false;
+
         const KeySlot *__restrict__ slot = slots + ch.key;
         const uint32_t *__restrict__ rk = slot->rk;
         const int ntasks = (int)((ch.count + R - 1) / R);

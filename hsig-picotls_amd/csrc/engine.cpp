@@ -983,6 +983,8 @@ static void *mapped_ptr(const void *h)
  * lane groups turn each load / store instruction into longer contiguous runs per record, i.e. fewer, larger PCIe
  * requests.  Measured (tools/hostmem_probe.py, seal+open GiB/s at 4 / 8 / 16 / 32 lanes): 1350-B records 31.7 /
  * 34.8 / 36.7 / 39.5; 16-KiB records - / 36.6 / 40.2 / 41.5; 64 B - 16 KiB over 64K keys at 16 / 32: 28.6 / 36.2.
+ * Records of >= 64 GHASH elements go to the wave-per-record kernel (one 1-KiB run per wave instruction): 16 / 32 / 64
+ * lanes 1350-B records 36.5 / 39.2 / 40.4, 16-KiB records 40.1 / 41.5 / 42.7 (one 1-GiB batch each).
  * Batches for the sparse-key kernel keep it. */
 static int mapped_lanes(const std::vector<ptls_hip_record_t> &recs)
 {
@@ -993,7 +995,7 @@ static int mapped_lanes(const std::vector<ptls_hip_record_t> &recs)
     for (const auto &r : recs)
         sum += (double)((r.aad_len + 15) / 16 + (r.len + 15) / 16 + 1);
     const double mean = sum / (double)recs.size();
-    return mean >= 32 ? 32 : mean >= 16 ? std::max(lanes, 16) : lanes;
+    return mean >= 64 ? SPARSE_LANES : mean >= 32 ? 32 : mean >= 16 ? std::max(lanes, 16) : lanes;
 }
 
 /* PTLS_HIP_TRANSPORT_MAPPED: the batch kernel reads the records from, and writes them to, the caller's pinned host
