@@ -80,14 +80,12 @@ def make_workload(cfg, rank):
         idx = np.arange(base, base + n, dtype=np.uint64)
         keyslot = np.zeros(n, dtype=np.uint32)
         seq = idx.copy()
-    else:  # record i uses key i % K, per-key seq i // K; order records by key
-        K = cfg["keys"]
-        per = n // K
-        kk = np.repeat(np.arange(K, dtype=np.uint64), per)
-        ss = np.tile(np.arange(per, dtype=np.uint64), K)
-        idx = np.uint64(base) + ss * np.uint64(K) + kk
-        keyslot = kk.astype(np.uint32)
-        seq = (idx // np.uint64(K)).astype(np.uint64)
+    else:  # record i uses key i % K, per-key seq i // K; order records by key (any n, not only multiples of K)
+        K = np.uint64(cfg["keys"])
+        allidx = np.arange(base, base + n, dtype=np.uint64)
+        idx = allidx[np.argsort(allidx % K, kind="stable")]
+        keyslot = (idx % K).astype(np.uint32)
+        seq = (idx // K).astype(np.uint64)
     if cfg["L"] is None:
         lens = (np.uint64(64) + splitmix_at(np.uint64(SEED_LEN) ^ idx, 0) % np.uint64(16321)).astype(np.uint64)
     else:

@@ -740,3 +740,39 @@ def test_tls12_record_layer_over_non_temporal_objects(engine, bits):
     assert h_cli.receive(bytes(wire)) == f_cli.receive(bytes(wire))
     for c in (f_srv, h_srv, f_cli, h_cli):
         c.close()
+
+
+@pytest.mark.parametrize("lanes", (0, 1, 8, 32, 64))
+def test_empty_batches_and_empty_records(engine, oracle, lanes):
+    """a batch of no records is a no-op on every path (batch, copy / mapped pipeline); a batch of records with no
+    payload (tag = E_K(J0) ^ GHASH of the AAD and length block only) equals the oracle and opens to length 0"""
+    empty = np.zeros(0, dtype=ptls_hip.RECORD_DTYPE)
+    ks = ptls_hip.KeySet(engine, 16, 1)
+    k0, iv0 = oracle.gen_key(0, 16)
+    ks.set(0, k0, iv0)
+    b = ptls_hip.Batch(engine, empty)
+    b.set_lanes(lanes)
+    buf = torch.zeros(64, dtype=torch.uint8, device="cuda")
+    res = torch.zeros(1, dtype=torch.int64, device="cuda")
+    b.seal(ks, buf, buf, buf)
+    b.open(ks, buf, buf, buf, res)
+    torch.cuda.synchronize()
+    b.close()
+    h = torch.zeros(64, dtype=torch.uint8).pin_memory()
+    h_res = torch.zeros(1, dtype=torch.int64).pin_memory()
+    for t in TRANSPORTS.values():
+        pipe = ptls_hip.Pipeline(engine, 1 << 20, transport=t)
+        pipe.seal(ks, empty, h, h, h)
+        pipe.open(ks, empty, h, h, h, h_res)
+        pipe.close()
+    ks.close()
+    recs = []
+    for i, A in enumerate([0, 0, 5, 13, 16, 17, 0, 32]):
+        key, iv = oracle.gen_key(i % 3, 16)
+        recs.append((key, iv, 1000 + i, oracle.gen_record(50 + i, A), b""))
+    hb = HostBatch(engine, recs)
+    outs = hb.seal(lanes)
+    assert outs == [oracle.seal(*r) for r in recs]
+    res_, pts = hb.open(outs, lanes)
+    assert res_ == [0] * len(recs) and pts == [b""] * len(recs)
+    hb.close()
