@@ -1,6 +1,6 @@
 #!/bin/bash
 # where c4's time goes: AES-only / GHASH-only probes at 16 and 32 lanes, and c4's shape with one factor changed at a time
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 P=hsig-picotls_amd/libptls_hip.so; V=hsig-picotls_amd/variants
 tools/gpu_steps.sh \
   "c4_16:300:python tools/time_cfg.py --config c4 --lanes 16 $P $V/libptls_hip_split1.so $V/libptls_hip_split2.so" \

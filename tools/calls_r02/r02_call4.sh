@@ -1,6 +1,6 @@
 #!/bin/bash
 # round-2 evidence call: host-memory transport probe, c4s sparse-kernel ablations and counters
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 V=hsig-picotls_amd/variants
 tools/gpu_steps.sh \
   "hostmem:300:python tools/hostmem_probe.py" \

@@ -1,6 +1,6 @@
 #!/bin/bash
 # sparse kernel rewrite: parity (sparse + pipeline tests), A/B timing vs the previous sparse kernel, c4s bench
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 V=hsig-picotls_amd/variants
 tools/gpu_steps.sh \
   "tests:600:python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread" \
