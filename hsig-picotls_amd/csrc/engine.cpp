@@ -1606,9 +1606,9 @@ struct PluginSupp {
     uint8_t *output; /* host: supp->output */
 };
 
-/* pinned / device staging layout of one plugin call (256 B): record @0, chunk @64, order @96, result @128,
- * supp descriptor @160, header-protection mask @192 */
-static const size_t ST_REC = 0, ST_CHUNK = 64, ST_ORDER = 96, ST_RESULT = 128, ST_SUPP = 160, ST_MASK = 192;
+/* pinned / device staging layout of one plugin call (256 B): result @128, supp descriptor @160, header-protection
+ * mask @192 (the record descriptor travels in the kernel arguments) */
+static const size_t ST_RESULT = 128, ST_SUPP = 160, ST_MASK = 192;
 
 /* run one record: in/out/aad are the caller's (unpinned) host buffers.  The sparse kernel (one wave per record,
  * its own 8 KiB H^64 table, none for records of <= 64 GHASH elements) serves a single record without building
@@ -1630,12 +1630,7 @@ static uint64_t plugin_run(hip_aead_state *st, bool open, void *output, const vo
     rec.seq = seq;
     rec.len = (uint32_t)len;
     rec.aad_len = (uint32_t)aadlen;
-    const Chunk ch{0, 1, 0, 1};
-    const uint32_t order0 = 0;
     const ptls_hip_supp_t sp{ps != nullptr ? ps->sample_off : 0, 0, 0, PTLS_HIP_SUPP_ENABLE};
-    std::memcpy(st->h_stage + ST_REC, &rec, sizeof(rec));
-    std::memcpy(st->h_stage + ST_CHUNK, &ch, sizeof(ch));
-    std::memcpy(st->h_stage + ST_ORDER, &order0, sizeof(order0));
     std::memcpy(st->h_stage + ST_SUPP, &sp, sizeof(sp));
     if (tag != nullptr) { /* open with a detached tag (ptls_fusion_aesgcm_decrypt, lib/fusion.c:660-661) */
         if (len != 0)
@@ -1647,11 +1642,8 @@ static uint64_t plugin_run(hip_aead_state *st, bool open, void *output, const vo
     if (aadlen != 0)
         std::memcpy(h_aad, aad, aadlen);
     KernelArgs a{};
-    a.recs = reinterpret_cast<const ptls_hip_record_t *>(st->d_stage + ST_REC);
-    a.recs_ord = a.recs; /* one record: chunk order is the caller's */
-    a.order = reinterpret_cast<const uint32_t *>(st->d_stage + ST_ORDER);
-    a.chunks = reinterpret_cast<const Chunk *>(st->d_stage + ST_CHUNK);
-    a.nchunks = 1;
+    a.one = rec; /* by value in the kernel arguments (recs_ord stays null): the kernel's first dependent host read is
+                    the record's own bytes */
     a.in = d_in;
     a.aad = d_aad;
     a.out = d_out;

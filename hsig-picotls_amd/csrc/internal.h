@@ -80,6 +80,9 @@ struct KernelArgs {
     const KeySlot *hp_slots;
     uint32_t hp_nslots; /* supp[i].hp_key >= hp_nslots: that record's mask is left untouched */
     uint8_t *mask;
+    /* sparse kernel only: with recs_ord == nullptr it runs this one record, passed by value in the kernel arguments
+     * (the plugin's single-record calls: no dependent reads of host-staged descriptors) */
+    ptls_hip_record_t one;
 };
 
 /* host-side launchers, defined next to the kernels (aesgcm_kernels.hip, batch_g*.hip) */

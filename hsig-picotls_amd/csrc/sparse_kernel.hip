@@ -125,7 +125,7 @@ __global__ void __launch_bounds__(SPARSE_WG)
                          const Chunk *__restrict__ chunks, uint32_t nchunks, const uint8_t *in, const uint8_t *__restrict__ aad,
                          uint8_t *out, uint64_t *__restrict__ result, const KeySlot *__restrict__ slots,
                          const uint32_t *__restrict__ basis, const uint32_t *__restrict__ t0, const ptls_hip_supp_t *__restrict__ supp,
-                         const KeySlot *__restrict__ hp_slots, uint32_t hp_nslots, uint8_t *mask)
+                         const KeySlot *__restrict__ hp_slots, uint32_t hp_nslots, uint8_t *mask, ptls_hip_record_t one)
 {
     __shared__ __attribute__((aligned(16))) uint8_t lds[SP_TAB + (SPARSE_WG / 64) * 8192];
     static_assert(SP_TAB + (SPARSE_WG / 64) * 8192 <= 163840, "AES tables + per-wave GHASH tables must fit the CU's 160 KiB");
@@ -134,17 +134,21 @@ __global__ void __launch_bounds__(SPARSE_WG)
     const uint32_t tab = __builtin_amdgcn_readfirstlane(SP_TAB + (uint32_t)(threadIdx.x >> 6) * 8192u); /* wave-uniform */
     build_aes_tables_at0(lds, t0);
     __syncthreads();
-    if (nchunks == 0)
-        return;
-    /* build_chunks places the chunks' records contiguously from position 0 */
-    const Chunk last = chunks[nchunks - 1];
-    const uint32_t nrecs = last.first + last.count;
+    /* one record by value (recs_ord == nullptr), or build_chunks' chunks with their records contiguous from 0 */
+    const bool by_value = recs_ord == nullptr;
+    uint32_t nrecs = 1;
+    if (!by_value) {
+        if (nchunks == 0)
+            return;
+        const Chunk last = chunks[nchunks - 1];
+        nrecs = last.first + last.count;
+    }
     const uint32_t waves = gridDim.x * (SPARSE_WG / 64);
     const uint32_t w0 = __builtin_amdgcn_readfirstlane(blockIdx.x * (SPARSE_WG / 64) + (threadIdx.x >> 6));
 
     for (uint32_t pos = w0; pos < nrecs; pos += waves) {
-        const ptls_hip_record_t rec = recs_ord[pos];
-        const uint32_t rec_i = order[pos];
+        const ptls_hip_record_t rec = by_value ? one : recs_ord[pos];
+        const uint32_t rec_i = by_value ? 0u : order[pos];
         const uint32_t key = __builtin_amdgcn_readfirstlane(rec.key);
         const KeySlot *__restrict__ slot = slots + key;
         const uint32_t *__restrict__ rk = slot->rk;
@@ -349,10 +353,10 @@ static hipError_t launch_sparse_one(unsigned grid, hipStream_t s, const KernelAr
 {
     if (aligned)
         hipLaunchKernelGGL((aesgcm_sparse_kernel<R, O, true>), dim3(grid), dim3(SPARSE_WG), 0, s, a.recs_ord, a.order, a.chunks,
-                           a.nchunks, a.in, a.aad, a.out, a.result, a.slots, a.basis, a.t0, a.supp, a.hp_slots, a.hp_nslots, a.mask);
+                           a.nchunks, a.in, a.aad, a.out, a.result, a.slots, a.basis, a.t0, a.supp, a.hp_slots, a.hp_nslots, a.mask, a.one);
     else
         hipLaunchKernelGGL((aesgcm_sparse_kernel<R, O, false>), dim3(grid), dim3(SPARSE_WG), 0, s, a.recs_ord, a.order, a.chunks,
-                           a.nchunks, a.in, a.aad, a.out, a.result, a.slots, a.basis, a.t0, a.supp, a.hp_slots, a.hp_nslots, a.mask);
+                           a.nchunks, a.in, a.aad, a.out, a.result, a.slots, a.basis, a.t0, a.supp, a.hp_slots, a.hp_nslots, a.mask, a.one);
     return hipGetLastError();
 }
 
