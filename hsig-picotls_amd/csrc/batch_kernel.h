@@ -45,6 +45,9 @@ __host__ __device__ constexpr uint32_t lds_bytes(int log2g)
  *   SKEWED       full-block loop with the lane's KP blocks 1/KP of a round apart (0: round-phased)
  *   SETPRIO      wave priority while a wave issues a segment's lookups;  PFPRIO  ... and its prefetch loads
  *   PURE_BLOCKS  KP, data blocks per lane per full-block iteration */
+#ifndef CTRHI_PROBE
+#define CTRHI_PROBE 0 /* timing probe only (wrong output): rounds 1-2 of the skewed loop as if the counter's high byte were fixed */
+#endif
 #ifndef SETPRIO
 #define SETPRIO 1 /* wave priority while issuing a segment's lookups: c2 +6 % measured */
 #endif
@@ -476,7 +479,13 @@ __device__ __forceinline__ void ctr_ghash_skewed(const uint8_t *lds, uint32_t lb
             if (r == 1) {
                 const uint32_t x3 = cw[b] ^ cc.r03;
                 M[b][0] = lT2<3>(lds, x3, lb);
-                M[b][1] = lT2<2>(lds, x3, lb);
+                if (!CTRHI_PROBE)
+                    M[b][1] = lT2<2>(lds, x3, lb);
+            } else if (r == 2 && CTRHI_PROBE) {
+                M[b][0] = lT0<0>(lds, t0[b], lb);
+                M[b][3] = lT2<3>(lds, t0[b], lb);
+                M[b][4] = lT2<2>(lds, t0[b], lb);
+                M[b][6] = lT0<1>(lds, t0[b], lb);
             } else if (r == 2) {
                 M[b][0] = lT0<0>(lds, t0[b], lb);
                 M[b][1] = lT0<1>(lds, t1[b], lb);
@@ -502,7 +511,13 @@ __device__ __forceinline__ void ctr_ghash_skewed(const uint8_t *lds, uint32_t lb
             const int b = fs % KP, r = fs / KP + 1;
             if (r == 1) {
                 t0[b] = cc.k10 ^ rotl8(M[b][0]);
-                t1[b] = cc.k11 ^ M[b][1];
+                if (!CTRHI_PROBE)
+                    t1[b] = cc.k11 ^ M[b][1];
+            } else if (r == 2 && CTRHI_PROBE) {
+                s[b].w0 = cc.k20 ^ M[b][0];
+                s[b].w1 = cc.k21 ^ rotl8(M[b][3]);
+                s[b].w2 = cc.k22 ^ M[b][4];
+                s[b].w3 = cc.k23 ^ rotl8(M[b][6]);
             } else if (r == 2) {
                 s[b].w0 = xor3(cc.k20, M[b][0], rotl8(M[b][1]));
                 s[b].w1 = xor3(cc.k21, M[b][2], rotl8(M[b][3]));

@@ -17,7 +17,7 @@
 
 namespace ptls_hip {
 
-constexpr int NPOW = 7;          /* H^1, H^2, H^4, H^8, H^16 (batch kernel tables), H^32, H^64 (sparse kernel) */
+constexpr int NPOW = 7;          /* H^1 .. H^16 (batch kernel main and tree tables), H^32 (batch kernel main table at G = 32), H^64 (sparse kernel) */
 /* GHASH basis slot: NPOW x 128 vectors P * x^e, then H^1 .. H^64 (the sparse kernel's per-lane final powers) */
 constexpr int LANE_POWS = 64;
 /* HYBRID (measurement switch): this many waves per batch-kernel workgroup (the last ones) run their
