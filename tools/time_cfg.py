@@ -14,6 +14,7 @@ ap.add_argument("--records", type=int, default=0, help="override the config's re
 ap.add_argument("--key-len", type=int, default=0, help="override the key size (16 / 32)")
 ap.add_argument("--fixed-len", type=int, default=0, help="every record this many bytes (instead of the config's lengths)")
 ap.add_argument("--keys", type=int, default=0, help="override the number of keys")
+ap.add_argument("--wg", type=int, default=0, help="workgroup size (512 / 768; 0 = the planner's)")
 args = ap.parse_args()
 import torch
 import bench
@@ -39,10 +40,14 @@ for lib in args.libs:
     sb = ptls_hip.Batch(eng, recs)
     if args.lanes:
         sb.set_lanes(args.lanes)
+    if args.wg:
+        sb.set_workgroup(args.wg)
     ro = recs.copy()
     ro["in_off"], ro["out_off"] = recs["out_off"], recs["in_off"]
     ob = ptls_hip.Batch(eng, ro)
     ob.set_lanes(sb.lanes)
+    if args.wg:
+        ob.set_workgroup(args.wg)
     d_pt = torch.zeros(in_total + 64, dtype=torch.uint8, device="cuda")
     d_ct = torch.zeros(out_total + 64, dtype=torch.uint8, device="cuda")
     d_out = torch.empty(in_total + 64, dtype=torch.uint8, device="cuda")
@@ -57,7 +62,7 @@ for lib in args.libs:
             ts.append((ev[0].elapsed_time(ev[1]), ev[1].elapsed_time(ev[2])))
     s, o = np.median(np.array(ts), axis=0)
     gib = float(lens.sum()) / 2 ** 30
-    print(f"{os.path.basename(lib)} {args.config} lanes={sb.lanes}: seal {s:.3f} ms ({gib / s * 1e3:.1f} GiB/s)  "
+    print(f"{os.path.basename(lib)} {args.config} lanes={sb.lanes} wg={sb.workgroup}: seal {s:.3f} ms ({gib / s * 1e3:.1f} GiB/s)  "
           f"open {o:.3f} ms ({gib / o * 1e3:.1f} GiB/s)", flush=True)
     sb.close(); ob.close(); ks.close(); eng.close()
     del d_pt, d_ct, d_out
