@@ -59,7 +59,7 @@ __global__ void __launch_bounds__(256) aesecb_batch_kernel(const ptls_hip_supp_t
                                                            const uint32_t *__restrict__ t0)
 {
     __shared__ __attribute__((aligned(16))) uint8_t lds[LDS_AES + 65536];
-    build_aes_tables(lds, t0);
+    build_aes_tables<256>(lds, LDS_AES, t0);
     __syncthreads();
     const uint32_t lb_aes = (uint32_t)(threadIdx.x & 31) * 4u | LDS_AES;
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
@@ -71,6 +71,10 @@ __global__ void __launch_bounds__(256) aesecb_batch_kernel(const ptls_hip_supp_t
     }
 }
 
+
+#ifndef KEYSETUP_WIDE_MAX
+#define KEYSETUP_WIDE_MAX 4096 /* slots up to which key setup runs one wave per slot (keysetup_wide_kernel) */
+#endif
 
 /* ======================================================================================= *
  *  key setup: one thread per key slot (setup_crypto, lib/fusion.c:1184-1206, :984-1010)    *
@@ -125,23 +129,21 @@ __device__ __forceinline__ uint8_t xtime8(uint8_t a)
     return (uint8_t)((a << 1) ^ ((a & 0x80) ? 0x1b : 0));
 }
 
-__global__ void keysetup_kernel(KeySlot *slots, uint32_t *basis, const uint8_t *keys, const uint8_t *ivs, uint32_t first,
-                                uint32_t count, int key_size, const uint32_t *t0)
+/* FIPS-197 key expansion (words as raw little-endian uint32, 60 entries, the unused ones 0) and H = E_K(0^128)
+ * with a byte-oriented AES (setup only) */
+__device__ V4 expand_key_h(const uint8_t *key, int key_size, const uint32_t *t0, uint32_t (&w)[60], int &rounds)
 {
-    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
-    if (k >= count)
-        return;
-    KeySlot *slot = slots + first + k;
-    const uint8_t *key = keys + (size_t)k * key_size;
-    const int nk = key_size / 4, rounds = nk + 6, total = 4 * (rounds + 1);
-
-    /* key expansion (FIPS-197 §5.2), words kept as raw little-endian uint32 */
-    uint32_t w[60];
+    const int nk = key_size / 4, total = 4 * (nk + 6 + 1);
+    rounds = nk + 6;
     for (int i = 0; i < nk; ++i)
         w[i] = (uint32_t)key[4 * i] | ((uint32_t)key[4 * i + 1] << 8) | ((uint32_t)key[4 * i + 2] << 16) |
                ((uint32_t)key[4 * i + 3] << 24);
     uint8_t rcon = 1;
-    for (int i = nk; i < total; ++i) {
+    for (int i = nk; i < 60; ++i) {
+        if (i >= total) {
+            w[i] = 0;
+            continue;
+        }
         uint32_t t = w[i - 1];
         if (i % nk == 0) {
             t = (t >> 8) | (t << 24); /* RotWord on raw bytes */
@@ -155,14 +157,6 @@ __global__ void keysetup_kernel(KeySlot *slots, uint32_t *basis, const uint8_t *
         }
         w[i] = w[i - nk] ^ t;
     }
-    for (int i = 0; i < 60; ++i)
-        slot->rk[i] = i < total ? w[i] : 0;
-    slot->rounds = (uint32_t)rounds;
-    for (int i = 0; i < 3; ++i)
-        slot->iv[i] = (uint32_t)ivs[12 * k + 4 * i] | ((uint32_t)ivs[12 * k + 4 * i + 1] << 8) |
-                      ((uint32_t)ivs[12 * k + 4 * i + 2] << 16) | ((uint32_t)ivs[12 * k + 4 * i + 3] << 24);
-
-    /* H = E_K(0^128), byte-oriented AES (setup only) */
     uint8_t s[16], tmp[16];
     for (int i = 0; i < 16; ++i)
         s[i] = (uint8_t)(w[i >> 2] >> (8 * (i & 3)));
@@ -191,6 +185,30 @@ __global__ void keysetup_kernel(KeySlot *slots, uint32_t *basis, const uint8_t *
     h.w1 = (uint32_t)s[4] | ((uint32_t)s[5] << 8) | ((uint32_t)s[6] << 16) | ((uint32_t)s[7] << 24);
     h.w2 = (uint32_t)s[8] | ((uint32_t)s[9] << 8) | ((uint32_t)s[10] << 16) | ((uint32_t)s[11] << 24);
     h.w3 = (uint32_t)s[12] | ((uint32_t)s[13] << 8) | ((uint32_t)s[14] << 16) | ((uint32_t)s[15] << 24);
+    return h;
+}
+
+__device__ void write_slot_keys(KeySlot *slot, const uint32_t (&w)[60], int rounds, const uint8_t *iv)
+{
+    for (int i = 0; i < 60; ++i)
+        slot->rk[i] = w[i];
+    slot->rounds = (uint32_t)rounds;
+    for (int i = 0; i < 3; ++i)
+        slot->iv[i] = (uint32_t)iv[4 * i] | ((uint32_t)iv[4 * i + 1] << 8) | ((uint32_t)iv[4 * i + 2] << 16) |
+                      ((uint32_t)iv[4 * i + 3] << 24);
+}
+
+__global__ void keysetup_kernel(KeySlot *slots, uint32_t *basis, const uint8_t *keys, const uint8_t *ivs, uint32_t first,
+                                uint32_t count, int key_size, const uint32_t *t0)
+{
+    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= count)
+        return;
+    KeySlot *slot = slots + first + k;
+    uint32_t w[60];
+    int rounds;
+    const V4 h = expand_key_h(keys + (size_t)k * key_size, key_size, t0, w, rounds);
+    write_slot_keys(slot, w, rounds, ivs + 12 * (size_t)k);
 
     U128 p = u128_from_raw(h);
     uint4 *bs = reinterpret_cast<uint4 *>(basis) + (size_t)(first + k) * BASIS_VECS;
@@ -221,6 +239,61 @@ __global__ void keysetup_kernel(KeySlot *slots, uint32_t *basis, const uint8_t *
     /* round keys 1..rounds in the bit-sliced form of the batch kernel's hybrid waves (bs8_aes.h) */
     bs8::slice_key(w, rounds, reinterpret_cast<uint32_t *>(bs + BS_KEY_OFF));
 #endif
+}
+
+/* The same outputs with one 64-lane wave per key slot, for a few slots at a time (picotls's setup_crypto keys ONE
+ * context): keysetup_kernel does a slot's ~70 serial GF(2^128) multiplies and 896 basis vectors in one thread
+ * (~540 us for a single slot); here every lane expands the key and squares H up to H^64 itself (no LDS, no
+ * barrier), lane j then writes basis vectors e = j and j + 64 of every plane and the lane power H^(j+1) (at most
+ * six multiplies of the squares), lane 0 the slot's round keys and powers. */
+__global__ void __launch_bounds__(64) keysetup_wide_kernel(KeySlot *slots, uint32_t *basis, const uint8_t *keys,
+                                                           const uint8_t *ivs, uint32_t first, int key_size, const uint32_t *t0)
+{
+    static_assert(LANE_POWS == 64 && NPOW == 7, "one lane power per lane; H^(j+1) from the squares H^(2^t), t < 7");
+    const uint32_t k = blockIdx.x;
+    const int j = (int)threadIdx.x;
+    KeySlot *slot = slots + first + k;
+    uint4 *bs = reinterpret_cast<uint4 *>(basis) + (size_t)(first + k) * BASIS_VECS;
+    uint32_t w[60];
+    int rounds;
+    const V4 h = expand_key_h(keys + (size_t)k * key_size, key_size, t0, w, rounds);
+    V4 pw[NPOW];
+    pw[0] = h;
+    for (int t = 1; t < NPOW; ++t)
+        pw[t] = gf_mul_valu(pw[t - 1], pw[t - 1]);
+    if (j == 0) {
+        write_slot_keys(slot, w, rounds, ivs + 12 * (size_t)k);
+        for (int t = 0; t < NPOW; ++t) {
+            slot->hpow[t][0] = pw[t].w0;
+            slot->hpow[t][1] = pw[t].w1;
+            slot->hpow[t][2] = pw[t].w2;
+            slot->hpow[t][3] = pw[t].w3;
+        }
+#if HYBRID
+        bs8::slice_key(w, rounds, reinterpret_cast<uint32_t *>(bs + BS_KEY_OFF));
+#endif
+    }
+    for (int t = 0; t < NPOW; ++t) {
+        U128 b = u128_from_raw(pw[t]);
+        for (int e = 0; e < j; ++e)
+            b = gf_mulx(b);
+        V4 br = u128_to_raw(b);
+        bs[t * 128 + j] = make_uint4(br.w0, br.w1, br.w2, br.w3);
+        for (int e = 0; e < 64; ++e)
+            b = gf_mulx(b);
+        br = u128_to_raw(b);
+        bs[t * 128 + 64 + j] = make_uint4(br.w0, br.w1, br.w2, br.w3);
+    }
+    const int q1 = j + 1; /* 1 .. 64 */
+    V4 acc = V4{0, 0, 0, 0};
+    bool any = false;
+    for (int t = 0; t < NPOW; ++t) {
+        if ((q1 >> t) & 1) {
+            acc = any ? gf_mul_valu(acc, pw[t]) : pw[t];
+            any = true;
+        }
+    }
+    bs[NPOW * 128 + j] = make_uint4(acc.w0, acc.w1, acc.w2, acc.w3);
 }
 
 /* ======================================================================================= *
@@ -292,6 +365,12 @@ int launch_batch(int lanes, int rounds, bool open, int wg, unsigned grid, void *
 int launch_keysetup(KeySlot *slots, uint32_t *basis, const uint8_t *keys, const uint8_t *ivs, uint32_t first, uint32_t count,
                     int key_size, const uint32_t *t0, void *stream)
 {
+    /* few slots: one wave per slot (latency, ~40 us); many: one thread per slot (throughput: 64K slots in ~1 ms) */
+    if (count <= KEYSETUP_WIDE_MAX) {
+        hipLaunchKernelGGL(keysetup_wide_kernel, dim3(count), dim3(64), 0, static_cast<hipStream_t>(stream), slots, basis, keys,
+                           ivs, first, key_size, t0);
+        return (int)hipGetLastError();
+    }
     const unsigned threads = 64, grid = (count + threads - 1) / threads;
     hipLaunchKernelGGL(keysetup_kernel, dim3(grid), dim3(threads), 0, static_cast<hipStream_t>(stream), slots, basis, keys, ivs,
                        first, count, key_size, t0);

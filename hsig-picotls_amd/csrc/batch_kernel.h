@@ -765,14 +765,27 @@ __device__ __forceinline__ V4 ld_basis(const uint32_t *b, int e)
     return V4{v.x, v.y, v.z, v.w};
 }
 
-/* AES tables: row v = [T0[v] x 32 | rotl16(T0[v]) x 32] */
-__device__ void build_aes_tables(uint8_t *lds, const uint32_t *__restrict__ t0)
+/* AES tables at LDS byte offset `base`: row v = [T0[v] x 32 | rotl16(T0[v]) x 32], 256 B = 16 chunks of 16 B.
+ * Thread i (of NT) writes chunks i, i + NT, ... (row c >> 4, chunk c & 15) with one ds_write_b128 each, the T0 loads
+ * of all its chunks issued first (one global-load latency instead of one per entry: what a single-record launch
+ * waits on); consecutive threads write consecutive 16-B chunks (conflict-free). */
+template <int NT>
+__device__ __forceinline__ void build_aes_tables(uint8_t *lds, uint32_t base, const uint32_t *__restrict__ t0)
 {
-    for (int e = threadIdx.x; e < 256 * 32; e += blockDim.x) {
-        const int v = e >> 5, s = e & 31; /* row v, lane slot s */
-        const uint32_t t = t0[v];
-        *reinterpret_cast<uint32_t *>(lds + LDS_AES + v * 256 + s * 4) = t;
-        *reinterpret_cast<uint32_t *>(lds + LDS_AES + v * 256 + 128 + s * 4) = (t << 16) | (t >> 16);
+    constexpr int IT = (256 * 16 + NT - 1) / NT;
+    uint32_t t[IT];
+#pragma unroll
+    for (int k = 0; k < IT; ++k) {
+        const int c = (int)threadIdx.x + k * NT;
+        t[k] = c < 256 * 16 ? t0[c >> 4] : 0u;
+    }
+#pragma unroll
+    for (int k = 0; k < IT; ++k) {
+        const int c = (int)threadIdx.x + k * NT;
+        if (c < 256 * 16) {
+            const uint32_t x = (c & 15) < 8 ? t[k] : (t[k] << 16) | (t[k] >> 16);
+            lds128_store(lds, base + (uint32_t)(c >> 4) * 256u + (uint32_t)(c & 15) * 16u, V4{x, x, x, x});
+        }
     }
 }
 
@@ -1060,7 +1073,7 @@ __global__ void __launch_bounds__(WGT)
     const int r = lane & (G - 1);
     const int grp = lane >> LOG2G;
 
-    build_aes_tables(lds, t0);
+    build_aes_tables<WGT>(lds, LDS_AES, t0);
     uint32_t cur_key = 0xffffffffu;
     /* DYN: g = the wave's next task in the workgroup's same-key run of chunks (drawn, not yet used);
      * cbase = tasks of the run's chunks before the current one */

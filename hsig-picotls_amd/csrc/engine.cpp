@@ -19,6 +19,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <chrono>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -1365,6 +1366,7 @@ struct hip_aead_state {
     uint8_t *h_stage, *d_stage; /* pinned 256 B: record, chunk, order, result, supp, mask (ST_*) and its device address */
     uint8_t iv[12];
     bool iv_dirty;
+    uint32_t done_seq; /* completion word sequence of the last call (ST_DONE) */
 };
 
 struct hip_aead_context {
@@ -1588,6 +1590,8 @@ static void state_reserve(hip_aead_state *st, size_t len, size_t aadlen)
         aad_cap *= 2;
     cap = (cap + 15) & ~(size_t)15;
     aad_cap = (aad_cap + 15) & ~(size_t)15;
+    /* a previous call's kernel may still be retiring after its completion word (plugin_wait) */
+    plugin_check(hipStreamSynchronize(st->stream), "hipStreamSynchronize");
     if (st->h_io != nullptr) {
         std::memset(st->h_io, 0, st->cap + st->cap + 16 + st->aad_cap);
         plugin_check(hipHostFree(st->h_io), "hipHostFree");
@@ -1607,8 +1611,30 @@ struct PluginSupp {
 };
 
 /* pinned / device staging layout of one plugin call (256 B): result @128, supp descriptor @160, header-protection
- * mask @192 (the record descriptor travels in the kernel arguments) */
-static const size_t ST_RESULT = 128, ST_SUPP = 160, ST_MASK = 192;
+ * mask @192, completion word @224 (the record descriptor travels in the kernel arguments) */
+static const size_t ST_RESULT = 128, ST_SUPP = 160, ST_MASK = 192, ST_DONE = 224;
+
+/* Wait for a plugin launch by spinning on its completion word in pinned host memory (the kernel stores the call's
+ * sequence number there after everything else, system scope) instead of hipStreamSynchronize's completion path
+ * (DESIGN.md §6.2).  A call whose word does not show up within 2 s falls back to the stream synchronize, which
+ * reports a device fault; a kernel that completed without writing the word is a bug. */
+static void plugin_wait(hipStream_t stream, const uint8_t *h_stage, uint32_t seq)
+{
+    const uint32_t *word = reinterpret_cast<const uint32_t *>(h_stage + ST_DONE);
+    const auto t0 = std::chrono::steady_clock::now();
+    for (uint32_t spin = 1;; ++spin) {
+        if (__atomic_load_n(word, __ATOMIC_ACQUIRE) == seq)
+            return;
+        __builtin_ia32_pause();
+        if ((spin & 4095) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(2))
+            break;
+    }
+    plugin_check(hipStreamSynchronize(stream), "hipStreamSynchronize");
+    if (__atomic_load_n(word, __ATOMIC_ACQUIRE) != seq) {
+        g_err = "kernel completed without its completion word";
+        plugin_die("plugin_wait");
+    }
+}
 
 /* run one record: in/out/aad are the caller's (unpinned) host buffers.  The sparse kernel (one wave per record,
  * its own 8 KiB H^64 table, none for records of <= 64 GHASH elements) serves a single record without building
@@ -1657,12 +1683,14 @@ static uint64_t plugin_run(hip_aead_state *st, bool open, void *output, const vo
         a.hp_nslots = 1;
         a.mask = st->d_stage + ST_MASK;
     }
+    a.done = reinterpret_cast<uint32_t *>(st->d_stage + ST_DONE);
+    a.done_seq = ++st->done_seq;
     const int e = launch_batch(SPARSE_LANES, st->ks->key_size == 16 ? 10 : 14, open, 0, 1, st->stream, a, true);
     if (e != 0) {
         g_err = hipGetErrorString((hipError_t)e);
         plugin_die("launch");
     }
-    plugin_check(hipStreamSynchronize(st->stream), "hipStreamSynchronize");
+    plugin_wait(st->stream, st->h_stage, a.done_seq);
     uint64_t result = len;
     if (open) {
         if (len != 0)
@@ -1683,8 +1711,8 @@ static void state_free(hip_aead_state *st)
 {
     {
         DeviceGuard g(st->eng->device);
+        (void)hipStreamSynchronize(st->stream); /* the last call's kernel may still be retiring (plugin_wait) */
         ptls_hip_keyset_free(st->ks);
-        (void)hipStreamSynchronize(st->stream);
         if (st->h_io != nullptr) {
             std::memset(st->h_io, 0, st->cap + st->cap + 16 + st->aad_cap);
             (void)hipHostFree(st->h_io);
@@ -1825,6 +1853,7 @@ static hip_aead_state *state_new(const void *key, const void *iv, size_t key_siz
         return nullptr;
     }
     st->d_stage = static_cast<uint8_t *>(d_stage);
+    std::memset(st->h_stage, 0, 256); /* the completion word starts below the first call's sequence number */
     std::memcpy(st->iv, iv, 12);
     st->iv_dirty = false;
     return st;

@@ -83,6 +83,11 @@ struct KernelArgs {
     /* sparse kernel only: with recs_ord == nullptr it runs this one record, passed by value in the kernel arguments
      * (the plugin's single-record calls: no dependent reads of host-staged descriptors) */
     ptls_hip_record_t one;
+    /* optional completion word (the plugin's pinned staging): the wave that ran the by-value record stores done_seq
+     * there, system scope, after all its output, tag, result and mask stores (the host spins on it instead of a
+     * stream synchronize) */
+    uint32_t *done;
+    uint32_t done_seq;
 };
 
 /* host-side launchers, defined next to the kernels (aesgcm_kernels.hip, batch_g*.hip) */

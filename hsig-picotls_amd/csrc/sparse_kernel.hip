@@ -37,21 +37,13 @@ namespace ptls_hip {
 #ifndef SPARSE_PURE
 #define SPARSE_PURE 1 /* the branch-free skewed stretch over full blocks (0: every element on the generic path) */
 #endif
+#ifndef PLUGIN_PROBE
+#define PLUGIN_PROBE 0 /* timing probe only (wrong output): 1 = no AES table build */
+#endif
 #ifndef SPARSE_PE
 #define SPARSE_PE 2 /* GHASH elements (AES blocks) per lane per main-loop iteration */
 #endif
 constexpr uint32_t SP_TAB = 65536; /* per-wave nibble tables, 8 KiB each */
-
-/* T0 / T2 replicated per lane slot at LDS offset 0 (the batch kernel's layout minus its 64 KiB base) */
-__device__ void build_aes_tables_at0(uint8_t *lds, const uint32_t *__restrict__ t0)
-{
-    for (int e = threadIdx.x; e < 256 * 32; e += blockDim.x) {
-        const int v = e >> 5, s = e & 31;
-        const uint32_t t = t0[v];
-        *reinterpret_cast<uint32_t *>(lds + v * 256 + s * 4) = t;
-        *reinterpret_cast<uint32_t *>(lds + v * 256 + 128 + s * 4) = (t << 16) | (t >> 16);
-    }
-}
 
 /* the wave's LDS operations are processed in order: only the compiler must not move them across this */
 __device__ __forceinline__ void wave_lds_sync()
@@ -125,14 +117,16 @@ __global__ void __launch_bounds__(SPARSE_WG)
                          const Chunk *__restrict__ chunks, uint32_t nchunks, const uint8_t *in, const uint8_t *__restrict__ aad,
                          uint8_t *out, uint64_t *__restrict__ result, const KeySlot *__restrict__ slots,
                          const uint32_t *__restrict__ basis, const uint32_t *__restrict__ t0, const ptls_hip_supp_t *__restrict__ supp,
-                         const KeySlot *__restrict__ hp_slots, uint32_t hp_nslots, uint8_t *mask, ptls_hip_record_t one)
+                         const KeySlot *__restrict__ hp_slots, uint32_t hp_nslots, uint8_t *mask, ptls_hip_record_t one,
+                         uint32_t *done, uint32_t done_seq)
 {
     __shared__ __attribute__((aligned(16))) uint8_t lds[SP_TAB + (SPARSE_WG / 64) * 8192];
     static_assert(SP_TAB + (SPARSE_WG / 64) * 8192 <= 163840, "AES tables + per-wave GHASH tables must fit the CU's 160 KiB");
     const int lane = threadIdx.x & 63;
     const uint32_t lb_aes = (uint32_t)(lane & 31) * 4u; /* table base 0: byte 2 of the address is 0 */
     const uint32_t tab = __builtin_amdgcn_readfirstlane(SP_TAB + (uint32_t)(threadIdx.x >> 6) * 8192u); /* wave-uniform */
-    build_aes_tables_at0(lds, t0);
+    if (!PLUGIN_PROBE)
+        build_aes_tables<SPARSE_WG>(lds, 0, t0); /* the batch kernel's layout at offset 0 */
     __syncthreads();
     /* one record by value (recs_ord == nullptr), or build_chunks' chunks with their records contiguous from 0 */
     const bool by_value = recs_ord == nullptr;
@@ -346,6 +340,13 @@ __global__ void __launch_bounds__(SPARSE_WG)
             }
         }
     }
+    if (done != nullptr && w0 == 0) {
+        /* the by-value record's wave: every store above (the whole wave's, s_waitcnt is wave-wide) reaches system
+         * scope before the completion word does; a vector store (global memory, never the scalar cache) */
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+        if (lane == 0)
+            __hip_atomic_store(done, done_seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
 }
 
 template <int R, bool O>
@@ -353,10 +354,10 @@ static hipError_t launch_sparse_one(unsigned grid, hipStream_t s, const KernelAr
 {
     if (aligned)
         hipLaunchKernelGGL((aesgcm_sparse_kernel<R, O, true>), dim3(grid), dim3(SPARSE_WG), 0, s, a.recs_ord, a.order, a.chunks,
-                           a.nchunks, a.in, a.aad, a.out, a.result, a.slots, a.basis, a.t0, a.supp, a.hp_slots, a.hp_nslots, a.mask, a.one);
+                           a.nchunks, a.in, a.aad, a.out, a.result, a.slots, a.basis, a.t0, a.supp, a.hp_slots, a.hp_nslots, a.mask, a.one, a.done, a.done_seq);
     else
         hipLaunchKernelGGL((aesgcm_sparse_kernel<R, O, false>), dim3(grid), dim3(SPARSE_WG), 0, s, a.recs_ord, a.order, a.chunks,
-                           a.nchunks, a.in, a.aad, a.out, a.result, a.slots, a.basis, a.t0, a.supp, a.hp_slots, a.hp_nslots, a.mask, a.one);
+                           a.nchunks, a.in, a.aad, a.out, a.result, a.slots, a.basis, a.t0, a.supp, a.hp_slots, a.hp_nslots, a.mask, a.one, a.done, a.done_seq);
     return hipGetLastError();
 }
 

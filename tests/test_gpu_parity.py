@@ -776,3 +776,23 @@ def test_empty_batches_and_empty_records(engine, oracle, lanes):
     res_, pts = hb.open(outs, lanes)
     assert res_ == [0] * len(recs) and pts == [b""] * len(recs)
     hb.close()
+
+
+@pytest.mark.parametrize("key_len", [16, 32])
+def test_key_setup_for_many_slots(engine, oracle, key_len):
+    """key setup runs one wave per slot up to 4096 slots per call (keysetup_wide_kernel, every other test) and one
+    thread per slot above (keysetup_kernel): 4100 keys in one call, one record each of 0-4000 B, sealed at every
+    lanes-per-record value (each reads its own H-power planes: H .. H^64 and the lane powers), equal the oracle"""
+    rng = np.random.default_rng(4100 + key_len)
+    recs = []
+    for i in range(4100):
+        key, iv = oracle.gen_key(20000 + i, key_len)
+        L = int(rng.integers(0, 4000))
+        recs.append((key, iv, i, tls_aad(L), oracle.stream(30000 + i, L)))
+    expect = [oracle.seal(*r) for r in recs]
+    hb = HostBatch(engine, recs)
+    for lanes in LANES:
+        outs = hb.seal(lanes)
+        bad = [j for j, (o, e) in enumerate(zip(outs, expect)) if o != e]
+        assert not bad, f"lanes {lanes}: {len(bad)} mismatches, first {bad[:8]}"
+    hb.close()

@@ -4,7 +4,7 @@
 # SRCS (optional) = the kernel sources that get EXTRA (default: all); the others reuse the product build's objects.
 set -e
 cd "$(dirname "$0")/../hsig-picotls_amd"
-make -s -j8 libptls_hip.so >/dev/null
+make -s -j8 "$PWD/libptls_hip.so" >/dev/null  # the rule's target is the absolute path
 name=$1; out=variants/libptls_hip_${name}.so
 ALL="aesgcm_kernels sparse_kernel batch_g1 batch_g2 batch_g4 batch_g8 batch_g16 batch_g32"
 SRCS=${SRCS:-$ALL}
