@@ -56,7 +56,7 @@ template <int ROUNDS>
 __global__ void __launch_bounds__(256) aesecb_batch_kernel(const ptls_hip_supp_t *__restrict__ supp, uint32_t n,
                                                            const uint8_t *__restrict__ src, uint8_t *__restrict__ mask,
                                                            const KeySlot *__restrict__ hp_slots, uint32_t hp_nslots,
-                                                           const uint32_t *__restrict__ t0)
+                                                           const uint32_t *__restrict__ t0, uint32_t *done, uint32_t done_seq)
 {
     __shared__ __attribute__((aligned(16))) uint8_t lds[LDS_AES + 65536];
     build_aes_tables<256>(lds, LDS_AES, t0);
@@ -68,6 +68,12 @@ __global__ void __launch_bounds__(256) aesecb_batch_kernel(const ptls_hip_supp_t
             const V4 m = aes_encrypt<ROUNDS>(lds, lb_aes, hp_slots[sp.hp_key].rk, load_full(src + sp.sample_off));
             store_full(mask + sp.mask_off, m);
         }
+    }
+    if (done != nullptr && blockIdx.x == 0 && threadIdx.x == 0) {
+        /* single-block plugin call (n = 1, handled by this thread): its mask reaches system scope before the
+         * completion word (a vector store) that the host spins on */
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+        __hip_atomic_store(done, done_seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
 }
 
@@ -398,13 +404,15 @@ int launch_tls13_inner(const ptls_hip_record_t *recs, uint32_t n, const uint8_t 
 }
 
 int launch_aesecb(int rounds, const ptls_hip_supp_t *supp, uint32_t n, const uint8_t *src, uint8_t *mask, const KeySlot *hp_slots,
-                  uint32_t hp_nslots, const uint32_t *t0, unsigned grid, void *stream)
+                  uint32_t hp_nslots, const uint32_t *t0, unsigned grid, void *stream, uint32_t *done, uint32_t done_seq)
 {
     hipStream_t s = static_cast<hipStream_t>(stream);
     if (rounds == 10)
-        hipLaunchKernelGGL(aesecb_batch_kernel<10>, dim3(grid), dim3(256), 0, s, supp, n, src, mask, hp_slots, hp_nslots, t0);
+        hipLaunchKernelGGL(aesecb_batch_kernel<10>, dim3(grid), dim3(256), 0, s, supp, n, src, mask, hp_slots, hp_nslots, t0, done,
+                           done_seq);
     else
-        hipLaunchKernelGGL(aesecb_batch_kernel<14>, dim3(grid), dim3(256), 0, s, supp, n, src, mask, hp_slots, hp_nslots, t0);
+        hipLaunchKernelGGL(aesecb_batch_kernel<14>, dim3(grid), dim3(256), 0, s, supp, n, src, mask, hp_slots, hp_nslots, t0, done,
+                           done_seq);
     return (int)hipGetLastError();
 }
 

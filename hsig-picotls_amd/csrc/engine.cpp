@@ -1389,6 +1389,28 @@ static void plugin_check(hipError_t e, const char *what)
     }
 }
 
+/* Wait for a plugin launch by spinning on its completion word in pinned host memory (the kernel stores the call's
+ * sequence number there after everything else, system scope) instead of hipStreamSynchronize's completion path
+ * (DESIGN.md §6.2).  A call whose word does not show up within 2 s falls back to the stream synchronize, which
+ * reports a device fault; a kernel that completed without writing the word is a bug. */
+static void plugin_wait(hipStream_t stream, const uint8_t *word_p, uint32_t seq)
+{
+    const uint32_t *word = reinterpret_cast<const uint32_t *>(word_p);
+    const auto t0 = std::chrono::steady_clock::now();
+    for (uint32_t spin = 1;; ++spin) {
+        if (__atomic_load_n(word, __ATOMIC_ACQUIRE) == seq)
+            return;
+        __builtin_ia32_pause();
+        if ((spin & 4095) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(2))
+            break;
+    }
+    plugin_check(hipStreamSynchronize(stream), "hipStreamSynchronize");
+    if (__atomic_load_n(word, __ATOMIC_ACQUIRE) != seq) {
+        g_err = "kernel completed without its completion word";
+        plugin_die("plugin_wait");
+    }
+}
+
 /* ---- CTR cipher for header protection (replaces lib/fusion.c:1050-1100) ---------------------------- */
 
 struct hip_ctr_state {
@@ -1399,6 +1421,7 @@ struct hip_ctr_state {
     uint8_t *d_stage; /* its device address: the kernel reads and writes it in place */
     uint8_t bits[16];
     bool ready;
+    uint32_t done_seq; /* completion word sequence of the last block (ECB_DONE) */
 };
 
 struct hip_ctr_context {
@@ -1415,6 +1438,9 @@ static const hip_ctr_state *ctr_state_of(const ptls_cipher_context_t *c)
     return reinterpret_cast<const hip_ctr_context *>(c)->st;
 }
 
+/* ECB staging (128 B pinned): supp descriptor @0, input block @32, output block @48, completion word @64 */
+static const size_t ECB_DONE = 64;
+
 /* one AES-ECB block on the device with the state's key (fusion: aesecb_encrypt, lib/fusion.c:322-334) */
 static void ecb_block(hip_ctr_state *st, const void *src, uint8_t dst[16])
 {
@@ -1423,12 +1449,13 @@ static void ecb_block(hip_ctr_state *st, const void *src, uint8_t dst[16])
     std::memcpy(st->h_stage, &sp, sizeof(sp));
     std::memcpy(st->h_stage + 32, src, 16);
     const int e = launch_aesecb(st->ks->key_size == 16 ? 10 : 14, reinterpret_cast<const ptls_hip_supp_t *>(st->d_stage), 1,
-                                st->d_stage, st->d_stage, st->ks->d_slots, 1, st->eng->d_t0, 1, st->stream);
+                                st->d_stage, st->d_stage, st->ks->d_slots, 1, st->eng->d_t0, 1, st->stream,
+                                reinterpret_cast<uint32_t *>(st->d_stage + ECB_DONE), ++st->done_seq);
     if (e != 0) {
         g_err = hipGetErrorString((hipError_t)e);
         plugin_die("ecb launch");
     }
-    plugin_check(hipStreamSynchronize(st->stream), "ecb sync");
+    plugin_wait(st->stream, st->h_stage + ECB_DONE, st->done_seq);
     std::memcpy(dst, st->h_stage + 48, 16);
     std::memset(st->h_stage + 32, 0, 32);
 }
@@ -1469,7 +1496,7 @@ static hip_ctr_state *ecb_state_new(const void *key, size_t key_size)
     }
     st->ks = ptls_hip_keyset_new(eng, key_size, 1);
     void *d_stage = nullptr;
-    const bool ok = st->ks != nullptr && hipHostMalloc(&st->h_stage, 64, hipHostMallocDefault) == hipSuccess &&
+    const bool ok = st->ks != nullptr && hipHostMalloc(&st->h_stage, 128, hipHostMallocDefault) == hipSuccess &&
                     hipHostGetDevicePointer(&d_stage, st->h_stage, 0) == hipSuccess &&
                     ptls_hip_keyset_set(st->ks, 0, 1, key, nullptr, st->stream) == 0;
     st->d_stage = static_cast<uint8_t *>(d_stage);
@@ -1481,6 +1508,7 @@ static hip_ctr_state *ecb_state_new(const void *key, size_t key_size)
         delete st;
         return nullptr;
     }
+    std::memset(st->h_stage, 0, 128); /* the completion word starts below the first block's sequence number */
     return st;
 }
 
@@ -1488,10 +1516,10 @@ static void ecb_state_free(hip_ctr_state *st)
 {
     {
         DeviceGuard g(st->eng->device);
+        (void)hipStreamSynchronize(st->stream); /* the last block's kernel may still be retiring (plugin_wait) */
         ptls_hip_keyset_free(st->ks);
-        (void)hipStreamSynchronize(st->stream);
         if (st->h_stage != nullptr)
-            std::memset(st->h_stage, 0, 64);
+            std::memset(st->h_stage, 0, 128);
         (void)hipHostFree(st->h_stage);
         (void)hipStreamDestroy(st->stream);
     }
@@ -1614,27 +1642,6 @@ struct PluginSupp {
  * mask @192, completion word @224 (the record descriptor travels in the kernel arguments) */
 static const size_t ST_RESULT = 128, ST_SUPP = 160, ST_MASK = 192, ST_DONE = 224;
 
-/* Wait for a plugin launch by spinning on its completion word in pinned host memory (the kernel stores the call's
- * sequence number there after everything else, system scope) instead of hipStreamSynchronize's completion path
- * (DESIGN.md §6.2).  A call whose word does not show up within 2 s falls back to the stream synchronize, which
- * reports a device fault; a kernel that completed without writing the word is a bug. */
-static void plugin_wait(hipStream_t stream, const uint8_t *h_stage, uint32_t seq)
-{
-    const uint32_t *word = reinterpret_cast<const uint32_t *>(h_stage + ST_DONE);
-    const auto t0 = std::chrono::steady_clock::now();
-    for (uint32_t spin = 1;; ++spin) {
-        if (__atomic_load_n(word, __ATOMIC_ACQUIRE) == seq)
-            return;
-        __builtin_ia32_pause();
-        if ((spin & 4095) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(2))
-            break;
-    }
-    plugin_check(hipStreamSynchronize(stream), "hipStreamSynchronize");
-    if (__atomic_load_n(word, __ATOMIC_ACQUIRE) != seq) {
-        g_err = "kernel completed without its completion word";
-        plugin_die("plugin_wait");
-    }
-}
 
 /* run one record: in/out/aad are the caller's (unpinned) host buffers.  The sparse kernel (one wave per record,
  * its own 8 KiB H^64 table, none for records of <= 64 GHASH elements) serves a single record without building
@@ -1690,7 +1697,7 @@ static uint64_t plugin_run(hip_aead_state *st, bool open, void *output, const vo
         g_err = hipGetErrorString((hipError_t)e);
         plugin_die("launch");
     }
-    plugin_wait(st->stream, st->h_stage, a.done_seq);
+    plugin_wait(st->stream, st->h_stage + ST_DONE, a.done_seq);
     uint64_t result = len;
     if (open) {
         if (len != 0)

@@ -102,7 +102,8 @@ int launch_batch(int lanes, int rounds, bool open, int wg, unsigned grid, void *
 int launch_keysetup(KeySlot *slots, uint32_t *basis, const uint8_t *keys, const uint8_t *ivs, uint32_t first, uint32_t count,
                     int key_size, const uint32_t *t0, void *stream);
 int launch_aesecb(int rounds, const ptls_hip_supp_t *supp, uint32_t n, const uint8_t *src, uint8_t *mask, const KeySlot *hp_slots,
-                  uint32_t hp_nslots, const uint32_t *t0, unsigned grid, void *stream);
+                  uint32_t hp_nslots, const uint32_t *t0, unsigned grid, void *stream,
+                  uint32_t *done = nullptr, uint32_t done_seq = 0);
 int launch_tls13_headers(const ptls_hip_record_t *recs, uint32_t n, uint8_t *hdr, unsigned grid, void *stream);
 int launch_tls13_inner(const ptls_hip_record_t *recs, uint32_t n, const uint8_t *out, uint64_t *result, unsigned grid, void *stream);
 int launch_derive_traffic_keys(const uint8_t *secrets_in, uint8_t *secrets_out, uint32_t count, int hash_size, int key_size,

@@ -31,4 +31,13 @@ out = {"lib": os.path.basename(ptls_hip.LIB_PATH), "torch_noop_launch_sync_us": 
 for L in (0, 16, 1500, 16384):
     r = ref_ptlsbench(hip, 1000, L)
     out[f"L{L}"] = {"enc_us": r["enc_us_per_call"], "dec_us": r["dec_us_per_call"]}
+ecb = ptls_hip.AesEcb(bytes(range(16)))
+blk = bytes(16)
+for _ in range(50):
+    blk = ecb.encrypt(blk)
+t0 = time.perf_counter()
+for _ in range(1000):
+    blk = ecb.encrypt(blk)
+out["aesecb_encrypt_us"] = round((time.perf_counter() - t0) / 1000 * 1e6, 2)  # one block per call (CTR do_init, HP mask)
+ecb.close()
 print(json.dumps(out), flush=True)
