@@ -159,6 +159,14 @@ __global__ void __launch_bounds__(SPARSE_WG)
         const uint32_t n0 = __builtin_amdgcn_readfirstlane(slot->iv[0]),
                        n1 = __builtin_amdgcn_readfirstlane(slot->iv[1] ^ bswap32((uint32_t)(rec.seq >> 32))),
                        n2 = __builtin_amdgcn_readfirstlane(slot->iv[2] ^ bswap32((uint32_t)rec.seq));
+        const int iters = (N + 63) >> 6;
+        const bool horner = SPARSE_ABLATE != 3 && iters > 1; /* N <= 64: one element per lane, no Horner step */
+        V4 b[4];
+        /* a single record (the plugin's launch): the H^64 basis loads go out before the counter-mode constants, so their
+         * memory latency overlaps that LDS chain (in batches other waves hide it; there the early loads cost c4s open
+         * 2.5 %, measured) */
+        if (horner && by_value)
+            load_wave_basis(bs + 6 * 128, lane, b); /* H^64 */
         /* the record (and so its counter-mode constants) is the wave's alone: keep them in SGPRs */
         CtrConst cc = ctr_const(lds, lb_aes, rk, n0, n1, n2);
         cc.k10 = __builtin_amdgcn_readfirstlane(cc.k10);
@@ -168,12 +176,10 @@ __global__ void __launch_bounds__(SPARSE_WG)
         cc.k22 = __builtin_amdgcn_readfirstlane(cc.k22);
         cc.k23 = __builtin_amdgcn_readfirstlane(cc.k23);
         cc.r03 = __builtin_amdgcn_readfirstlane(cc.r03);
-        const int iters = (N + 63) >> 6;
         wave_lds_sync(); /* the previous record's Horner reads of the table are done */
-        if (SPARSE_ABLATE != 3 && iters > 1) { /* N <= 64: one element per lane, no Horner step */
-            /* (loading these during the previous record's VALU combine measured no faster: other waves hide it) */
-            V4 b[4];
-            load_wave_basis(bs + 6 * 128, lane, b); /* H^64 */
+        if (horner) { /* (loading the basis during the previous record's VALU combine measured no faster: other waves hide it) */
+            if (!by_value)
+                load_wave_basis(bs + 6 * 128, lane, b); /* H^64 */
             store_wave_table(lds, tab, b, lane);
         }
         wave_lds_sync();
@@ -239,7 +245,9 @@ __global__ void __launch_bounds__(SPARSE_WG)
         const int mhi = lastc + na - 63 >= 0 ? ((lastc + na - 63) >> 6) + 1 : 0; /* m < mhi: lane 63's block <= lastc */
         const int npure = SPARSE_PURE && mhi > pm0 ? (mhi - pm0) / KP : 0;
         const int pm1 = pm0 + npure * KP;
-        generic_range(0, pm0);
+        /* without a stretch the head and tail are one range: element pairs straddling pm0 share one round trip to the
+         * record's memory (a single record read over PCIe by the plugin: one load latency instead of two) */
+        generic_range(0, npure ? pm0 : iters);
         if (npure) {
             const int c0 = 64 * pm0 + lane - na; /* the lane's first data block of the stretch */
             const uint8_t *src = in_p + 16 * (size_t)c0;
@@ -308,7 +316,8 @@ __global__ void __launch_bounds__(SPARSE_WG)
                     y = v4xor(gh_mul_nibble(lds, tab, y), pend[b]);
             }
         }
-        generic_range(pm1, iters);
+        if (npure)
+            generic_range(pm1, iters);
 
         /* lane l's sum times H^(q+1), q = distance of its last element from the end of the GHASH input, on the
          * VALU; the XOR butterfly then sums the 64 lanes (ghash_combine) */
