@@ -78,7 +78,9 @@ __host__ __device__ constexpr uint32_t lds_bytes(int log2g)
 #define PURE_BLOCKS 2 /* data blocks per lane per iteration of the branch-free loop */
 #endif
 #ifndef KEYSWITCH_PROBE
-#define KEYSWITCH_PROBE 0 /* timing ablation only: 1 = key switches keep their barriers but skip the table build (wrong output) */
+#define KEYSWITCH_PROBE 0 /* timing ablation only (wrong output): 1 = key switches keep their barriers but skip the table build;
+                           * 2 (with DYN_DEAL=0) = key switches after the first neither wait nor rebuild; 3 = the same with
+                           * dynamic dealing running on across keys */
 #endif
 #ifndef DEAL_MUTANT
 #define DEAL_MUTANT 0 /* TEST-ONLY broken builds (tools/build_mutants.sh, tests/test_gpu_dealing.py): 1 = the task a wave
@@ -1082,7 +1084,11 @@ __global__ void __launch_bounds__(WGT)
 
     for (uint32_t ci = blockIdx.x; ci < nchunks; ci += gridDim.x) {
         const Chunk ch = chunks[ci];
-        if (SPLIT_PROBE != 1 && ch.key != cur_key) {
+        if ((KEYSWITCH_PROBE == 2 || KEYSWITCH_PROBE == 3) && cur_key != 0xffffffffu && ch.key != cur_key) {
+            /* timing bound only: later key switches neither wait nor rebuild; with DYN (3) the workgroup's task counter
+             * and the waves' cursors run on across keys as across the chunks of one key run */
+            cur_key = ch.key;
+        } else if (SPLIT_PROBE != 1 && ch.key != cur_key) {
             __syncthreads();
             if (KEYSWITCH_PROBE != 1 || cur_key == 0xffffffffu)
                 build_ghash_tables(lds, basis + (size_t)ch.key * (BASIS_VECS * 4), LOG2G, !(VALU_TREE != 0 || G >= 32));
