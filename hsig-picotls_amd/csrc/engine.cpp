@@ -402,19 +402,19 @@ extern "C" int ptls_hip_keyset_xor_iv(ptls_hip_keyset_t *ks, size_t slot, const 
  * records each (a server's connections): a workgroup works on one key at a time (its GHASH tables fill
  * the LDS), so with 8 lanes a 64-record key run gives only 8 wave tasks to 12 waves; 16 lanes per
  * record doubles the tasks per key run (measured on the 64K-key BASELINE shape). */
-static int choose_lanes(const std::vector<ptls_hip_record_t> &recs)
+static int choose_lanes(const ptls_hip_record_t *recs, size_t n)
 {
-    if (recs.empty())
+    if (n == 0)
         return 1;
     double sum = 0;
     size_t runs = 1;
-    for (size_t i = 0; i < recs.size(); ++i) {
+    for (size_t i = 0; i < n; ++i) {
         sum += (double)((recs[i].aad_len + 15) / 16 + (recs[i].len + 15) / 16 + 1);
         if (i != 0 && recs[i].key != recs[i - 1].key)
             ++runs;
     }
-    const double mean = sum / (double)recs.size();
-    const double per_run = (double)recs.size() / (double)runs;
+    const double mean = sum / (double)n;
+    const double per_run = (double)n / (double)runs;
     const int g = mean >= 128 ? 8 : mean >= 48 ? 4 : mean >= 16 ? 2 : 1;
     /* key runs too short to amortise the per-key GHASH tables: the key-independent wave-per-record kernel */
     if (per_run < SPARSE_MAX_PER_RUN)
@@ -464,12 +464,31 @@ static void build_chunks(const ptls_hip_record_t *recs, size_t n, int lanes, uns
         /* the sparse kernel keeps no per-key workgroup state and its waves take records grid-stride: in
          * decreasing length over the whole batch every wave gets a similar share of bytes.  One chunk holds
          * the record count (the kernel reads nothing else from it); its key field names no slot. */
+        bool sorted = true;
+        uint32_t max_len = 0;
         for (size_t i = 0; i < n; ++i) {
             order[i] = (uint32_t)i;
             if (((recs[i].in_off | recs[i].out_off | recs[i].aad_off) & 15) != 0)
                 all_aligned = false;
+            if (i != 0 && recs[i].len > recs[i - 1].len)
+                sorted = false;
+            max_len = std::max(max_len, recs[i].len);
         }
-        std::stable_sort(order.begin(), order.end(), [&](uint32_t x, uint32_t y) { return recs[x].len > recs[y].len; });
+        /* (the host plans every slice of a host-resident pipeline while the device runs the previous one: a comparison
+         * sort of ~200K QUIC records per slice took longer than the slice's kernel) */
+        if (!sorted && max_len < (1u << 24)) {
+            /* stable counting sort by decreasing 16-byte block count: the kernel balances GHASH elements, not bytes */
+            const uint32_t nb = (max_len >> 4) + 1;
+            std::vector<uint32_t> start(nb + 1, 0);
+            for (size_t i = 0; i < n; ++i)
+                ++start[nb - 1 - (recs[i].len >> 4) + 1];
+            for (uint32_t b = 0; b < nb; ++b)
+                start[b + 1] += start[b];
+            for (size_t i = 0; i < n; ++i)
+                order[start[nb - 1 - (recs[i].len >> 4)]++] = (uint32_t)i;
+        } else if (!sorted) {
+            std::stable_sort(order.begin(), order.end(), [&](uint32_t x, uint32_t y) { return recs[x].len > recs[y].len; });
+        }
         if (n != 0)
             ch.push_back(Chunk{0, (uint32_t)n, 0xffffffffu, all_aligned ? 1u : 0u});
         return;
@@ -548,7 +567,7 @@ extern "C" ptls_hip_batch_t *ptls_hip_batch_new(ptls_hip_engine_t *eng, const pt
     b->max_key = 0;
     for (size_t i = 0; i < n; ++i)
         b->max_key = std::max(b->max_key, recs[i].key);
-    b->auto_lanes = b->lanes = choose_lanes(b->h_recs);
+    b->auto_lanes = b->lanes = choose_lanes(b->h_recs.data(), b->h_recs.size());
     if (n != 0) {
         if (hipMalloc(&b->d_recs, n * sizeof(ptls_hip_record_t)) != hipSuccess ||
             hipMemcpy(b->d_recs, recs, n * sizeof(ptls_hip_record_t), hipMemcpyHostToDevice) != hipSuccess) {
@@ -987,16 +1006,28 @@ static void *mapped_ptr(const void *h)
  * Records of >= 64 GHASH elements go to the wave-per-record kernel (one 1-KiB run per wave instruction): 16 / 32 / 64
  * lanes 1350-B records 36.5 / 39.2 / 40.4, 16-KiB records 40.1 / 41.5 / 42.7 (one 1-GiB batch each).
  * Batches for the sparse-key kernel keep it. */
-static int mapped_lanes(const std::vector<ptls_hip_record_t> &recs)
+static int mapped_lanes(const ptls_hip_record_t *recs, size_t n)
 {
-    const int lanes = choose_lanes(recs);
-    if (lanes == SPARSE_LANES || recs.empty())
+    const int lanes = choose_lanes(recs, n);
+    if (lanes == SPARSE_LANES || n == 0)
         return lanes;
     double sum = 0;
-    for (const auto &r : recs)
-        sum += (double)((r.aad_len + 15) / 16 + (r.len + 15) / 16 + 1);
-    const double mean = sum / (double)recs.size();
+    for (size_t i = 0; i < n; ++i)
+        sum += (double)((recs[i].aad_len + 15) / 16 + (recs[i].len + 15) / 16 + 1);
+    const double mean = sum / (double)n;
     return mean >= 64 ? SPARSE_LANES : mean >= 32 ? 32 : mean >= 16 ? std::max(lanes, 16) : lanes;
+}
+
+/* The kernels read the descriptors in plan order (recs_ord).  When the plan keeps the caller's order (records that
+ * already come as the planner sorts them: equal lengths, non-increasing lengths within each key run), the caller-order
+ * copy serves as both: no host gather and one descriptor upload less per pipeline slice (a 1 GiB slice set of QUIC
+ * records is ~800K descriptors; the host plans each slice while the device runs the previous one). */
+static bool identity_order(const std::vector<uint32_t> &order, size_t n)
+{
+    for (size_t t = 0; t < n; ++t)
+        if (order[t] != (uint32_t)t)
+            return false;
+    return true;
 }
 
 /* PTLS_HIP_TRANSPORT_MAPPED: the batch kernel reads the records from, and writes them to, the caller's pinned host
@@ -1027,15 +1058,18 @@ static int pipeline_run_mapped(ptls_hip_pipeline_t *p, ptls_hip_keyset_t *ks, co
         if (s.busy)
             HIP_TRY(hipEventSynchronize(s.done), PTLS_HIP_ENODEV);
         std::memcpy(s.h_recs, recs + i, cnt * sizeof(ptls_hip_record_t));
-        const int lanes = mapped_lanes(std::vector<ptls_hip_record_t>(s.h_recs, s.h_recs + cnt));
+        const int lanes = mapped_lanes(s.h_recs, cnt);
         bool aligned;
         build_chunks(s.h_recs, cnt, lanes, (unsigned)p->eng->ncu, ch, order, aligned);
         std::memcpy(s.h_chunks, ch.data(), ch.size() * sizeof(Chunk));
         std::memcpy(s.h_order, order.data(), cnt * sizeof(uint32_t));
-        for (size_t t = 0; t < cnt; ++t)
-            s.h_recs_ord[t] = s.h_recs[order[t]];
-        HIP_TRY(hipMemcpyAsync(s.d_recs_ord, s.h_recs_ord, cnt * sizeof(ptls_hip_record_t), hipMemcpyHostToDevice, s.stream),
-                PTLS_HIP_ENODEV);
+        const bool ident = identity_order(order, cnt);
+        if (!ident) {
+            for (size_t t = 0; t < cnt; ++t)
+                s.h_recs_ord[t] = s.h_recs[order[t]];
+            HIP_TRY(hipMemcpyAsync(s.d_recs_ord, s.h_recs_ord, cnt * sizeof(ptls_hip_record_t), hipMemcpyHostToDevice, s.stream),
+                    PTLS_HIP_ENODEV);
+        }
         HIP_TRY(hipMemcpyAsync(s.d_order, s.h_order, cnt * sizeof(uint32_t), hipMemcpyHostToDevice, s.stream), PTLS_HIP_ENODEV);
         HIP_TRY(hipMemcpyAsync(s.d_recs, s.h_recs, cnt * sizeof(ptls_hip_record_t), hipMemcpyHostToDevice, s.stream),
                 PTLS_HIP_ENODEV);
@@ -1054,7 +1088,7 @@ static int pipeline_run_mapped(ptls_hip_pipeline_t *p, ptls_hip_keyset_t *ks, co
         uint64_t *res = d_res != nullptr ? d_res + i : s.d_result;
         KernelArgs a{};
         a.recs = s.d_recs;
-        a.recs_ord = s.d_recs_ord;
+        a.recs_ord = ident ? s.d_recs : s.d_recs_ord;
         a.order = s.d_order;
         a.chunks = s.d_chunks;
         a.nchunks = (uint32_t)ch.size();
@@ -1194,11 +1228,7 @@ static int pipeline_run(ptls_hip_pipeline_t *p, ptls_hip_keyset_t *ks, const ptl
             s.h_recs[t].out_off -= out_base;
             s.h_recs[t].aad_off -= aad_in_out ? out_base : aad_in_in ? in_base : aad_base;
         }
-        int lanes;
-        {
-            std::vector<ptls_hip_record_t> tmp(s.h_recs, s.h_recs + cnt);
-            lanes = choose_lanes(tmp);
-        }
+        const int lanes = choose_lanes(s.h_recs, cnt);
         bool aligned;
         build_chunks(s.h_recs, cnt, lanes, (unsigned)p->eng->ncu, ch, order, aligned);
         const uint64_t mask_base = mk.lo & ~(uint64_t)15;
@@ -1220,10 +1250,13 @@ static int pipeline_run(ptls_hip_pipeline_t *p, ptls_hip_keyset_t *ks, const ptl
         }
         std::memcpy(s.h_chunks, ch.data(), ch.size() * sizeof(Chunk));
         std::memcpy(s.h_order, order.data(), cnt * sizeof(uint32_t));
-        for (size_t t = 0; t < cnt; ++t)
-            s.h_recs_ord[t] = s.h_recs[order[t]];
-        HIP_TRY(hipMemcpyAsync(s.d_recs_ord, s.h_recs_ord, cnt * sizeof(ptls_hip_record_t), hipMemcpyHostToDevice, s.stream),
-                PTLS_HIP_ENODEV);
+        const bool ident = identity_order(order, cnt);
+        if (!ident) {
+            for (size_t t = 0; t < cnt; ++t)
+                s.h_recs_ord[t] = s.h_recs[order[t]];
+            HIP_TRY(hipMemcpyAsync(s.d_recs_ord, s.h_recs_ord, cnt * sizeof(ptls_hip_record_t), hipMemcpyHostToDevice, s.stream),
+                    PTLS_HIP_ENODEV);
+        }
         HIP_TRY(hipMemcpyAsync(s.d_order, s.h_order, cnt * sizeof(uint32_t), hipMemcpyHostToDevice, s.stream), PTLS_HIP_ENODEV);
         HIP_TRY(hipMemcpyAsync(s.d_recs, s.h_recs, cnt * sizeof(ptls_hip_record_t), hipMemcpyHostToDevice, s.stream),
                 PTLS_HIP_ENODEV);
@@ -1241,7 +1274,7 @@ static int pipeline_run(ptls_hip_pipeline_t *p, ptls_hip_keyset_t *ks, const ptl
         }
         KernelArgs a{};
         a.recs = s.d_recs;
-        a.recs_ord = s.d_recs_ord;
+        a.recs_ord = ident ? s.d_recs : s.d_recs_ord;
         a.order = s.d_order;
         a.chunks = s.d_chunks;
         a.nchunks = (uint32_t)ch.size();
