@@ -4,7 +4,7 @@
 On 1 GiB of c2-shaped records in pinned host memory: ptls_hip_pipeline_seal/open over the MAPPED transport (the
 kernels read and write host memory) alone, over the COPY transport (SDMA slices) alone, and the batch split between
 the two, each part on its own pipeline driven from its own host thread (ctypes releases the GIL), for several
-split fractions (usage: transport_mix_probe.py [config] [fractions, e.g. 0,0.25,1]).  Reports seal+open GiB/s of the whole batch.  Timing plus a round-trip check; one JSON line."""
+split fractions (usage: transport_mix_probe.py [config] [fractions, e.g. 0,0.25,1] [pipeline slice MiB, default 64]).  Reports seal+open GiB/s of the whole batch.  Timing plus a round-trip check; one JSON line."""
 import json
 import os
 import sys
@@ -49,7 +49,8 @@ def main():
     ro = recs.copy()
     ro["in_off"], ro["out_off"] = recs["out_off"], recs["in_off"]
     sumL = float(lens.sum())
-    pipes = {t: ptls_hip.Pipeline(eng, 64 << 20, transport=t) for t in (ptls_hip.TRANSPORT_MAPPED, ptls_hip.TRANSPORT_COPY)}
+    slice_mib = int(sys.argv[3]) if len(sys.argv) > 3 else 64
+    pipes = {t: ptls_hip.Pipeline(eng, slice_mib << 20, transport=t) for t in (ptls_hip.TRANSPORT_MAPPED, ptls_hip.TRANSPORT_COPY)}
     res_np = h_res.numpy()
 
     def run(split, reps=3):
@@ -84,12 +85,12 @@ def main():
         return {"copy_fraction": split, "seal_gibps": round(sumL / t_s / GIB, 2), "open_gibps": round(sumL / t_o / GIB, 2),
                 "seal_open_gibps": round(2 * sumL / (t_s + t_o) / GIB, 2), "roundtrip_ok": ok}
 
-    out = {"config": cfg["desc"], "records": n, "runs": []}
+    out = {"config": cfg["desc"], "records": n, "slice_mib": slice_mib, "runs": []}
     splits = [float(x) for x in sys.argv[2].split(",")] if len(sys.argv) > 2 else [0.0, 1.0, 0.15, 0.25, 0.35, 0.5]
     for split in splits:
         r = run(split)
         out["runs"].append(r)
-        print(r, flush=True)
+        print(dict(r, slice_mib=slice_mib), flush=True)
     print(json.dumps(out), flush=True)
     for p in pipes.values():
         p.close()
