@@ -796,3 +796,48 @@ def test_key_setup_for_many_slots(engine, oracle, key_len):
         bad = [j for j, (o, e) in enumerate(zip(outs, expect)) if o != e]
         assert not bad, f"lanes {lanes}: {len(bad)} mismatches, first {bad[:8]}"
     hb.close()
+
+
+@pytest.mark.parametrize("transport", ["copy", "mapped"])
+@pytest.mark.parametrize("shape", ["equal", "descending"])
+def test_host_pipeline_plan_keeps_caller_order(engine, oracle, transport, shape):
+    """records that already come as the planner orders them (equal lengths, or non-increasing within each key run):
+    the pipeline reuses the caller-order descriptors as the plan-order ones (no gather, one upload per slice,
+    engine.cpp identity_order); several slices, two key runs; bit-exact vs the oracle and opened back"""
+    n = 1200
+    if shape == "equal":
+        lens = [1350] * n
+    else:
+        lens = sorted((int(x) for x in np.random.default_rng(11).integers(0, 5000, n // 2)), reverse=True) * 2
+    recs_in = []
+    for i, L in enumerate(lens):
+        key, iv = oracle.gen_key(50 + i // (n // 2), 16)
+        recs_in.append((key, iv, i, tls_aad(L), oracle.gen_record(9000 + i, L)))
+    recs, in_total, out_total, aad_total = ptls_hip.layout_records(lens, [5] * n, [i // (n // 2) for i in range(n)],
+                                                                   np.arange(n), align=16, tag_in_input=True)
+    ks = ptls_hip.KeySet(engine, 16, 2)
+    k0, iv0 = oracle.gen_key(50, 16)
+    k1, iv1 = oracle.gen_key(51, 16)
+    ks.set(0, k0 + k1, iv0 + iv1)
+    h_in = torch.zeros(in_total + 16, dtype=torch.uint8).pin_memory()
+    h_aad = torch.zeros(aad_total + 16, dtype=torch.uint8).pin_memory()
+    h_out = torch.zeros(out_total + 16, dtype=torch.uint8).pin_memory()
+    hin, haad = h_in.numpy(), h_aad.numpy()
+    for r, rec in zip(recs_in, recs):
+        hin[rec["in_off"]: rec["in_off"] + len(r[4])] = np.frombuffer(r[4], np.uint8)
+        haad[rec["aad_off"]: rec["aad_off"] + 5] = np.frombuffer(r[3], np.uint8)
+    pipe = ptls_hip.Pipeline(engine, 256 << 10, transport=TRANSPORTS[transport])
+    pipe.seal(ks, recs, h_in, h_aad, h_out)
+    hout = h_out.numpy()
+    sealed = [hout[rec["out_off"]: rec["out_off"] + len(r[4]) + 16].tobytes() for r, rec in zip(recs_in, recs)]
+    bad = [i for i, (r, s_) in enumerate(zip(recs_in, sealed)) if s_ != oracle.seal(*r)]
+    assert not bad, f"{len(bad)} mismatches, first {bad[:8]}"
+    for s_, rec in zip(sealed, recs):
+        hin[rec["in_off"]: rec["in_off"] + len(s_)] = np.frombuffer(s_, np.uint8)
+    h_res = torch.zeros(n, dtype=torch.int64).pin_memory()
+    h_out.zero_()
+    pipe.open(ks, recs, h_in, h_aad, h_out, h_res)
+    assert [int(x) for x in h_res.numpy()] == lens
+    assert all(hout[rec["out_off"]: rec["out_off"] + len(r[4])].tobytes() == r[4] for r, rec in zip(recs_in, recs))
+    pipe.close()
+    ks.close()
