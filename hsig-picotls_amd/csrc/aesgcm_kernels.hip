@@ -255,7 +255,7 @@ __global__ void keysetup_kernel(KeySlot *slots, uint32_t *basis, const uint8_t *
 __global__ void __launch_bounds__(64) keysetup_wide_kernel(KeySlot *slots, uint32_t *basis, const uint8_t *keys,
                                                            const uint8_t *ivs, uint32_t first, int key_size, const uint32_t *t0)
 {
-    static_assert(LANE_POWS == 64 && NPOW == 7, "one lane power per lane; H^(j+1) from the squares H^(2^t), t < 7");
+    static_assert(LANE_POWS == 64 && NPOW >= 7, "one lane power per lane; H^(j+1) from the squares H^(2^t), t < 7");
     const uint32_t k = blockIdx.x;
     const int j = (int)threadIdx.x;
     KeySlot *slot = slots + first + k;
@@ -293,7 +293,7 @@ __global__ void __launch_bounds__(64) keysetup_wide_kernel(KeySlot *slots, uint3
     const int q1 = j + 1; /* 1 .. 64 */
     V4 acc = V4{0, 0, 0, 0};
     bool any = false;
-    for (int t = 0; t < NPOW; ++t) {
+    for (int t = 0; t < 7; ++t) {
         if ((q1 >> t) & 1) {
             acc = any ? gf_mul_valu(acc, pw[t]) : pw[t];
             any = true;

@@ -82,6 +82,9 @@ __host__ __device__ constexpr uint32_t lds_bytes(int log2g)
                            * 2 (with DYN_DEAL=0) = key switches after the first neither wait nor rebuild; 3 = the same with
                            * dynamic dealing running on across keys */
 #endif
+#ifndef SPLIT_TASKS
+#define SPLIT_TASKS 1 /* G >= 16: the planner may deal a key run's longest tasks as two part tasks (split records) */
+#endif
 #ifndef DEAL_MUTANT
 #define DEAL_MUTANT 0 /* TEST-ONLY broken builds (tools/build_mutants.sh, tests/test_gpu_dealing.py): 1 = the task a wave
                          drew past one chunk is dropped at the next chunk of the key run, 2 = cbase is not advanced */
@@ -961,6 +964,21 @@ __device__ __forceinline__ V4 put_byte(V4 v, int pos, uint32_t b)
     return V4{v.w0 | (w == 0 ? x : 0u), v.w1 | (w == 1 ? x : 0u), v.w2 | (w == 2 ? x : 0u), v.w3 | (w == 3 ? x : 0u)};
 }
 
+/* Diagnostic clock stamps (ptls_hip_batch_set_clock; nothing runs unless a buffer is given): thread 0 of a workgroup
+ * reads the shader-cycle counter and the constant 100 MHz counter at the start (slot 0) and the end (slot 1) of the
+ * workgroup's work into clk[4 * block + 2 * slot + {0, 1}].  The host takes delta(cycles) / delta(100 MHz ticks) as the
+ * clock the launch ran at (MI355X_MICROARCH.md, DVFS).  The values go only to that buffer; no output depends on them. */
+__device__ __forceinline__ void clock_stamp(uint64_t *__restrict__ clk, int slot)
+{
+    if (clk != nullptr && threadIdx.x == 0) {
+        const uint64_t t = __builtin_amdgcn_s_memtime();
+        const uint64_t r = __builtin_amdgcn_s_memrealtime();
+        __builtin_amdgcn_s_waitcnt(0xC07F); /* lgkmcnt(0): the counters are back before any LDS wait is counted */
+        clk[4 * blockIdx.x + 2 * slot] = t;
+        clk[4 * blockIdx.x + 2 * slot + 1] = r;
+    }
+}
+
 __device__ __forceinline__ int wave_max(int v)
 {
 #pragma unroll
@@ -1001,6 +1019,35 @@ __device__ __forceinline__ void bs8_ctr(const uint32_t *__restrict__ rk, const u
         ks[k] = V4{W[k][0], W[k][1], W[k][2], W[k][3]};
 }
 
+/* y * P for the G lanes of one record group, all holding y: `plane` = basis plane of P (plane[e] = P * x^e, GCM bit e =
+ * raw byte e / 8, bit 7 - e % 8); lane r XORs the vectors of bits [r 128 / G, (r + 1) 128 / G) of y (independent
+ * loads, one memory latency), an XOR butterfly over the group sums them: every lane of the group gets y * P */
+template <int G>
+__device__ __forceinline__ V4 mul_by_plane(V4 y, const uint4 *__restrict__ plane, int r)
+{
+    constexpr int BPL = 128 / G;
+    const uint32_t w[4] = {y.w0, y.w1, y.w2, y.w3};
+    uint4 v[BPL];
+#pragma unroll
+    for (int k = 0; k < BPL; ++k)
+        v[k] = plane[r * BPL + k];
+    V4 acc = V4{0, 0, 0, 0};
+#pragma unroll
+    for (int k = 0; k < BPL; ++k) {
+        const int e = r * BPL + k, byte = e >> 3;
+        const uint32_t m = 0u - ((w[byte >> 2] >> (8 * (byte & 3) + 7 - (e & 7))) & 1u);
+        acc = V4{acc.w0 ^ (m & v[k].x), acc.w1 ^ (m & v[k].y), acc.w2 ^ (m & v[k].z), acc.w3 ^ (m & v[k].w)};
+    }
+#pragma unroll
+    for (int o = G / 2; o > 0; o >>= 1) {
+        acc.w0 ^= __shfl_xor(acc.w0, o, 64);
+        acc.w1 ^= __shfl_xor(acc.w1, o, 64);
+        acc.w2 ^= __shfl_xor(acc.w2, o, 64);
+        acc.w3 ^= __shfl_xor(acc.w3, o, 64);
+    }
+    return acc;
+}
+
 /* ======================================================================================= *
  *  batch seal / open                                                                       *
  * ======================================================================================= */
@@ -1011,13 +1058,15 @@ struct Elem {
     int i, c, nbytes;
 };
 
-__device__ __forceinline__ Elem elem_of(int i, int N, int na, int nc, int L)
+/* element i of a record of N GHASH elements (na AAD blocks, nc data blocks, the length block), as seen by a task that
+ * handles the elements below `hi` (N, or the end of a split record's first part) */
+__device__ __forceinline__ Elem elem_of(int i, int N, int na, int nc, int L, int hi)
 {
     Elem e;
     e.i = i;
-    e.active = i < N;
-    e.is_aad = i < na;
-    e.is_c = !e.is_aad && i < na + nc;
+    e.active = i < hi;
+    e.is_aad = e.active && i < na;
+    e.is_c = e.active && !e.is_aad && i < na + nc;
     e.is_len = e.active && i == N - 1;
     e.c = i - na;
     e.nbytes = e.is_c ? min(16, L - 16 * e.c) : 0;
@@ -1057,14 +1106,18 @@ __global__ void __launch_bounds__(WGT)
                         const uint8_t *in, const uint8_t *__restrict__ aad, uint8_t *out, uint64_t *__restrict__ result,
                         const KeySlot *__restrict__ slots, const uint32_t *__restrict__ basis, const uint32_t *__restrict__ t0,
                         const ptls_hip_supp_t *__restrict__ supp, const KeySlot *__restrict__ hp_slots, uint32_t hp_nslots,
-                        uint8_t *mask)
+                        uint8_t *mask, uint64_t *__restrict__ clk)
 {
     constexpr int LOG2G = G == 1 ? 0 : G == 2 ? 1 : G == 4 ? 2 : G == 8 ? 3 : G == 16 ? 4 : 5;
     static_assert(G >= 1 && G <= 32 && (G & (G - 1)) == 0, "lanes per record: 1, 2, 4, 8, 16 or 32");
-    /* DYN_DEAL: the task counter sits after the tables */
+    /* DYN_DEAL: the task counter sits after the tables; SPLIT (G >= 16): then the split-record slots */
     constexpr bool DYN = DYN_DEAL != 0 && SPLIT_PROBE != 1; /* the counter is reset at key switches, which SPLIT_PROBE 1 skips */
-    static_assert(lds_bytes(LOG2G) + 16 <= 163840, "tables + task counter must fit the CU's 160 KiB");
-    __shared__ __attribute__((aligned(16))) uint8_t lds[lds_bytes(LOG2G) + (DYN ? 16 : 0)];
+    constexpr bool SPLIT = SPLIT_TASKS != 0 && G >= 16 && DYN && SPLIT_PROBE == 0 && HYBRID == 0 && KEYSWITCH_PROBE == 0;
+    constexpr uint32_t LDS_SPLIT = lds_bytes(LOG2G) + 16;                 /* partials: [slot][part] 16 B each */
+    constexpr uint32_t LDS_SPLIT_CTR = LDS_SPLIT + SPLIT_SLOTS * 32;      /* arrival counters: [slot] */
+    constexpr uint32_t LDS_TOTAL = SPLIT ? LDS_SPLIT_CTR + SPLIT_SLOTS * 4 : lds_bytes(LOG2G) + (DYN ? 16 : 0);
+    static_assert(LDS_TOTAL <= 163840, "tables + task counter + split slots must fit the CU's 160 KiB");
+    __shared__ __attribute__((aligned(16))) uint8_t lds[LDS_TOTAL];
     uint32_t *const task_ctr = reinterpret_cast<uint32_t *>(lds + lds_bytes(LOG2G));
     constexpr int R = 64 / G; /* records per wave task */
 
@@ -1075,11 +1128,12 @@ __global__ void __launch_bounds__(WGT)
     const int r = lane & (G - 1);
     const int grp = lane >> LOG2G;
 
+    clock_stamp(clk, 0);
     build_aes_tables<WGT>(lds, LDS_AES, t0);
     uint32_t cur_key = 0xffffffffu;
     /* DYN: g = the wave's next task in the workgroup's same-key run of chunks (drawn, not yet used);
-     * cbase = tasks of the run's chunks before the current one */
-    uint32_t g = 0, cbase = 0;
+     * cbase = tasks of the run's chunks before the current one; sbase = split tasks of those chunks (slot numbering) */
+    uint32_t g = 0, cbase = 0, sbase = 0;
     bool have_g = false;
 
     for (uint32_t ci = blockIdx.x; ci < nchunks; ci += gridDim.x) {
@@ -1094,9 +1148,13 @@ __global__ void __launch_bounds__(WGT)
                 build_ghash_tables(lds, basis + (size_t)ch.key * (BASIS_VECS * 4), LOG2G, !(VALU_TREE != 0 || G >= 32));
             if (DYN && threadIdx.x == 0)
                 *task_ctr = 0;
+            if (SPLIT)
+                for (int k = (int)threadIdx.x; k < SPLIT_SLOTS; k += WGT)
+                    reinterpret_cast<uint32_t *>(lds + LDS_SPLIT_CTR)[k] = 0;
             __syncthreads();
             cur_key = ch.key;
             cbase = 0;
+            sbase = 0;
             have_g = false; /* a task drawn past the old key's run belongs to no chunk */
         }
         if (DEAL_MUTANT == 1)
@@ -1104,7 +1162,9 @@ __global__ void __launch_bounds__(WGT)
 
         const KeySlot *__restrict__ slot = slots + ch.key;
         const uint32_t *__restrict__ rk = slot->rk;
-        const int ntasks = (int)((ch.count + R - 1) / R);
+        /* tasks of the chunk: its first nsplit (longest) tasks are dealt as two part tasks each, part A then part B */
+        const int nsplit = SPLIT ? (int)((ch.flags >> 8) & 0xffu) : 0;
+        const int ntasks = (int)((ch.count + R - 1) / R) + nsplit;
 
         /* DYN: a wave draws its next task when it finishes one, across the chunks of a same-key run, in order
          * (records sorted by decreasing length: longest first).  Waves on one SIMD do not progress equally
@@ -1131,7 +1191,11 @@ __global__ void __launch_bounds__(WGT)
                 if (t >= ntasks)
                     break;
             }
-            const uint32_t ridx = (uint32_t)t * R + grp;
+            /* part: -1 = the whole record, 0 / 1 = part A / B of a split record; tt = the task's record group */
+            const bool is_part = SPLIT && t < 2 * nsplit;
+            const int part = is_part ? (t & 1) : -1;
+            const int tt = is_part ? (t >> 1) : t - nsplit;
+            const uint32_t ridx = (uint32_t)tt * R + grp;
             const bool valid = ridx < ch.count;
             /* descriptors in chunk order: the record is one load away (its caller index only matters for
              * result[] and supp[] at the end) */
@@ -1143,7 +1207,10 @@ __global__ void __launch_bounds__(WGT)
             const int na = (A + 15) >> 4, nc = (L + 15) >> 4;
             const int N = valid ? na + nc + 1 : 0;
             const int i0 = (r + na) & (G - 1);
-            const int my_iters = i0 < N ? ((N - 1 - i0) >> LOG2G) + 1 : 0;
+            /* the elements [e_lo, e_hi) this task handles; the lane's are i0 + m G for m in [m_lo, m_hi) */
+            const int e_lo = is_part && part == 1 ? N - split_tail(N) : 0, e_hi = is_part && part == 0 ? N - split_tail(N) : N;
+            const int m_lo = e_lo > i0 ? ((e_lo - 1 - i0) >> LOG2G) + 1 : 0;
+            const int my_iters = e_hi > i0 ? ((e_hi - 1 - i0) >> LOG2G) + 1 : 0;
 
             /* seal of a TLS 1.3 record: the last plaintext byte is the content type, not input */
             const bool tflag = !OPEN && (rec.flags & 1u) != 0 && L > 0;
@@ -1169,7 +1236,7 @@ __global__ void __launch_bounds__(WGT)
                 int big = 0;
 #pragma unroll
                 for (int b = 0; b < 2; ++b) {
-                    e[b] = elem_of(i0 + (m + b) * G, N, na, nc, L);
+                    e[b] = elem_of(i0 + (m + b) * G, N, na, nc, L, e_hi);
                     in[b] = V4{0, 0, 0, 0};
                     if (e[b].is_c) {
                         const bool tb = tflag && e[b].c == nc - 1; /* the block holding the content-type byte */
@@ -1206,7 +1273,7 @@ __global__ void __launch_bounds__(WGT)
             };
 
             auto generic_iter_m = [&](int m) {
-                const Elem e0 = elem_of(i0 + m * G, N, na, nc, L);
+                const Elem e0 = elem_of(i0 + m * G, N, na, nc, L, e_hi);
                 V4 in0 = V4{0, 0, 0, 0};
                 if (e0.is_c) {
                     const bool tb = tflag && e0.c == nc - 1; /* the block holding the content-type byte */
@@ -1237,14 +1304,15 @@ __global__ void __launch_bounds__(WGT)
              * GHASH lookups of the previous iteration's ciphertext can all be in flight together. */
             constexpr int KP = PURE_BLOCKS;
             const int nf = (L - (tflag ? 1 : 0)) >> 4; /* full blocks that are all input bytes */
-            const int my_mlo = na > i0 ? (na - i0 + G - 1) >> LOG2G : 0;
+            /* the lane's AAD elements (m < my_mlo); a split record's part B has none (the planner splits past the AAD) */
+            const int my_mlo = is_part && part == 1 ? 0 : na > i0 ? (na - i0 + G - 1) >> LOG2G : 0;
             /* full blocks only, and (for the counter-mode shortcut) block counters c + 2 < 2^16 */
             const int lastc = min(nf, 65534) - 1; /* last data block index allowed in the pure stretch */
-            const int my_mhi = (valid && na + lastc - i0 >= 0) ? ((na + lastc - i0) >> LOG2G) + 1 : 0;
-            /* Each lane starts the stretch at its own first data element (after its AAD elements), so the
-             * lanes without AAD do not spend a generic step on data block 0; the stretch length is the
-             * shortest lane's. */
-            const int pm0 = my_mlo;
+            const int my_mhi = min((valid && na + lastc - i0 >= 0) ? ((na + lastc - i0) >> LOG2G) + 1 : 0, my_iters);
+            /* Each lane starts the stretch at its own first data element (after its AAD elements, or at its first
+             * element of a part B), so the lanes without AAD do not spend a generic step on data block 0; the stretch
+             * length is the shortest lane's. */
+            const int pm0 = max(my_mlo, m_lo);
             const int npure = -wave_max(-max(my_mhi - pm0, 0)) / KP;
             const int pm1 = pm0 + npure * KP; /* per lane: first element after the stretch */
 
@@ -1252,7 +1320,7 @@ __global__ void __launch_bounds__(WGT)
             const int naad = wave_max(my_mlo);
             for (int j = 0; j < naad; ++j) {
                 if (SPLIT_PROBE != 1 && j < my_mlo) {
-                    const Elem e = elem_of(i0 + j * G, N, na, nc, L);
+                    const Elem e = elem_of(i0 + j * G, N, na, nc, L, e_hi);
                     const V4 x = load_block<ALIGNED>(aad_p + 16 * e.i, min(16, A - 16 * e.i));
                     y = j == 0 ? x : gh_mul_main(lds, gl, y, x);
                 }
@@ -1378,7 +1446,7 @@ __global__ void __launch_bounds__(WGT)
              * nibble tables of H, H^2, H^4 in LDS; G = 32 (or VALU_TREE): one VALU multiply per lane by its own
              * power H^(q+1) (keysetup's list) and an XOR butterfly over the record's lanes */
             constexpr bool VCOMB = VALU_TREE != 0 || G >= 32;
-            const int q = (nc - r) & (G - 1);
+            const int q = (e_hi - 1 - na - r) & (G - 1); /* (nc - r) mod G for a whole record or a part B */
             V4 s; /* the record's GHASH (VCOMB: in every lane; tree: computed below in lane q == 0) */
             if constexpr (VCOMB) {
                 s = V4{0, 0, 0, 0};
@@ -1414,6 +1482,54 @@ __global__ void __launch_bounds__(WGT)
                         y = v4xor(y, w);
                 }
             }
+            if (is_part) {
+                /* a part of a split record: part A's partial times H^B (N - e_hi = B = 2^t: basis plane t, the record's
+                 * G lanes multiply 128 / G bits each, then XOR-reduce); part B's XOR E_K(J0).  Both go to the record's
+                 * slot; the part arriving second sums them into the tag. */
+                if constexpr (!VCOMB)
+                    s = gh_mul_nibble(lds, LDS_GTREE, y); /* * H (meaningful in the q == 0 lane) */
+                V4 sp = s;
+                if (part == 0) {
+                    if constexpr (!VCOMB) { /* the q == 0 lane's value to the record's G lanes */
+                        const int src = (lane & ~(G - 1)) | ((e_hi - 1 - na) & (G - 1));
+                        sp = V4{__shfl(s.w0, src, 64), __shfl(s.w1, src, 64), __shfl(s.w2, src, 64), __shfl(s.w3, src, 64)};
+                    }
+                    sp = mul_by_plane<G>(sp, reinterpret_cast<const uint4 *>(basis) + (size_t)ch.key * BASIS_VECS +
+                                                 split_plane(N) * 128, r);
+                } else {
+                    sp = v4xor(sp, ek0);
+                }
+                if (valid && q == 0) {
+                    const uint32_t sl = (sbase + (uint32_t)tt) * R + (uint32_t)grp;
+                    lds128_store(lds, LDS_SPLIT + sl * 32u + (uint32_t)part * 16u, sp);
+                    /* the other part's ciphertext (header protection samples it) and partial are visible once its
+                     * counter increment is: release / acquire around the LDS atomic */
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+                    const uint32_t arrived = __hip_atomic_fetch_add(reinterpret_cast<uint32_t *>(lds + LDS_SPLIT_CTR) + sl, 1u,
+                                                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    if (arrived == 1) {
+                        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                        const V4 tag = v4xor(sp, lds128(lds, LDS_SPLIT + sl * 32u + (uint32_t)(1 - part) * 16u));
+                        if (OPEN) {
+                            const V4 rt = load_full(in_p + L);
+                            const bool ok = rt.w0 == tag.w0 && rt.w1 == tag.w1 && rt.w2 == tag.w2 && rt.w3 == tag.w3;
+                            result[rec_i] = ok ? (uint64_t)L : ~(uint64_t)0;
+                        } else {
+                            store_full(out_p + L, tag);
+                            if (supp != nullptr) { /* header protection after the whole record, tag included */
+                                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+                                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                                const ptls_hip_supp_t sp2 = supp[rec_i];
+                                if ((sp2.flags & PTLS_HIP_SUPP_ENABLE) && sp2.hp_key < hp_nslots) {
+                                    const V4 sample = load_full(out + sp2.sample_off);
+                                    store_full(mask + sp2.mask_off, aes_encrypt<ROUNDS>(lds, lb_aes, hp_slots[sp2.hp_key].rk, sample));
+                                }
+                            }
+                        }
+                    }
+                }
+                continue;
+            }
             if (valid && q == 0) {
                 if constexpr (!VCOMB)
                     s = gh_mul_nibble(lds, LDS_GTREE, y); /* * H */
@@ -1445,6 +1561,11 @@ __global__ void __launch_bounds__(WGT)
         }
         if (DEAL_MUTANT != 2)
             cbase += (uint32_t)ntasks;
+        sbase += (uint32_t)nsplit;
+    }
+    if (clk != nullptr) { /* the workgroup's end: after its last wave */
+        __syncthreads();
+        clock_stamp(clk, 1);
     }
 }
 
@@ -1453,10 +1574,10 @@ static hipError_t launch_one(unsigned grid, hipStream_t s, const KernelArgs &a, 
 {
     if (aligned)
         hipLaunchKernelGGL((aesgcm_batch_kernel<G, R, O, true, W>), dim3(grid), dim3(W), 0, s, a.recs_ord, a.order, a.chunks,
-                           a.nchunks, a.in, a.aad, a.out, a.result, a.slots, a.basis, a.t0, a.supp, a.hp_slots, a.hp_nslots, a.mask);
+                           a.nchunks, a.in, a.aad, a.out, a.result, a.slots, a.basis, a.t0, a.supp, a.hp_slots, a.hp_nslots, a.mask, a.clk);
     else
         hipLaunchKernelGGL((aesgcm_batch_kernel<G, R, O, false, W>), dim3(grid), dim3(W), 0, s, a.recs_ord, a.order, a.chunks,
-                           a.nchunks, a.in, a.aad, a.out, a.result, a.slots, a.basis, a.t0, a.supp, a.hp_slots, a.hp_nslots, a.mask);
+                           a.nchunks, a.in, a.aad, a.out, a.result, a.slots, a.basis, a.t0, a.supp, a.hp_slots, a.hp_nslots, a.mask, a.clk);
     return hipGetLastError();
 }
 

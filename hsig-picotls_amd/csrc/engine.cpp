@@ -22,6 +22,7 @@
 #include <chrono>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "internal.h"
@@ -128,6 +129,9 @@ struct st_ptls_hip_batch_t {
     bool forced;
     uint32_t max_key; /* largest key slot any record names (checked against the keyset at seal/open) */
     unsigned max_wg;  /* 0, or a cap on the workgroups of a launch (planning then sizes chunks for that many) */
+    uint32_t nsplit;  /* wave tasks the plan deals as two part tasks (split records) */
+    uint64_t *d_clk;  /* diagnostic clock stamps of the next launches (ptls_hip_batch_set_clock), or nullptr */
+    size_t clk_bytes;
 };
 
 /* CUs a batch is planned and launched for: the device's, or fewer when the batch caps its grid */
@@ -169,6 +173,8 @@ extern "C" int ptls_hip_is_supported(void)
     return 0;
 }
 
+static int engine_self_check(ptls_hip_engine_t *e);
+
 extern "C" ptls_hip_engine_t *ptls_hip_engine_new(int device)
 {
     int ndev = 0;
@@ -198,6 +204,12 @@ extern "C" ptls_hip_engine_t *ptls_hip_engine_new(int device)
     if (hipMalloc(&e->d_t0, sizeof(t0)) != hipSuccess || hipMemcpy(e->d_t0, t0, sizeof(t0), hipMemcpyHostToDevice) != hipSuccess) {
         fail(PTLS_HIP_ENOMEM, "cannot allocate the AES table on device %d", device);
         delete e;
+        return nullptr;
+    }
+    if (engine_self_check(e) != 0) {
+        const std::string why = g_err;
+        ptls_hip_engine_free(e);
+        fail(PTLS_HIP_ENODEV, "device %d: engine self-check failed: %s", device, why.c_str());
         return nullptr;
     }
     return e;
@@ -449,6 +461,68 @@ static int plan_wg(const std::vector<Chunk> &ch, int lanes)
     return WG_ALT;
 }
 
+/* Split tasks (batch_kernel.h, G >= 16).  A workgroup works through one key run at a time; with few wave tasks per run
+ * (configs[3]: 64 records per key = 16 tasks of 4 records at 16 lanes for 12 waves) the run's longest task takes
+ * ~1.5x a wave's share and the other waves idle at the key switch (a 7 % bound).  The planner deals a
+ * run's longest tasks as two part tasks each (GHASH elements [0, N - B) and [N - B, N) of the task's records, combined
+ * through LDS by the part that finishes last) while a task's cost (its first record's GHASH elements: records are
+ * sorted longest first) exceeds `pct` % of the run's share per wave.  PTLS_HIP_SPLIT_PCT (environment) overrides the
+ * measured default; 0 switches splitting off. */
+static int split_pct(void)
+{
+    static const int pct = [] {
+        const char *e = getenv("PTLS_HIP_SPLIT_PCT");
+        return e != nullptr ? atoi(e) : 75;
+    }();
+    return pct;
+}
+
+static void plan_splits(const ptls_hip_record_t *recs, const std::vector<uint32_t> &order, std::vector<Chunk> &ch, int lanes)
+{
+    const int pct = split_pct();
+    if (pct <= 0)
+        return;
+    const uint32_t R = 64u / (uint32_t)lanes;
+    const int nwaves = WG_ALT / 64;
+    auto elems = [&](uint32_t pos) {
+        const ptls_hip_record_t &r = recs[order[pos]];
+        return (int)((r.aad_len + 15) / 16 + (r.len + 15) / 16 + 1);
+    };
+    for (size_t a = 0; a < ch.size();) {
+        size_t b = a + 1;
+        while (b < ch.size() && ch[b].key == ch[a].key)
+            ++b;
+        /* key run = chunks [a, b): task costs and the share per wave */
+        double total = 0;
+        size_t tasks = 0;
+        for (size_t c = a; c < b; ++c)
+            for (uint32_t t = 0; t * R < ch[c].count; ++t, ++tasks)
+                total += elems(ch[c].first + t * R);
+        if (tasks < (size_t)(4 * nwaves)) { /* many tasks per wave balance by themselves */
+            const double limit = total / nwaves * pct / 100.0;
+            uint32_t slots = 0;
+            for (size_t c = a; c < b; ++c) {
+                uint32_t ns = 0;
+                for (uint32_t t = 0; (t + 1) * R <= ch[c].count && ns < 255; ++t) {
+                    const uint32_t p0 = ch[c].first + t * R;
+                    bool ok = elems(p0) > limit && slots + R <= (uint32_t)SPLIT_SLOTS;
+                    for (uint32_t k = 0; ok && k < R; ++k) {
+                        const ptls_hip_record_t &r = recs[order[p0 + k]];
+                        const int n = elems(p0 + k), na = (int)((r.aad_len + 15) / 16);
+                        ok = n >= SPLIT_MIN_N && n <= SPLIT_MAX_N && n - split_tail(n) > na;
+                    }
+                    if (!ok)
+                        break;
+                    ++ns;
+                    slots += R;
+                }
+                ch[c].flags = (ch[c].flags & ~0xff00u) | (ns << 8);
+            }
+        }
+        a = b;
+    }
+}
+
 /* chunk = run of records with one key slot, sized to keep all waves of a workgroup busy for a few tasks
  * (at most 32 wave tasks), but small enough that a batch of fewer tasks still spreads over every CU (the
  * grid is one workgroup per chunk up to the CU count).  Inside a chunk the records are ordered by
@@ -520,6 +594,8 @@ static void build_chunks(const ptls_hip_record_t *recs, size_t n, int lanes, uns
         all_aligned = all_aligned && (c.flags & 1u);
         ch.push_back(c);
     }
+    if (lanes >= 16)
+        plan_splits(recs, order, ch, lanes);
 }
 
 static int plan_chunks(ptls_hip_batch_t *b)
@@ -538,6 +614,9 @@ static int plan_chunks(ptls_hip_batch_t *b)
     b->d_order = nullptr;
     b->d_recs_ord = nullptr;
     b->nchunks = (uint32_t)ch.size();
+    b->nsplit = 0;
+    for (const Chunk &c : ch)
+        b->nsplit += (c.flags >> 8) & 0xffu;
     if (ch.empty())
         return 0;
     HIP_TRY(hipMalloc(&b->d_chunks, ch.size() * sizeof(Chunk)), PTLS_HIP_ENOMEM);
@@ -642,6 +721,27 @@ extern "C" int ptls_hip_batch_set_max_workgroups(ptls_hip_batch_t *b, int n)
     return plan_chunks(b);
 }
 
+extern "C" int ptls_hip_batch_grid(ptls_hip_batch_t *b)
+{
+    if (b == nullptr)
+        return fail(PTLS_HIP_EINVAL, "batch_grid: null batch");
+    return (int)plan_grid(b->n, b->nchunks, b->lanes, batch_cus(b));
+}
+
+extern "C" int ptls_hip_batch_split_tasks(ptls_hip_batch_t *b)
+{
+    return b != nullptr ? (int)b->nsplit : fail(PTLS_HIP_EINVAL, "batch_split_tasks: null batch");
+}
+
+extern "C" int ptls_hip_batch_set_clock(ptls_hip_batch_t *b, void *d_buf, size_t nbytes)
+{
+    if (b == nullptr || (d_buf != nullptr && nbytes < (size_t)ptls_hip_batch_grid(b) * 32))
+        return fail(PTLS_HIP_EINVAL, "batch_set_clock: the buffer needs 32 bytes per workgroup of the launch");
+    b->d_clk = static_cast<uint64_t *>(d_buf);
+    b->clk_bytes = d_buf != nullptr ? nbytes : 0;
+    return 0;
+}
+
 static int run_batch(ptls_hip_batch_t *b, ptls_hip_keyset_t *ks, const void *in, const void *aad, void *out, uint64_t *result,
                      void *stream, bool open, ptls_hip_keyset_t *hp_ks = nullptr, const ptls_hip_supp_t *supp = nullptr,
                      void *mask = nullptr)
@@ -679,6 +779,9 @@ static int run_batch(ptls_hip_batch_t *b, ptls_hip_keyset_t *ks, const void *in,
                                 reinterpret_cast<uintptr_t>(out)) & 15) == 0;
     const bool aligned = base_aligned && b->all_aligned;
     const unsigned grid = plan_grid(b->n, b->nchunks, b->lanes, batch_cus(b));
+    if (b->d_clk != nullptr && b->clk_bytes < (size_t)grid * 32)
+        return fail(PTLS_HIP_EINVAL, "seal/open: the clock-stamp buffer is smaller than 32 bytes x %u workgroups", grid);
+    a.clk = b->d_clk;
     const int rounds = ks->key_size == 16 ? 10 : 14;
     int e = launch_batch(b->lanes, rounds, open, b->wg, grid, stream, a, aligned);
     if (e != 0)
@@ -849,6 +952,69 @@ extern "C" int ptls_hip_fill_records(ptls_hip_batch_t *b, void *buf, uint64_t se
     return 0;
 }
 
+/* The reference's gcm_basic #2 (t/fusion.c:251-273: key 00 11 .. ff, iv 20 .. 31, AAD 0 .. 19, the 85 bytes of
+ * "hello world\n" x 7 + NUL, seq 0) sealed through the wave-per-record kernel, the batch kernel's table tree (8 lanes
+ * per record) and its VALU combination (32 lanes), and opened back, whenever an engine starts: a library that computes
+ * anything else (a probe build, a broken device) fails ptls_hip_engine_new instead of serving records. */
+static int engine_self_check(ptls_hip_engine_t *e)
+{
+    static const uint8_t key[16] = {0x00, 0x11, 0x22, 0x33, 0x44, 0x55, 0x66, 0x77, 0x88, 0x99, 0xaa, 0xbb, 0xcc, 0xdd, 0xee, 0xff};
+    static const uint8_t expected[101] = {
+        0xd3, 0xa8, 0x1d, 0x96, 0x4c, 0x9b, 0x02, 0xd7, 0x9a, 0xb0, 0x41, 0x07, 0x4c, 0x8c, 0xe2, 0xe0, 0x2e,
+        0x83, 0x54, 0x52, 0x45, 0xcb, 0xd4, 0x68, 0xc8, 0x43, 0x45, 0xca, 0x91, 0xfb, 0xa3, 0x7a, 0x67, 0xed,
+        0xe8, 0xd7, 0x5e, 0xe2, 0x33, 0xd1, 0x3e, 0xbf, 0x50, 0xc2, 0x4b, 0x86, 0x83, 0x55, 0x11, 0xbb, 0x17,
+        0x4f, 0xf5, 0x78, 0xb8, 0x65, 0xeb, 0x9a, 0x2b, 0x8f, 0x77, 0x08, 0xa9, 0x60, 0x17, 0x73, 0xc5, 0x07,
+        0xf3, 0x04, 0xc9, 0x3f, 0x67, 0x4d, 0x12, 0xa1, 0x02, 0x93, 0xc2, 0x3c, 0xd3, 0xf8, 0x59, 0x33, 0xd5,
+        0x01, 0xc3, 0xbb, 0xaa, 0xe6, 0x3f, 0xbb, 0x23, 0x66, 0x94, 0x26, 0x28, 0x43, 0xa5, 0xfd, 0x2f};
+    uint8_t iv[12], aad[20], pt[85], buf[512];
+    for (int i = 0; i < 12; ++i)
+        iv[i] = (uint8_t)(20 + i);
+    for (int i = 0; i < 20; ++i)
+        aad[i] = (uint8_t)i;
+    for (int i = 0; i < 84; ++i)
+        pt[i] = (uint8_t)"hello world\n"[i % 12];
+    pt[84] = 0;
+    /* device buffer: plaintext @0, AAD @128, sealed @256 (101 B), opened @384 (85 B), result @480 */
+    ptls_hip_keyset_t *ks = ptls_hip_keyset_new(e, 16, 1);
+    uint8_t *d = nullptr;
+    int rc = ks == nullptr ? -1 : 0;
+    if (rc == 0 && ptls_hip_keyset_set(ks, 0, 1, key, iv, nullptr) != 0)
+        rc = -1;
+    if (rc == 0 && hipMalloc(&d, sizeof(buf)) != hipSuccess)
+        rc = fail(PTLS_HIP_ENOMEM, "self-check: no device memory");
+    if (rc == 0) {
+        std::memset(buf, 0, sizeof(buf));
+        std::memcpy(buf, pt, sizeof(pt));
+        std::memcpy(buf + 128, aad, sizeof(aad));
+        if (hipMemcpy(d, buf, sizeof(buf), hipMemcpyHostToDevice) != hipSuccess)
+            rc = fail(PTLS_HIP_ENODEV, "self-check: upload failed");
+    }
+    static const int lanes[] = {SPARSE_LANES, 8, 32};
+    for (int li = 0; rc == 0 && li < 3; ++li) {
+        const ptls_hip_record_t seal{0, 256, 128, 0, 85, 20, 0, 0}, open{256, 384, 128, 0, 85, 20, 0, 0};
+        ptls_hip_batch_t *bs = ptls_hip_batch_new(e, &seal, 1, nullptr), *bo = ptls_hip_batch_new(e, &open, 1, nullptr);
+        if (bs == nullptr || bo == nullptr || ptls_hip_batch_set_lanes(bs, lanes[li]) != 0 || ptls_hip_batch_set_lanes(bo, lanes[li]) != 0 ||
+            hipMemset(d + 256, 0, 256) != hipSuccess || ptls_hip_aesgcm_seal_batch(bs, ks, d, d, d, nullptr) != 0 ||
+            ptls_hip_aesgcm_open_batch(bo, ks, d, d, d, reinterpret_cast<uint64_t *>(d + 480), nullptr) != 0 ||
+            hipMemcpy(buf, d, sizeof(buf), hipMemcpyDeviceToHost) != hipSuccess) {
+            rc = fail(PTLS_HIP_ENODEV, "self-check: launch failed (%s)", g_err.c_str());
+        } else {
+            uint64_t res = 0;
+            std::memcpy(&res, buf + 480, 8);
+            if (std::memcmp(buf + 256, expected, sizeof(expected)) != 0 || res != 85 || std::memcmp(buf + 384, pt, sizeof(pt)) != 0)
+                rc = fail(PTLS_HIP_ENODEV, "gcm_basic (t/fusion.c:251-273) sealed or opened wrong at %d lanes per record", lanes[li]);
+        }
+        ptls_hip_batch_free(bs);
+        ptls_hip_batch_free(bo);
+    }
+    if (d != nullptr) {
+        (void)hipMemset(d, 0, sizeof(buf));
+        (void)hipFree(d);
+    }
+    ptls_hip_keyset_free(ks);
+    return rc;
+}
+
 /* ---------------------------------------------------------------------------------------------- */
 /* host-resident pipeline: pinned H2D -> kernel -> D2H, overlapped over NSLOT streams                */
 /* ---------------------------------------------------------------------------------------------- */
@@ -999,6 +1165,33 @@ static void *mapped_ptr(const void *h)
     return d;
 }
 
+/* the device address of h when pinned or registered host memory covers ALL of [h, h + need) with one mapping, else
+ * nullptr: a buffer registered only in part must not be handed to the kernels (they would touch unmapped host pages
+ * over PCIe; the copy transport reads any host memory).  The mapping's range comes from the pointer attributes; the
+ * last byte must also map, contiguously with the first. */
+static void *mapped_span(const void *h, uint64_t need)
+{
+    void *d = mapped_ptr(h);
+    if (d == nullptr || need <= 1)
+        return d;
+    const uintptr_t hp = reinterpret_cast<uintptr_t>(h), dp = reinterpret_cast<uintptr_t>(d);
+    uintptr_t start = 0;
+    size_t size = 0;
+    if (hipPointerGetAttribute(&start, HIP_POINTER_ATTRIBUTE_RANGE_START_ADDR, reinterpret_cast<hipDeviceptr_t>(d)) == hipSuccess &&
+        hipPointerGetAttribute(&size, HIP_POINTER_ATTRIBUTE_RANGE_SIZE, reinterpret_cast<hipDeviceptr_t>(d)) == hipSuccess &&
+        size != 0) {
+        const bool in_range = (start <= dp && dp + need <= start + size) || (start <= hp && hp + need <= start + size);
+        if (!in_range)
+            return nullptr;
+    } else {
+        (void)hipGetLastError();
+    }
+    void *d_last = mapped_ptr(static_cast<const uint8_t *>(h) + (need - 1));
+    if (d_last == nullptr || reinterpret_cast<uintptr_t>(d_last) != dp + (need - 1))
+        return nullptr;
+    return d;
+}
+
 /* lanes per record when the kernel reads and writes host memory: the launch is PCIe-bound, not LDS-bound, and wider
  * lane groups turn each load / store instruction into longer contiguous runs per record, i.e. fewer, larger PCIe
  * requests.  Measured (tools/hostmem_probe.py, seal+open GiB/s at 4 / 8 / 16 / 32 lanes): 1350-B records 31.7 /
@@ -1133,6 +1326,21 @@ static int pipeline_run_mapped(ptls_hip_pipeline_t *p, ptls_hip_keyset_t *ks, co
     return 0;
 }
 
+static int pipeline_run_copy(ptls_hip_pipeline_t *p, ptls_hip_keyset_t *ks, const ptls_hip_record_t *recs, size_t n,
+                             const void *h_in, const void *h_aad, void *h_out, uint64_t *h_result, PipeMode mode,
+                             ptls_hip_keyset_t *hp_ks, const ptls_hip_supp_t *supp, void *h_mask);
+
+/* wait for every slice still in flight and free the slots: also on an error path, because an earlier slice's kernel
+ * or copy may still read or write the caller's host buffers, which the caller may release once the call returned */
+static void drain_slots(ptls_hip_pipeline_t *p)
+{
+    for (auto &s : p->slot) {
+        if (s.busy)
+            (void)hipStreamSynchronize(s.stream);
+        s.busy = false;
+    }
+}
+
 static int pipeline_run(ptls_hip_pipeline_t *p, ptls_hip_keyset_t *ks, const ptls_hip_record_t *recs, size_t n, const void *h_in,
                         const void *h_aad, void *h_out, uint64_t *h_result, PipeMode mode, ptls_hip_keyset_t *hp_ks = nullptr,
                         const ptls_hip_supp_t *supp = nullptr, void *h_mask = nullptr)
@@ -1141,7 +1349,6 @@ static int pipeline_run(ptls_hip_pipeline_t *p, ptls_hip_keyset_t *ks, const ptl
                             hp_ks->key_size != ks->key_size || h_mask == nullptr))
         return fail(PTLS_HIP_EINVAL, "pipeline_seal_supp: the header-protection keyset must be on the same engine with the "
                                      "AEAD's key size, and h_mask must be given");
-    uint8_t *hmask = static_cast<uint8_t *>(h_mask);
     const bool open = mode == PIPE_OPEN || mode == PIPE_TLS13_OPEN;
     const bool aad_in_out = mode == PIPE_TLS13_SEAL, aad_in_in = mode == PIPE_TLS13_OPEN;
     if (p == nullptr || ks == nullptr || ks->eng != p->eng || (n != 0 && (recs == nullptr || h_in == nullptr || h_out == nullptr)) ||
@@ -1152,17 +1359,49 @@ static int pipeline_run(ptls_hip_pipeline_t *p, ptls_hip_keyset_t *ks, const ptl
             return fail(PTLS_HIP_EINVAL, "pipeline: record %zu names key slot %u, the keyset has %zu", i, recs[i].key, ks->nslots);
     DeviceGuard g(p->eng->device);
     if (p->transport != PTLS_HIP_TRANSPORT_COPY && n != 0) {
-        const uint8_t *d_in = static_cast<const uint8_t *>(mapped_ptr(h_in));
-        uint8_t *d_out = static_cast<uint8_t *>(mapped_ptr(h_out));
-        const uint8_t *d_aad = static_cast<const uint8_t *>(mapped_ptr(h_aad));
-        uint8_t *d_mask = static_cast<uint8_t *>(mapped_ptr(h_mask));
-        uint64_t *d_res = open ? static_cast<uint64_t *>(mapped_ptr(h_result)) : nullptr;
+        /* the bytes the kernels would touch in each buffer: [base, base + need) */
+        uint64_t need_in = 0, need_out = 0, need_aad = 0, need_mask = 0;
+        for (size_t i = 0; i < n; ++i) {
+            const ptls_hip_record_t &r = recs[i];
+            need_in = std::max<uint64_t>(need_in, r.in_off + r.len + (open ? 16 : 0));
+            need_out = std::max<uint64_t>(need_out, r.out_off + r.len + (open ? 0 : 16));
+            if (r.aad_len != 0) {
+                uint64_t &na = aad_in_out ? need_out : aad_in_in ? need_in : need_aad;
+                na = std::max<uint64_t>(na, r.aad_off + r.aad_len);
+            }
+            if (supp != nullptr && (supp[i].flags & PTLS_HIP_SUPP_ENABLE))
+                need_mask = std::max<uint64_t>(need_mask, supp[i].mask_off + 16);
+        }
+        const uint8_t *d_in = static_cast<const uint8_t *>(mapped_span(h_in, need_in));
+        uint8_t *d_out = static_cast<uint8_t *>(mapped_span(h_out, need_out));
+        const uint8_t *d_aad = static_cast<const uint8_t *>(mapped_span(h_aad, need_aad));
+        uint8_t *d_mask = static_cast<uint8_t *>(mapped_span(h_mask, need_mask));
+        uint64_t *d_res = open ? static_cast<uint64_t *>(mapped_span(h_result, (uint64_t)n * 8)) : nullptr;
         const bool ok = d_in != nullptr && d_out != nullptr && (h_aad == nullptr || d_aad != nullptr) && (h_mask == nullptr || d_mask != nullptr);
-        if (ok)
-            return pipeline_run_mapped(p, ks, recs, n, d_in, d_aad, d_out, h_result, d_res, mode, hp_ks, supp, d_mask);
+        if (ok) {
+            const int rc = pipeline_run_mapped(p, ks, recs, n, d_in, d_aad, d_out, h_result, d_res, mode, hp_ks, supp, d_mask);
+            if (rc != 0)
+                drain_slots(p);
+            return rc;
+        }
         if (p->transport == PTLS_HIP_TRANSPORT_MAPPED)
-            return fail(PTLS_HIP_EINVAL, "pipeline: transport MAPPED needs pinned or registered host buffers (in, out, aad, mask)");
+            return fail(PTLS_HIP_EINVAL, "pipeline: transport MAPPED needs host buffers (in, out, aad, mask) pinned or registered "
+                                         "over every byte the records touch");
     }
+    const int rc = pipeline_run_copy(p, ks, recs, n, h_in, h_aad, h_out, h_result, mode, hp_ks, supp, h_mask);
+    if (rc != 0)
+        drain_slots(p);
+    return rc;
+}
+
+/* PTLS_HIP_TRANSPORT_COPY: slices staged through the slots' device buffers by the copy engines */
+static int pipeline_run_copy(ptls_hip_pipeline_t *p, ptls_hip_keyset_t *ks, const ptls_hip_record_t *recs, size_t n,
+                             const void *h_in, const void *h_aad, void *h_out, uint64_t *h_result, PipeMode mode,
+                             ptls_hip_keyset_t *hp_ks, const ptls_hip_supp_t *supp, void *h_mask)
+{
+    uint8_t *hmask = static_cast<uint8_t *>(h_mask);
+    const bool open = mode == PIPE_OPEN || mode == PIPE_TLS13_OPEN;
+    const bool aad_in_out = mode == PIPE_TLS13_SEAL, aad_in_in = mode == PIPE_TLS13_OPEN;
     p->last_transport = PTLS_HIP_TRANSPORT_COPY;
     const int rounds = ks->key_size == 16 ? 10 : 14;
     const size_t tag_in = open ? 16 : 0, tag_out = open ? 0 : 16;
@@ -1357,6 +1596,167 @@ extern "C" int ptls_hip_pipeline_open(ptls_hip_pipeline_t *p, ptls_hip_keyset_t 
 }
 
 /* ---------------------------------------------------------------------------------------------- */
+/* one batch over several devices                                                 */
+/* ---------------------------------------------------------------------------------------------- */
+
+extern "C" int ptls_hip_partition_bytes(const ptls_hip_record_t *recs, size_t n, size_t parts, size_t *bounds)
+{
+    if ((recs == nullptr && n != 0) || parts == 0 || bounds == nullptr)
+        return fail(PTLS_HIP_EINVAL, "partition_bytes: bad arguments");
+    uint64_t total = 0;
+    for (size_t i = 0; i < n; ++i)
+        total += recs[i].len;
+    /* range r ends right after the first record whose prefix sum reaches ceil(total * (r + 1) / parts) (bench.py
+     * partition_bytes is the same rule) */
+    bounds[0] = 0;
+    size_t i = 0;
+    uint64_t csum = 0;
+    for (size_t r = 1; r < parts; ++r) {
+        const unsigned __int128 t = ((unsigned __int128)total * r + parts - 1) / parts;
+        const uint64_t target = (uint64_t)t;
+        if (total == 0) {
+            bounds[r] = 0;
+            continue;
+        }
+        while (i < n && csum < target)
+            csum += recs[i++].len;
+        bounds[r] = std::max(bounds[r - 1], i);
+    }
+    bounds[parts] = n;
+    return 0;
+}
+
+struct st_ptls_hip_node_t {
+    std::vector<ptls_hip_engine_t *> eng;
+    std::vector<ptls_hip_keyset_t *> ks;
+    std::vector<ptls_hip_pipeline_t *> pipe;
+    std::vector<double> seconds; /* per device, last call */
+    std::vector<size_t> bounds;  /* record ranges of the last call */
+};
+
+extern "C" void ptls_hip_node_free(ptls_hip_node_t *node)
+{
+    if (node == nullptr)
+        return;
+    for (auto *p : node->pipe)
+        ptls_hip_pipeline_free(p);
+    for (auto *k : node->ks)
+        ptls_hip_keyset_free(k);
+    for (auto *e : node->eng)
+        ptls_hip_engine_free(e);
+    delete node;
+}
+
+extern "C" ptls_hip_node_t *ptls_hip_node_new(const int *devices, size_t ndev, size_t key_size, size_t nslots, size_t slice_bytes)
+{
+    if (devices == nullptr || ndev == 0 || ndev > 64) {
+        fail(PTLS_HIP_EINVAL, "node_new: 1 to 64 devices");
+        return nullptr;
+    }
+    auto *node = new st_ptls_hip_node_t();
+    for (size_t d = 0; d < ndev; ++d) {
+        ptls_hip_engine_t *e = ptls_hip_engine_new(devices[d]);
+        node->eng.push_back(e);
+        ptls_hip_keyset_t *k = e != nullptr ? ptls_hip_keyset_new(e, key_size, nslots) : nullptr;
+        node->ks.push_back(k);
+        ptls_hip_pipeline_t *p = k != nullptr ? ptls_hip_pipeline_new(e, slice_bytes) : nullptr;
+        node->pipe.push_back(p);
+        if (p == nullptr) {
+            const std::string why = g_err;
+            ptls_hip_node_free(node);
+            fail(PTLS_HIP_ENODEV, "node_new: device %d: %s", devices[d], why.c_str());
+            return nullptr;
+        }
+    }
+    node->seconds.assign(ndev, 0.0);
+    node->bounds.assign(ndev + 1, 0);
+    return node;
+}
+
+extern "C" size_t ptls_hip_node_size(ptls_hip_node_t *node)
+{
+    return node != nullptr ? node->eng.size() : 0;
+}
+
+extern "C" int ptls_hip_node_keyset_set(ptls_hip_node_t *node, size_t first, size_t count, const void *keys, const void *ivs)
+{
+    if (node == nullptr)
+        return fail(PTLS_HIP_EINVAL, "node_keyset_set: null node");
+    for (auto *k : node->ks) /* replicated: every device holds every connection's key slot */
+        if (int rc = ptls_hip_keyset_set(k, first, count, keys, ivs, nullptr))
+            return rc;
+    return 0;
+}
+
+extern "C" int ptls_hip_node_set_transport(ptls_hip_node_t *node, int transport)
+{
+    if (node == nullptr)
+        return fail(PTLS_HIP_EINVAL, "node_set_transport: null node");
+    for (auto *p : node->pipe)
+        if (int rc = ptls_hip_pipeline_set_transport(p, transport))
+            return rc;
+    return 0;
+}
+
+/* the records split in contiguous ranges of about equal payload bytes, one host thread per device driving its own
+ * pipeline over its range (the host buffers are shared: offsets stay relative to them), no data crossing devices */
+static int node_run(ptls_hip_node_t *node, const ptls_hip_record_t *recs, size_t n, const void *h_in, const void *h_aad,
+                    void *h_out, uint64_t *h_result, bool open)
+{
+    if (node == nullptr || (n != 0 && (recs == nullptr || h_in == nullptr || h_out == nullptr)) || (open && h_result == nullptr))
+        return fail(PTLS_HIP_EINVAL, "node seal/open: bad arguments");
+    const size_t nd = node->eng.size();
+    if (int rc = ptls_hip_partition_bytes(recs, n, nd, node->bounds.data()))
+        return rc;
+    std::vector<int> rcs(nd, 0);
+    std::vector<std::string> errs(nd);
+    std::vector<std::thread> th;
+    for (size_t d = 0; d < nd; ++d) {
+        th.emplace_back([&, d]() {
+            const size_t lo = node->bounds[d], hi = node->bounds[d + 1];
+            const auto t0 = std::chrono::steady_clock::now();
+            int rc = 0;
+            if (hi > lo)
+                rc = open ? ptls_hip_pipeline_open(node->pipe[d], node->ks[d], recs + lo, hi - lo, h_in, h_aad, h_out, h_result + lo)
+                          : ptls_hip_pipeline_seal(node->pipe[d], node->ks[d], recs + lo, hi - lo, h_in, h_aad, h_out);
+            node->seconds[d] = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+            rcs[d] = rc;
+            if (rc != 0)
+                errs[d] = g_err; /* thread_local: carried back to the caller's thread */
+        });
+    }
+    for (auto &t : th)
+        t.join();
+    for (size_t d = 0; d < nd; ++d)
+        if (rcs[d] != 0)
+            return fail(rcs[d], "node: device %d: %s", node->eng[d]->device, errs[d].c_str());
+    return 0;
+}
+
+extern "C" int ptls_hip_node_seal(ptls_hip_node_t *node, const ptls_hip_record_t *recs, size_t n, const void *h_in, const void *h_aad,
+                                  void *h_out)
+{
+    return node_run(node, recs, n, h_in, h_aad, h_out, nullptr, false);
+}
+
+extern "C" int ptls_hip_node_open(ptls_hip_node_t *node, const ptls_hip_record_t *recs, size_t n, const void *h_in, const void *h_aad,
+                                  void *h_out, uint64_t *h_result)
+{
+    return node_run(node, recs, n, h_in, h_aad, h_out, h_result, true);
+}
+
+extern "C" int ptls_hip_node_last_split(ptls_hip_node_t *node, double *seconds, size_t *bounds)
+{
+    if (node == nullptr)
+        return fail(PTLS_HIP_EINVAL, "node_last_split: null node");
+    if (seconds != nullptr)
+        std::copy(node->seconds.begin(), node->seconds.end(), seconds);
+    if (bounds != nullptr)
+        std::copy(node->bounds.begin(), node->bounds.end(), bounds);
+    return 0;
+}
+
+/* ---------------------------------------------------------------------------------------------- */
 /* picotls plugin: ptls_hip_aes128gcm / ptls_hip_aes256gcm                                         */
 /* ---------------------------------------------------------------------------------------------- */
 
@@ -1433,7 +1833,11 @@ static void plugin_wait(hipStream_t stream, const uint8_t *word_p, uint32_t seq)
     for (uint32_t spin = 1;; ++spin) {
         if (__atomic_load_n(word, __ATOMIC_ACQUIRE) == seq)
             return;
+#if defined(__x86_64__) || defined(__i386__)
         __builtin_ia32_pause();
+#else
+        std::this_thread::yield();
+#endif
         if ((spin & 4095) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(2))
             break;
     }
@@ -1529,7 +1933,7 @@ static hip_ctr_state *ecb_state_new(const void *key, size_t key_size)
     }
     st->ks = ptls_hip_keyset_new(eng, key_size, 1);
     void *d_stage = nullptr;
-    const bool ok = st->ks != nullptr && hipHostMalloc(&st->h_stage, 128, hipHostMallocDefault) == hipSuccess &&
+    const bool ok = st->ks != nullptr && hipHostMalloc(&st->h_stage, 128, hipHostMallocCoherent) == hipSuccess &&
                     hipHostGetDevicePointer(&d_stage, st->h_stage, 0) == hipSuccess &&
                     ptls_hip_keyset_set(st->ks, 0, 1, key, nullptr, st->stream) == 0;
     st->d_stage = static_cast<uint8_t *>(d_stage);
@@ -1658,7 +2062,9 @@ static void state_reserve(hip_aead_state *st, size_t len, size_t aadlen)
         plugin_check(hipHostFree(st->h_io), "hipHostFree");
     }
     st->h_io = nullptr;
-    plugin_check(hipHostMalloc(&st->h_io, cap + (cap + 16) + aad_cap, hipHostMallocDefault), "hipHostMalloc(staging)");
+    /* fine-grained (coherent) whatever HIP_HOST_COHERENT says: the kernel reads the record and writes its output and the
+     * completion word there, and the next call rewrites the same bytes from the CPU without a stream synchronize */
+    plugin_check(hipHostMalloc(&st->h_io, cap + (cap + 16) + aad_cap, hipHostMallocCoherent), "hipHostMalloc(staging)");
     st->d_io = mapped_or_die(st->h_io);
     st->cap = cap;
     st->aad_cap = aad_cap;
@@ -1881,7 +2287,7 @@ static hip_aead_state *state_new(const void *key, const void *iv, size_t key_siz
     }
     st->ks = ptls_hip_keyset_new(eng, key_size, 1);
     void *d_stage = nullptr;
-    bool ok = st->ks != nullptr && hipHostMalloc(&st->h_stage, 256, hipHostMallocDefault) == hipSuccess &&
+    bool ok = st->ks != nullptr && hipHostMalloc(&st->h_stage, 256, hipHostMallocCoherent) == hipSuccess &&
               hipHostGetDevicePointer(&d_stage, st->h_stage, 0) == hipSuccess &&
               ptls_hip_keyset_set(st->ks, 0, 1, key, iv, st->stream) == 0;
     if (!ok) {

@@ -3,7 +3,7 @@
  *
  * HBM layout:
  *   key slots    KeySlot[nslots]             512 B each: round keys, static IV, H powers
- *   GHASH basis  uint4[nslots][BASIS_VECS]   15 KiB per slot: P * x^e for P in {H, H^2, ..., H^64}, then H^1..H^64
+ *   GHASH basis  uint4[nslots][BASIS_VECS]   21 KiB per slot: P * x^e for P in {H, H^2, ..., H^512}, then H^1..H^64
  *                                            (HYBRID builds: then the bit-sliced round keys, bs8_aes.h)
  *   records      ptls_hip_record_t[n]        48 B descriptors (caller's order)
  *   chunks       Chunk[nchunks]              runs of <= CHUNK_RECS records sharing one key slot
@@ -15,9 +15,20 @@
 #include <stdint.h>
 #include "ptls_hip.h"
 
+/* The product build (Makefile PROD) refuses every switch that makes the kernels compute something else: timing
+ * probes and ablations (wrong output by design) and the TEST-ONLY dealing mutants.  The
+ * measurement switches that stay bit-exact (VALU_TREE, HYBRID, GEN_MASK, ...) are tested as alternate builds. */
+#if defined(PTLS_HIP_PRODUCT)
+#if (defined(CTRHI_PROBE) && CTRHI_PROBE) || (defined(SPLIT_PROBE) && SPLIT_PROBE) || (defined(KEYSWITCH_PROBE) && KEYSWITCH_PROBE) || \
+    (defined(DEAL_MUTANT) && DEAL_MUTANT) || (defined(SPARSE_ABLATE) && SPARSE_ABLATE) || (defined(PLUGIN_PROBE) && PLUGIN_PROBE)
+#error "libptls_hip.so is built with a timing-probe, ablation or test-mutant switch set: such builds compute wrong output"
+#endif
+#endif
+
 namespace ptls_hip {
 
-constexpr int NPOW = 7;          /* H^1 .. H^16 (batch kernel main and tree tables), H^32 (batch kernel main table at G = 32), H^64 (sparse kernel) */
+constexpr int NPOW = 10; /* H^1 .. H^16 (batch kernel main and tree tables), H^32 (batch kernel main table at G = 32), H^64
+                            (sparse kernel), H^128 .. H^512 (the shift of a split record's first part, batch_kernel.h) */
 /* GHASH basis slot: NPOW x 128 vectors P * x^e, then H^1 .. H^64 (the sparse kernel's per-lane final powers) */
 constexpr int LANE_POWS = 64;
 /* HYBRID (measurement switch): this many waves per batch-kernel workgroup (the last ones) run their
@@ -29,7 +40,7 @@ constexpr int LANE_POWS = 64;
 /* with HYBRID, the slot also holds the bit-sliced round keys 1..rounds (bs8::slice_key: 32 words per round) */
 constexpr int BS_KEY_OFF = NPOW * 128 + LANE_POWS; /* uint4 offset in the slot */
 constexpr int BS_KEY_VECS = HYBRID ? 14 * 32 / 4 : 0;
-constexpr int BASIS_VECS = BS_KEY_OFF + BS_KEY_VECS; /* uint4 per key slot (15 KiB; 16.75 KiB with HYBRID) */
+constexpr int BASIS_VECS = BS_KEY_OFF + BS_KEY_VECS; /* uint4 per key slot (21 KiB; 22.75 KiB with HYBRID) */
 constexpr int MAX_LANES = 32;    /* lanes per record (G) of the batch kernel: 1, 2, 4, 8, 16, 32 */
 constexpr int SPARSE_LANES = 64; /* "lanes" value of the wave-per-record kernel (sparse_kernel.hip) */
 /* the planner picks that kernel when a batch's key runs hold fewer records than this on average */
@@ -39,6 +50,23 @@ constexpr int SPARSE_LANES = 64; /* "lanes" value of the wave-per-record kernel 
 /* one workgroup per CU (LDS-limited); 768 threads (3 waves per SIMD, 168 VGPRs) by default, 512 selectable
  * per batch (engine.cpp:plan_wg).  WG_MAX bounds the chunk size the planner cuts key runs into. */
 constexpr int WG_MAX = 1024;
+
+/* Split records (G >= 16, DESIGN.md §4.1 "split tasks"; planned in engine.cpp plan_splits): the planner may deal a key run's longest tasks as two part
+ * tasks each, part A = GHASH elements [0, N - B) of the task's records, part B = [N - B, N), B = split_tail(N) a power
+ * of two near N / 2.  Part A multiplies its partial GHASH by H^B (basis plane log2 B), each part leaves its partial in
+ * an LDS slot of the workgroup, and the part that finishes second XORs them into the tag.  The slots sit after the
+ * tables and the task counter: SPLIT_SLOTS records of {partial A, partial B} (32 B) + a 4-byte arrival counter. */
+constexpr int SPLIT_SLOTS = 192;
+constexpr int SPLIT_MIN_N = 256;  /* records of fewer GHASH elements are never split */
+constexpr int SPLIT_MAX_N = 1536; /* nor records of more (B would be under a third of N) */
+constexpr int split_tail(int N)
+{
+    return N >= 768 ? 512 : N >= 384 ? 256 : 128;
+}
+constexpr int split_plane(int N)
+{
+    return N >= 768 ? 9 : N >= 384 ? 8 : 7;
+}
 
 struct KeySlot {
     uint32_t rk[60];      /* AES round keys, raw byte order as little-endian words (11 or 15 used) */
@@ -58,7 +86,8 @@ struct Chunk {
     uint32_t first; /* position of the chunk's first record in the order array */
     uint32_t count; /* records in the chunk, all with the same key slot */
     uint32_t key;   /* key slot */
-    uint32_t flags; /* bit0: every record of the chunk is 16-byte aligned (in/out/aad offsets) */
+    uint32_t flags; /* bit0: every record of the chunk is 16-byte aligned (in/out/aad offsets); bits 8..15: how many of the
+                       chunk's first (longest) wave tasks are dealt as two part tasks each (split records, batch_kernel.h) */
 };
 
 struct KernelArgs {
@@ -88,6 +117,8 @@ struct KernelArgs {
      * stream synchronize) */
     uint32_t *done;
     uint32_t done_seq;
+    /* optional diagnostic clock stamps, 4 x uint64 per workgroup (ptls_hip_batch_set_clock); nullptr = none */
+    uint64_t *clk;
 };
 
 /* host-side launchers, defined next to the kernels (aesgcm_kernels.hip, batch_g*.hip) */

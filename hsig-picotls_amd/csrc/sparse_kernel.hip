@@ -118,13 +118,14 @@ __global__ void __launch_bounds__(SPARSE_WG)
                          uint8_t *out, uint64_t *__restrict__ result, const KeySlot *__restrict__ slots,
                          const uint32_t *__restrict__ basis, const uint32_t *__restrict__ t0, const ptls_hip_supp_t *__restrict__ supp,
                          const KeySlot *__restrict__ hp_slots, uint32_t hp_nslots, uint8_t *mask, ptls_hip_record_t one,
-                         uint32_t *done, uint32_t done_seq)
+                         uint32_t *done, uint32_t done_seq, uint64_t *__restrict__ clk)
 {
     __shared__ __attribute__((aligned(16))) uint8_t lds[SP_TAB + (SPARSE_WG / 64) * 8192];
     static_assert(SP_TAB + (SPARSE_WG / 64) * 8192 <= 163840, "AES tables + per-wave GHASH tables must fit the CU's 160 KiB");
     const int lane = threadIdx.x & 63;
     const uint32_t lb_aes = (uint32_t)(lane & 31) * 4u; /* table base 0: byte 2 of the address is 0 */
     const uint32_t tab = __builtin_amdgcn_readfirstlane(SP_TAB + (uint32_t)(threadIdx.x >> 6) * 8192u); /* wave-uniform */
+    clock_stamp(clk, 0);
     if (!PLUGIN_PROBE)
         build_aes_tables<SPARSE_WG>(lds, 0, t0); /* the batch kernel's layout at offset 0 */
     __syncthreads();
@@ -195,7 +196,7 @@ __global__ void __launch_bounds__(SPARSE_WG)
             int big = 0;
 #pragma unroll
             for (int b = 0; b < NE; ++b) {
-                e[b] = elem_of(m + b < mend ? lane + (m + b) * 64 : N, N, na, nc, L);
+                e[b] = elem_of(m + b < mend ? lane + (m + b) * 64 : N, N, na, nc, L, N);
                 inb[b] = V4{0, 0, 0, 0};
                 if (e[b].is_c) {
                     const bool tb = tflag && e[b].c == nc - 1; /* the block holding the content-type byte */
@@ -356,6 +357,10 @@ __global__ void __launch_bounds__(SPARSE_WG)
         if (lane == 0)
             __hip_atomic_store(done, done_seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
+    if (clk != nullptr) { /* the workgroup's end: after its last wave */
+        __syncthreads();
+        clock_stamp(clk, 1);
+    }
 }
 
 template <int R, bool O>
@@ -363,10 +368,10 @@ static hipError_t launch_sparse_one(unsigned grid, hipStream_t s, const KernelAr
 {
     if (aligned)
         hipLaunchKernelGGL((aesgcm_sparse_kernel<R, O, true>), dim3(grid), dim3(SPARSE_WG), 0, s, a.recs_ord, a.order, a.chunks,
-                           a.nchunks, a.in, a.aad, a.out, a.result, a.slots, a.basis, a.t0, a.supp, a.hp_slots, a.hp_nslots, a.mask, a.one, a.done, a.done_seq);
+                           a.nchunks, a.in, a.aad, a.out, a.result, a.slots, a.basis, a.t0, a.supp, a.hp_slots, a.hp_nslots, a.mask, a.one, a.done, a.done_seq, a.clk);
     else
         hipLaunchKernelGGL((aesgcm_sparse_kernel<R, O, false>), dim3(grid), dim3(SPARSE_WG), 0, s, a.recs_ord, a.order, a.chunks,
-                           a.nchunks, a.in, a.aad, a.out, a.result, a.slots, a.basis, a.t0, a.supp, a.hp_slots, a.hp_nslots, a.mask, a.one, a.done, a.done_seq);
+                           a.nchunks, a.in, a.aad, a.out, a.result, a.slots, a.basis, a.t0, a.supp, a.hp_slots, a.hp_nslots, a.mask, a.one, a.done, a.done_seq, a.clk);
     return hipGetLastError();
 }
 

@@ -57,6 +57,9 @@ SIGNATURES = {
     "ptls_hip_batch_set_workgroup": (_i, [_vp, _i]),
     "ptls_hip_batch_workgroup": (_i, [_vp]),
     "ptls_hip_batch_set_max_workgroups": (_i, [_vp, _i]),
+    "ptls_hip_batch_grid": (_i, [_vp]),
+    "ptls_hip_batch_split_tasks": (_i, [_vp]),
+    "ptls_hip_batch_set_clock": (_i, [_vp, _vp, _sz]),
     "ptls_hip_aesecb_init": (_i, [_vp, _i, _vp, _sz, _i]),
     "ptls_hip_aesecb_dispose": (None, [_vp]),
     "ptls_hip_aesecb_encrypt": (None, [_vp, _vp, _vp]),
@@ -88,6 +91,15 @@ SIGNATURES = {
     "ptls_hip_pipeline_last_transport": (_i, [_vp]),
     "ptls_hip_host_register": (_i, [_vp, _sz]),
     "ptls_hip_host_unregister": (_i, [_vp]),
+    "ptls_hip_partition_bytes": (_i, [_vp, _sz, _sz, _vp]),
+    "ptls_hip_node_new": (_vp, [_vp, _sz, _sz, _sz, _sz]),
+    "ptls_hip_node_free": (None, [_vp]),
+    "ptls_hip_node_size": (_sz, [_vp]),
+    "ptls_hip_node_keyset_set": (_i, [_vp, _sz, _sz, _vp, _vp]),
+    "ptls_hip_node_set_transport": (_i, [_vp, _i]),
+    "ptls_hip_node_seal": (_i, [_vp, _vp, _sz, _vp, _vp, _vp]),
+    "ptls_hip_node_open": (_i, [_vp, _vp, _sz, _vp, _vp, _vp, _vp]),
+    "ptls_hip_node_last_split": (_i, [_vp, _vp, _vp]),
 }
 DATA_SYMBOLS = ("ptls_hip_aes128ctr", "ptls_hip_aes128gcm", "ptls_hip_aes256ctr", "ptls_hip_aes256gcm",
                 "ptls_hip_non_temporal_aes128gcm", "ptls_hip_non_temporal_aes256gcm")
@@ -106,7 +118,9 @@ def lib():
             raise HipError(f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'`")
         L = ctypes.CDLL(LIB_PATH)
         for name, (res, args) in SIGNATURES.items():
-            f = getattr(L, name)
+            f = getattr(L, name, None)
+            if f is None:  # an older build loaded by an A/B tool (PTLS_HIP_LIB); tests/test_abi.py checks the product
+                continue
             f.restype = res
             f.argtypes = args
         _lib = L
@@ -245,6 +259,22 @@ class Batch:
         """cap the launch grid at n workgroups (0 = one per CU); chunks are then planned for n CUs"""
         _check(lib().ptls_hip_batch_set_max_workgroups(self.ptr, n), "batch_set_max_workgroups")
 
+    @property
+    def split_tasks(self):
+        """wave tasks the plan deals as two part tasks (split records)"""
+        return lib().ptls_hip_batch_split_tasks(self.ptr)
+
+    @property
+    def grid(self):
+        """workgroups of one launch"""
+        return lib().ptls_hip_batch_grid(self.ptr)
+
+    def set_clock(self, buf):
+        """diagnostic clock stamps of the following launches into `buf` (device tensor of >= 32 bytes per workgroup;
+        None = off): per workgroup {cycles0, ticks0, cycles1, ticks1}, see clock_of()"""
+        nbytes = 0 if buf is None else buf.numel() * buf.element_size()
+        _check(lib().ptls_hip_batch_set_clock(self.ptr, _ptr(buf), nbytes), "batch_set_clock")
+
     def seal(self, keyset, inp, aad, out, stream=None):
         _check(lib().ptls_hip_aesgcm_seal_batch(self.ptr, keyset.ptr, _ptr(inp), _ptr(aad), _ptr(out), _stream(stream)),
                "seal_batch")
@@ -276,6 +306,67 @@ class Batch:
         if self.ptr:
             lib().ptls_hip_batch_free(self.ptr)
             self.ptr = None
+
+
+def partition_bytes(recs, parts):
+    """ptls_hip_partition_bytes: record ranges of about equal payload bytes (host-only, no device needed)"""
+    recs = np.ascontiguousarray(recs, dtype=RECORD_DTYPE)
+    b = np.zeros(parts + 1, dtype=np.uint64)
+    _check(lib().ptls_hip_partition_bytes(recs.ctypes.data, len(recs), parts, b.ctypes.data), "partition_bytes")
+    return [int(x) for x in b]
+
+
+class Node:
+    """one batch over several devices (ptls_hip_node_*): byte-balanced contiguous ranges, one host thread + pipeline per
+    device; buffers are host memory (pinned for the zero-copy transport)"""
+
+    def __init__(self, devices, key_size, nslots, slice_bytes=64 << 20, transport=TRANSPORT_AUTO):
+        arr = (ctypes.c_int * len(devices))(*devices)
+        self.ndev, self.key_size = len(devices), key_size
+        self.ptr = lib().ptls_hip_node_new(arr, len(devices), key_size, nslots, slice_bytes)
+        if not self.ptr:
+            raise HipError(f"ptls_hip_node_new: {last_error()}")
+        _check(lib().ptls_hip_node_set_transport(self.ptr, transport), "node_set_transport")
+
+    def set_keys(self, first, keys, ivs):
+        """the same keys into every device's keyset: slots [first, first + len(keys) / key_size)"""
+        keys = bytes(keys)
+        ivs = None if ivs is None else bytes(ivs)
+        n = len(keys) // self.key_size
+        _check(lib().ptls_hip_node_keyset_set(self.ptr, first, n, keys, ivs), "node_keyset_set")
+
+    def seal(self, recs, h_in, h_aad, h_out):
+        recs = np.ascontiguousarray(recs, dtype=RECORD_DTYPE)
+        _check(lib().ptls_hip_node_seal(self.ptr, recs.ctypes.data, len(recs), _ptr(h_in), _ptr(h_aad), _ptr(h_out)), "node_seal")
+
+    def open(self, recs, h_in, h_aad, h_out, h_result):
+        recs = np.ascontiguousarray(recs, dtype=RECORD_DTYPE)
+        _check(lib().ptls_hip_node_open(self.ptr, recs.ctypes.data, len(recs), _ptr(h_in), _ptr(h_aad), _ptr(h_out),
+                                        _ptr(h_result)), "node_open")
+
+    def last_split(self):
+        """(per-device seconds, record bounds) of the last call"""
+        sec = np.zeros(self.ndev, dtype=np.float64)
+        b = np.zeros(self.ndev + 1, dtype=np.uint64)
+        _check(lib().ptls_hip_node_last_split(self.ptr, sec.ctypes.data, b.ctypes.data), "node_last_split")
+        return sec.tolist(), [int(x) for x in b]
+
+    def close(self):
+        if self.ptr:
+            lib().ptls_hip_node_free(self.ptr)
+            self.ptr = None
+
+
+def clock_of(stamps, grid):
+    """the clock one launch ran at, from its stamps (Batch.set_clock; array of >= 4 * grid uint64): per workgroup
+    delta(shader cycles) / delta(100 MHz ticks) x 100 MHz.  Returns (median GHz over workgroups, min, max, the launch's
+    span in ms from the first start to the last end on the 100 MHz counter)"""
+    a = np.asarray(stamps, dtype=np.uint64).reshape(-1, 4)[:grid].astype(np.float64)
+    dt, dr = a[:, 2] - a[:, 0], a[:, 3] - a[:, 1]
+    ok = dr > 0
+    ghz = dt[ok] / dr[ok] * 0.1
+    span_ms = (a[:, 3].max() - a[:, 1].min()) / 1e5
+    return float(np.median(ghz)), float(ghz.min()), float(ghz.max()), float(span_ms)
 
 
 def is_supported():

@@ -193,6 +193,16 @@ int ptls_hip_batch_workgroup(ptls_hip_batch_t *batch);
  * count, the default).  For tests of the work distribution (a workgroup then takes several chunks of one
  * key run) and for sharing a device with other work. */
 int ptls_hip_batch_set_max_workgroups(ptls_hip_batch_t *batch, int n);
+/* wave tasks the launch plan deals as two part tasks each (split records: a key run's longest records when its tasks
+ * are few for the workgroup's waves; lanes per record 16 and 32) */
+int ptls_hip_batch_split_tasks(ptls_hip_batch_t *batch);
+/* workgroups one seal/open launch of the batch uses (for sizing the clock-stamp buffer below) */
+int ptls_hip_batch_grid(ptls_hip_batch_t *batch);
+/* Diagnostic: the following launches of the batch write, per workgroup w, the shader-cycle counter and the constant
+ * 100 MHz counter at the start and at the end of its work: d_buf[4w .. 4w + 3] = {cycles0, ticks0, cycles1, ticks1}
+ * (uint64, device memory of >= 32 bytes per workgroup).  delta(cycles) / delta(ticks) x 100 MHz = the clock the launch
+ * ran at.  d_buf == NULL switches the stamps off (the default: then no stamp instruction executes). */
+int ptls_hip_batch_set_clock(ptls_hip_batch_t *batch, void *d_buf, size_t nbytes);
 
 /* Asynchronous on `stream`; all pointers are device (or device-accessible) memory.  Fails with
  * PTLS_HIP_EINVAL (nothing launched) when a record names a key slot outside `ks`. */
@@ -320,6 +330,35 @@ int ptls_hip_pipeline_set_transport(ptls_hip_pipeline_t *p, int transport);
 int ptls_hip_pipeline_last_transport(ptls_hip_pipeline_t *p);
 int ptls_hip_host_register(void *ptr, size_t len);
 int ptls_hip_host_unregister(void *ptr);
+
+/* ------------------------------------------------------------------------------------------ *
+ * 2d. one batch over several devices (records are independent, no collective)  *
+ * ------------------------------------------------------------------------------------------ */
+
+/* Host-side planning: contiguous ranges of about equal payload bytes.  bounds (parts + 1 entries): range r =
+ * records [bounds[r], bounds[r + 1]), bounds[0] = 0, bounds[parts] = n; range r ends right after the first record
+ * whose prefix sum of len reaches ceil(total * (r + 1) / parts).  Equal counts for equal lengths. */
+int ptls_hip_partition_bytes(const ptls_hip_record_t *recs, size_t n, size_t parts, size_t *bounds);
+
+/* A node: one engine, one keyset (nslots key slots of key_size) and one host pipeline (slice_bytes, as
+ * ptls_hip_pipeline_new) per listed device; a device may be listed more than once.  seal / open split the records by
+ * ptls_hip_partition_bytes and run every range on its own device from its own host thread, through that device's
+ * pipeline (transport AUTO by default: the kernels read and write pinned host buffers over the device's own PCIe link),
+ * and return when every device is done.  Records, offsets and buffers are as for ptls_hip_pipeline_seal / open.
+ * node_keyset_set loads the same keys into every device's keyset (ptls_hip_keyset_set semantics).
+ * last_split: the last call's per-device wall-clock seconds (ndev doubles) and record ranges (ndev + 1 bounds),
+ * either pointer may be NULL; whole-node rate = payload bytes / the largest of the seconds. */
+typedef struct st_ptls_hip_node_t ptls_hip_node_t;
+ptls_hip_node_t *ptls_hip_node_new(const int *devices, size_t ndev, size_t key_size, size_t nslots, size_t slice_bytes);
+void ptls_hip_node_free(ptls_hip_node_t *node);
+size_t ptls_hip_node_size(ptls_hip_node_t *node);
+int ptls_hip_node_keyset_set(ptls_hip_node_t *node, size_t first, size_t count, const void *keys, const void *ivs);
+int ptls_hip_node_set_transport(ptls_hip_node_t *node, int transport);
+int ptls_hip_node_seal(ptls_hip_node_t *node, const ptls_hip_record_t *recs, size_t n, const void *h_in, const void *h_aad,
+                       void *h_out);
+int ptls_hip_node_open(ptls_hip_node_t *node, const ptls_hip_record_t *recs, size_t n, const void *h_in, const void *h_aad,
+                       void *h_out, uint64_t *h_result);
+int ptls_hip_node_last_split(ptls_hip_node_t *node, double *seconds, size_t *bounds);
 
 /* ------------------------------------------------------------------------------------------ *
  * 3. synthetic workload (bench / tests): the payload of descriptor i is the splitmix64 stream     *

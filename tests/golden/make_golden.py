@@ -57,11 +57,16 @@ def config_record(o, cfg, i):
 
 
 def config_samples(cfg):
+    """first / last 64 records of every rank's shard at up to 8 ranks (bench.py: rank r owns records [r n, (r + 1) n)
+    of a per-GPU config, weak scaling; configs[4] is one 32M batch in 8 shards of 4M) and both sides of every seam"""
     n = cfg["n"]
-    idx = list(range(64)) + list(range(n - 64, n))
-    if n == 32 << 20:  # 8 shards of 4M: both sides of every seam
-        for r in range(1, 8):
-            idx += [r * (4 << 20) - 1, r * (4 << 20)]
+    shard = 4 << 20 if n == 32 << 20 else n
+    total = n if n == 32 << 20 else 8 * n
+    idx = []
+    for r in range(total // shard):
+        idx += list(range(r * shard, r * shard + 64)) + list(range((r + 1) * shard - 64, (r + 1) * shard))
+        if r:
+            idx += [r * shard - 1, r * shard]
     return sorted(set(idx))
 
 

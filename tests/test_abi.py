@@ -197,3 +197,42 @@ def test_aesecb_api_argument_checks():
         assert L.ptls_hip_aesecb_init(ctypes.addressof(ctx), 1, bytes(16), 16, 0) == -2
         assert not ctx.state and ctx.rounds == 0
         L.ptls_hip_aesecb_dispose(ctypes.addressof(ctx))  # no-op on an empty context
+
+
+def test_partition_bytes_matches_bench_rule():
+    """ptls_hip_partition_bytes (host-only, the node API's split) == bench.py's partition_bytes on configs[3]'s lengths"""
+    import numpy as np
+    import sys
+    sys.path.insert(0, ROOT)
+    import bench
+    lens = bench.record_lengths(bench.CONFIGS["c4"], np.arange(20000, dtype=np.uint64))
+    recs = np.zeros(len(lens), dtype=ptls_hip.RECORD_DTYPE)
+    recs["len"] = lens
+    for parts in (1, 2, 3, 7, 8):
+        assert ptls_hip.partition_bytes(recs, parts) == bench.partition_bytes(lens, parts)
+    assert ptls_hip.partition_bytes(recs[:0], 4) == [0, 0, 0, 0, 0]
+    eq = np.zeros(4096, dtype=ptls_hip.RECORD_DTYPE)
+    eq["len"] = 1350
+    assert ptls_hip.partition_bytes(eq, 4) == [0, 1024, 2048, 3072, 4096]
+
+
+def test_node_fails_loudly_without_device():
+    """the multi-device node has no CPU path either"""
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("needs a machine without a GPU")
+    with pytest.raises(ptls_hip.HipError):
+        ptls_hip.Node([0], 16, 1)
+
+
+@pytest.mark.skipif(shutil.which("/opt/rocm/bin/hipcc") is None, reason="hipcc missing")
+@pytest.mark.parametrize("switch", ["CTRHI_PROBE=1", "SPARSE_ABLATE=1", "DEAL_MUTANT=1"])
+def test_product_build_refuses_wrong_output_switches(switch, tmp_path):
+    """the product objects are compiled with PTLS_HIP_PRODUCT (hsig-picotls_amd/Makefile PROD): any timing-probe /
+    ablation / mutant switch (wrong output by design) is then a compile error, not a library"""
+    src = os.path.join(ROOT, "hsig-picotls_amd", "csrc", "sparse_kernel.hip")
+    inc = ["-I" + os.path.join(ROOT, "include"), "-I" + os.path.join(ROOT, "hsig-picotls_amd", "csrc")]
+    cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-std=c++17", "-fsyntax-only", "-DPTLS_HIP_PRODUCT=1", "-D" + switch,
+           *inc, src]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
+    assert r.returncode != 0 and "timing-probe, ablation or test-mutant switch" in r.stderr

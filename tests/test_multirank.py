@@ -19,7 +19,7 @@ def _worker(rank, world, port, cfg, q):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     import bench
     idx, recs, in_total, out_total, lens = bench.make_workload(cfg, rank)
-    t = bench.max_over_ranks(1.0 + rank, world, "cpu")
+    t = bench.max_over_ranks(1.0 + rank, world)
     q.put((rank, idx.copy(), recs["key"].copy(), recs["seq"].copy(), lens.copy(), t))
     dist.barrier()
     dist.destroy_process_group()
@@ -69,14 +69,14 @@ def test_multi_key_shards_key_major():
         assert lens.min() >= 64 and lens.max() <= 16384
 
 
-def _bench(*extra, env=None):
+def _bench(*extra, env=None, config="c3", records=2048):
     import json
     import subprocess
     e = dict(os.environ)
     for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
         e.pop(k, None)
     e.update(env or {})
-    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--dry-run", "--config", "c3", "--records", "2048",
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--dry-run", "--config", config, "--records", str(records),
                           "--steps", "3", "--warmup", "1", *extra], env=e, capture_output=True, text=True, timeout=240)
     lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
     return out.returncode, [json.loads(ln) for ln in lines], out.stderr
@@ -91,7 +91,11 @@ def test_bench_launches_its_own_ranks():
     assert len(lines) == 1, lines
     r = lines[0]
     assert r["n_gpus"] == 2 and len(r["per_rank"]) == 2
-    assert [x[0] for x in r["first_index_per_rank"]] == [0.0, 2048.0]  # disjoint record ranges
+    # disjoint record ranges: the first 2048 records of each rank's 4M-record shard (configs[2] per GPU), so every rank
+    # holds records with lib/fusion.c digests (tests/golden/configs.json) for its parity check
+    assert [x[0] for x in r["first_index_per_rank"]] == [0.0, float(4 << 20)]
+    assert [x["records"] for x in r["per_rank"]] == [[0, 2048], [4 << 20, (4 << 20) + 2048]]
+    assert all(x["golden_records_checked"] >= 64 for x in r["per_rank"])
     slow = max(x["seconds"] for x in r["per_rank"])
     assert r["per_rank"][1]["seconds"] > r["per_rank"][0]["seconds"]  # rank 1 sleeps twice as long
     total = 2 * 2 * 2048 * 1350 * 3 / (1 << 30)  # ranks x (seal + open) x bytes x steps
@@ -102,3 +106,48 @@ def test_bench_launches_its_own_ranks():
 def test_bench_rejects_a_world_size_mismatch():
     rc, lines, err = _bench("--gpus", "2", env={"WORLD_SIZE": "3", "RANK": "0", "LOCAL_RANK": "0"})
     assert rc == 2 and not lines and "WORLD_SIZE=3" in err
+
+
+def test_partition_bytes_balances_payload():
+    """contiguous ranges of about equal payload bytes (prefix sum of L) on configs[3]'s lengths"""
+    sys.path.insert(0, ROOT)
+    import bench
+    cfg = dict(bench.CONFIGS["c4"])
+    lens = bench.record_lengths(cfg, np.arange(1 << 16, dtype=np.uint64))
+    for parts in (1, 2, 3, 8):
+        b = bench.partition_bytes(lens, parts)
+        assert b[0] == 0 and b[-1] == len(lens) and all(x <= y for x, y in zip(b, b[1:]))
+        share = [int(lens[b[r]:b[r + 1]].sum()) for r in range(parts)]
+        assert sum(share) == int(lens.sum())
+        assert max(share) - min(share) <= 2 * 16384  # within one record's bytes of the mean on both sides
+    # equal counts for fixed L
+    assert bench.partition_bytes(np.full(4096, 1350, dtype=np.uint64), 4) == [0, 1024, 2048, 3072, 4096]
+    assert bench.partition_bytes(np.zeros(0, dtype=np.uint64), 2) == [0, 0, 0]
+
+
+def test_bench_strong_scaling_splits_by_bytes():
+    """--scaling strong: ONE batch of configs[3]'s records split over 2 ranks by payload bytes, not by count"""
+    rc, lines, err = _bench("--gpus", "2", "--scaling", "strong", config="c4", records=1 << 16)
+    assert rc == 0, err[-3000:]
+    r = lines[0]
+    assert r["scaling"] == "strong"
+    (a0, a1), (b0, b1) = (x["records"] for x in r["per_rank"])
+    assert a0 == 0 and a1 == b0 and b1 == 1 << 16  # contiguous, complete
+    p0, p1 = (x["payload_bytes"] for x in r["per_rank"])
+    assert abs(p0 - p1) <= 2 * 16384
+
+
+def test_every_rank_of_the_weak_c2_split_has_golden_records():
+    """bench.py checks sealed records against lib/fusion.c digests on EVERY rank: the fixture holds the first and last
+    64 records of each rank's 1M-record shard of configs[1] at up to 8 GPUs (and configs[4]'s 8 shards)"""
+    sys.path.insert(0, ROOT)
+    import bench
+    for name in ("c2", "c3", "c4", "c5"):
+        g = bench.golden_digests(name)
+        n = bench.CONFIGS[name]["n"]
+        for rank in range(8):
+            lo, hi = bench.rank_range(bench.CONFIGS[name], rank, 8, "weak")
+            head = np.arange(lo, lo + 64, dtype=np.uint64)
+            tail = np.arange(hi - 64, hi, dtype=np.uint64)
+            assert len(bench.golden_positions(head, g)) == 64 and len(bench.golden_positions(tail, g)) == 64, (name, rank)
+            assert hi - lo == n

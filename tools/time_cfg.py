@@ -15,6 +15,10 @@ ap.add_argument("--key-len", type=int, default=0, help="override the key size (1
 ap.add_argument("--fixed-len", type=int, default=0, help="every record this many bytes (instead of the config's lengths)")
 ap.add_argument("--keys", type=int, default=0, help="override the number of keys")
 ap.add_argument("--wg", type=int, default=0, help="workgroup size (512 / 768; 0 = the planner's)")
+ap.add_argument("--clock", action="store_true", help="one more seal + open with the kernels' clock stamps (builds that have them)")
+ap.add_argument("--reps", type=int, default=6, help="timed repetitions (the first is dropped)")
+ap.add_argument("--zeros", action="store_true", help="all-zero plaintext (default: bench.py's splitmix64 records; zero data "
+                "runs at a higher clock, MI355X_MICROARCH.md DVFS)")
 args = ap.parse_args()
 import torch
 import bench
@@ -49,21 +53,39 @@ for lib in args.libs:
     if args.wg:
         ob.set_workgroup(args.wg)
     d_pt = torch.zeros(in_total + 64, dtype=torch.uint8, device="cuda")
+    if not args.zeros:
+        d_idx = torch.from_numpy(idx.astype(np.int64)).cuda()
+        sb.fill(d_pt, bench.SEED_DATA, index=d_idx)
+        torch.cuda.synchronize()
+        del d_idx
     d_ct = torch.zeros(out_total + 64, dtype=torch.uint8, device="cuda")
     d_out = torch.empty(in_total + 64, dtype=torch.uint8, device="cuda")
     d_aad = torch.zeros(len(recs) * 16, dtype=torch.uint8, device="cuda")
     d_res = torch.zeros(len(recs), dtype=torch.int64, device="cuda")
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
     ts = []
-    for i in range(6):
+    for i in range(args.reps):
         ev[0].record(); sb.seal(ks, d_pt, d_aad, d_ct); ev[1].record(); ob.open(ks, d_ct, d_aad, d_out, d_res); ev[2].record()
         torch.cuda.synchronize()
         if i:
             ts.append((ev[0].elapsed_time(ev[1]), ev[1].elapsed_time(ev[2])))
     s, o = np.median(np.array(ts), axis=0)
     gib = float(lens.sum()) / 2 ** 30
-    print(f"{os.path.basename(lib)} {args.config} lanes={sb.lanes} wg={sb.workgroup}: seal {s:.3f} ms ({gib / s * 1e3:.1f} GiB/s)  "
-          f"open {o:.3f} ms ({gib / o * 1e3:.1f} GiB/s)", flush=True)
+    clk = ""
+    if args.clock and hasattr(ptls_hip.lib(), "ptls_hip_batch_set_clock"):
+        cs = torch.zeros(4 * sb.grid, dtype=torch.int64, device="cuda")
+        co = torch.zeros(4 * ob.grid, dtype=torch.int64, device="cuda")
+        sb.set_clock(cs); ob.set_clock(co)
+        ev[0].record(); sb.seal(ks, d_pt, d_aad, d_ct); ev[1].record(); ob.open(ks, d_ct, d_aad, d_out, d_res); ev[2].record()
+        torch.cuda.synchronize()
+        sc = ptls_hip.clock_of(cs.cpu().numpy().view(np.uint64), sb.grid)
+        oc = ptls_hip.clock_of(co.cpu().numpy().view(np.uint64), ob.grid)
+        clk = (f"  clock seal {sc[0]:.3f} GHz (wg {sc[1]:.3f}-{sc[2]:.3f}, span {sc[3]:.3f} ms, event {ev[0].elapsed_time(ev[1]):.3f} ms)"
+               f" open {oc[0]:.3f} GHz")
+        sb.set_clock(None); ob.set_clock(None)
+    print(f"{os.path.basename(os.path.dirname(os.path.dirname(lib))) or '.'}/{os.path.basename(lib)} {args.config} lanes={sb.lanes} "
+          f"wg={sb.workgroup}: seal {s:.3f} ms ({gib / s * 1e3:.1f} GiB/s)  open {o:.3f} ms ({gib / o * 1e3:.1f} GiB/s){clk}",
+          flush=True)
     sb.close(); ob.close(); ks.close(); eng.close()
     del d_pt, d_ct, d_out
     torch.cuda.empty_cache()
