@@ -1166,10 +1166,11 @@ static void *mapped_ptr(const void *h)
 }
 
 /* the device address of h when pinned or registered host memory covers ALL of [h, h + need) with one mapping, else
- * nullptr: a buffer registered only in part must not be handed to the kernels (they would touch unmapped host pages
- * over PCIe; the copy transport reads any host memory).  The mapping's range comes from the pointer attributes; the
- * last byte must also map, contiguously with the first. */
-static void *mapped_span(const void *h, uint64_t need)
+ * nullptr; *partial = the start is mapped but not the whole span.  Such a buffer (registered only in part) must not
+ * be handed to the kernels, which would touch unmapped host pages over PCIe, and the copy engines refuse it as well
+ * (hipMemcpyAsync: invalid argument), so the call fails with EINVAL.  The mapping's range comes from the pointer
+ * attributes; the last byte must also map, contiguously with the first. */
+static void *mapped_span(const void *h, uint64_t need, bool *partial)
 {
     void *d = mapped_ptr(h);
     if (d == nullptr || need <= 1)
@@ -1181,14 +1182,18 @@ static void *mapped_span(const void *h, uint64_t need)
         hipPointerGetAttribute(&size, HIP_POINTER_ATTRIBUTE_RANGE_SIZE, reinterpret_cast<hipDeviceptr_t>(d)) == hipSuccess &&
         size != 0) {
         const bool in_range = (start <= dp && dp + need <= start + size) || (start <= hp && hp + need <= start + size);
-        if (!in_range)
+        if (!in_range) {
+            *partial = true;
             return nullptr;
+        }
     } else {
         (void)hipGetLastError();
     }
     void *d_last = mapped_ptr(static_cast<const uint8_t *>(h) + (need - 1));
-    if (d_last == nullptr || reinterpret_cast<uintptr_t>(d_last) != dp + (need - 1))
+    if (d_last == nullptr || reinterpret_cast<uintptr_t>(d_last) != dp + (need - 1)) {
+        *partial = true;
         return nullptr;
+    }
     return d;
 }
 
@@ -1358,7 +1363,7 @@ static int pipeline_run(ptls_hip_pipeline_t *p, ptls_hip_keyset_t *ks, const ptl
         if (recs[i].key >= ks->nslots)
             return fail(PTLS_HIP_EINVAL, "pipeline: record %zu names key slot %u, the keyset has %zu", i, recs[i].key, ks->nslots);
     DeviceGuard g(p->eng->device);
-    if (p->transport != PTLS_HIP_TRANSPORT_COPY && n != 0) {
+    if (n != 0) {
         /* the bytes the kernels would touch in each buffer: [base, base + need) */
         uint64_t need_in = 0, need_out = 0, need_aad = 0, need_mask = 0;
         for (size_t i = 0; i < n; ++i) {
@@ -1372,13 +1377,17 @@ static int pipeline_run(ptls_hip_pipeline_t *p, ptls_hip_keyset_t *ks, const ptl
             if (supp != nullptr && (supp[i].flags & PTLS_HIP_SUPP_ENABLE))
                 need_mask = std::max<uint64_t>(need_mask, supp[i].mask_off + 16);
         }
-        const uint8_t *d_in = static_cast<const uint8_t *>(mapped_span(h_in, need_in));
-        uint8_t *d_out = static_cast<uint8_t *>(mapped_span(h_out, need_out));
-        const uint8_t *d_aad = static_cast<const uint8_t *>(mapped_span(h_aad, need_aad));
-        uint8_t *d_mask = static_cast<uint8_t *>(mapped_span(h_mask, need_mask));
-        uint64_t *d_res = open ? static_cast<uint64_t *>(mapped_span(h_result, (uint64_t)n * 8)) : nullptr;
+        bool partial = false;
+        const uint8_t *d_in = static_cast<const uint8_t *>(mapped_span(h_in, need_in, &partial));
+        uint8_t *d_out = static_cast<uint8_t *>(mapped_span(h_out, need_out, &partial));
+        const uint8_t *d_aad = static_cast<const uint8_t *>(mapped_span(h_aad, need_aad, &partial));
+        uint8_t *d_mask = static_cast<uint8_t *>(mapped_span(h_mask, need_mask, &partial));
+        uint64_t *d_res = open ? static_cast<uint64_t *>(mapped_span(h_result, (uint64_t)n * 8, &partial)) : nullptr;
+        if (partial)
+            return fail(PTLS_HIP_EINVAL, "pipeline: a host buffer is pinned or registered only in part (its mapping ends before "
+                                         "the last byte the records touch): neither transport can use it");
         const bool ok = d_in != nullptr && d_out != nullptr && (h_aad == nullptr || d_aad != nullptr) && (h_mask == nullptr || d_mask != nullptr);
-        if (ok) {
+        if (ok && p->transport != PTLS_HIP_TRANSPORT_COPY) {
             const int rc = pipeline_run_mapped(p, ks, recs, n, d_in, d_aad, d_out, h_result, d_res, mode, hp_ks, supp, d_mask);
             if (rc != 0)
                 drain_slots(p);
@@ -2070,6 +2079,15 @@ static void state_reserve(hip_aead_state *st, size_t len, size_t aadlen)
     st->aad_cap = aad_cap;
 }
 
+#if STAMP_PHASES
+/* diagnostic build (Makefile `diag`): the last plugin call's phase stamps (sparse_kernel.hip phase_stamp) */
+static uint64_t *g_diag_stamps = nullptr;
+extern "C" int ptls_hip_diag_plugin_stamps(uint64_t *out)
+{
+    return g_diag_stamps == nullptr ? -1 : (int)hipMemcpy(out, g_diag_stamps, 16 * sizeof(uint64_t), hipMemcpyDeviceToHost);
+}
+#endif
+
 /* fused header protection for one plugin call: sample offset inside the record output, hp key slots */
 struct PluginSupp {
     uint64_t sample_off;
@@ -2131,6 +2149,11 @@ static uint64_t plugin_run(hip_aead_state *st, bool open, void *output, const vo
     }
     a.done = reinterpret_cast<uint32_t *>(st->d_stage + ST_DONE);
     a.done_seq = ++st->done_seq;
+#if STAMP_PHASES
+    if (g_diag_stamps == nullptr)
+        plugin_check(hipMalloc(&g_diag_stamps, 16 * sizeof(uint64_t)), "hipMalloc(stamps)");
+    a.clk = g_diag_stamps;
+#endif
     const int e = launch_batch(SPARSE_LANES, st->ks->key_size == 16 ? 10 : 14, open, 0, 1, st->stream, a, true);
     if (e != 0) {
         g_err = hipGetErrorString((hipError_t)e);

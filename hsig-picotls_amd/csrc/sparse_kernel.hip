@@ -43,7 +43,35 @@ namespace ptls_hip {
 #ifndef SPARSE_PE
 #define SPARSE_PE 2 /* GHASH elements (AES blocks) per lane per main-loop iteration */
 #endif
+#ifndef STAMP_PHASES
+#define STAMP_PHASES 0 /* diagnostic build only (Makefile `diag`, tools/plugin_stamps.py): the single-record (plugin) launch
+                          stamps the shader clock at its phase boundaries into clk[0 .. 11] (clk[14], clk[15]: the 100 MHz
+                          counter at the first and last stamp).  Its run times are not quoted, only its phase shares. */
+#endif
 constexpr uint32_t SP_TAB = 65536; /* per-wave nibble tables, 8 KiB each */
+
+/* phase stamp k of the by-value record's wave (STAMP_PHASES builds; the stamp and its LDS drain in one statement) */
+__device__ __forceinline__ void phase_stamp(uint64_t *__restrict__ clk, bool on, int lane, int k)
+{
+#if STAMP_PHASES
+    if (on && clk != nullptr) {
+        uint64_t t;
+        __builtin_amdgcn_sched_barrier(0);
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+        __builtin_amdgcn_sched_barrier(0);
+        if (lane == 0)
+            clk[k] = t;
+        if (k == 0 || k == 11) {
+            const uint64_t r = __builtin_amdgcn_s_memrealtime();
+            __builtin_amdgcn_s_waitcnt(0xC07F);
+            if (lane == 0)
+                clk[k == 0 ? 14 : 15] = r;
+        }
+    }
+#else
+    (void)clk, (void)on, (void)lane, (void)k;
+#endif
+}
 
 /* the wave's LDS operations are processed in order: only the compiler must not move them across this */
 __device__ __forceinline__ void wave_lds_sync()
@@ -125,12 +153,16 @@ __global__ void __launch_bounds__(SPARSE_WG)
     const int lane = threadIdx.x & 63;
     const uint32_t lb_aes = (uint32_t)(lane & 31) * 4u; /* table base 0: byte 2 of the address is 0 */
     const uint32_t tab = __builtin_amdgcn_readfirstlane(SP_TAB + (uint32_t)(threadIdx.x >> 6) * 8192u); /* wave-uniform */
-    clock_stamp(clk, 0);
+    /* one record by value (recs_ord == nullptr), or build_chunks' chunks with their records contiguous from 0 */
+    const bool by_value = recs_ord == nullptr;
+    const bool stamps = STAMP_PHASES && by_value && blockIdx.x == 0 && threadIdx.x < 64;
+    phase_stamp(clk, stamps, lane, 0);
+    if (!STAMP_PHASES)
+        clock_stamp(clk, 0);
     if (!PLUGIN_PROBE)
         build_aes_tables<SPARSE_WG>(lds, 0, t0); /* the batch kernel's layout at offset 0 */
     __syncthreads();
-    /* one record by value (recs_ord == nullptr), or build_chunks' chunks with their records contiguous from 0 */
-    const bool by_value = recs_ord == nullptr;
+    phase_stamp(clk, stamps, lane, 1);
     uint32_t nrecs = 1;
     if (!by_value) {
         if (nchunks == 0)
@@ -177,6 +209,7 @@ __global__ void __launch_bounds__(SPARSE_WG)
         cc.k22 = __builtin_amdgcn_readfirstlane(cc.k22);
         cc.k23 = __builtin_amdgcn_readfirstlane(cc.k23);
         cc.r03 = __builtin_amdgcn_readfirstlane(cc.r03);
+        phase_stamp(clk, stamps, lane, 2);
         wave_lds_sync(); /* the previous record's Horner reads of the table are done */
         if (horner) { /* (loading the basis during the previous record's VALU combine measured no faster: other waves hide it) */
             if (!by_value)
@@ -184,6 +217,7 @@ __global__ void __launch_bounds__(SPARSE_WG)
             store_wave_table(lds, tab, b, lane);
         }
         wave_lds_sync();
+        phase_stamp(clk, stamps, lane, 3);
 
         V4 y = V4{0, 0, 0, 0}, ek0 = V4{0, 0, 0, 0};
         /* generic elements m .. m + NE - 1 of the lane (past `mend`: skipped): partial / AAD / length blocks and
@@ -249,6 +283,7 @@ __global__ void __launch_bounds__(SPARSE_WG)
         /* without a stretch the head and tail are one range: element pairs straddling pm0 share one round trip to the
          * record's memory (a single record read over PCIe by the plugin: one load latency instead of two) */
         generic_range(0, npure ? pm0 : iters);
+        phase_stamp(clk, stamps, lane, 4);
         if (npure) {
             const int c0 = 64 * pm0 + lane - na; /* the lane's first data block of the stretch */
             const uint8_t *src = in_p + 16 * (size_t)c0;
@@ -317,14 +352,17 @@ __global__ void __launch_bounds__(SPARSE_WG)
                     y = v4xor(gh_mul_nibble(lds, tab, y), pend[b]);
             }
         }
+        phase_stamp(clk, stamps, lane, 5);
         if (npure)
             generic_range(pm1, iters);
+        phase_stamp(clk, stamps, lane, 6);
 
         /* lane l's sum times H^(q+1), q = distance of its last element from the end of the GHASH input, on the
          * VALU; the XOR butterfly then sums the 64 lanes (ghash_combine) */
         const int q = (N - 1 - lane) & 63;
         if (SPARSE_ABLATE != 1)
             y = ghash_combine(bs, q, y);
+        phase_stamp(clk, stamps, lane, 7);
         if (q == 0) {
             const V4 tag = v4xor(y, ek0);
             if (OPEN) {
@@ -335,6 +373,7 @@ __global__ void __launch_bounds__(SPARSE_WG)
                 store_full(out_p + L, tag);
             }
         }
+        phase_stamp(clk, stamps, lane, 8);
         if (!OPEN && supp != nullptr) {
             /* QUIC header protection after the record (lib/fusion.c:636-650), as in aesgcm_batch_kernel: the
              * sample may cover the tag written by another lane of this wave */
@@ -353,11 +392,14 @@ __global__ void __launch_bounds__(SPARSE_WG)
     if (done != nullptr && w0 == 0) {
         /* the by-value record's wave: every store above (the whole wave's, s_waitcnt is wave-wide) reaches system
          * scope before the completion word does; a vector store (global memory, never the scalar cache) */
+        phase_stamp(clk, stamps, lane, 9);
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+        phase_stamp(clk, stamps, lane, 10);
         if (lane == 0)
             __hip_atomic_store(done, done_seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        phase_stamp(clk, stamps, lane, 11);
     }
-    if (clk != nullptr) { /* the workgroup's end: after its last wave */
+    if (!STAMP_PHASES && clk != nullptr) { /* the workgroup's end: after its last wave */
         __syncthreads();
         clock_stamp(clk, 1);
     }

@@ -85,9 +85,10 @@ def test_node_splits_one_batch_over_two_engines(oracle, transport, key_len):
         node.close()
 
 
-def test_partly_registered_input_falls_back_to_copy(engine, oracle):
-    """a buffer registered only in part must not go to the zero-copy transport (the kernel would touch
-    unmapped host pages over PCIe).  AUTO then takes the copy transport (bit-exact), MAPPED refuses with EINVAL."""
+def test_partly_registered_input_is_refused(engine, oracle):
+    """a buffer registered only in part must never reach the zero-copy transport (the kernel would touch
+    unmapped host pages over PCIe), and the copy engines refuse it too (hipMemcpyAsync: invalid argument): every
+    transport returns EINVAL before anything runs.  Registered over all its bytes, the same buffer goes zero-copy."""
     n = 64
     recs_in = [(*oracle.gen_key(5, 16), i, tls_aad(16000), oracle.gen_record(77000 + i, 16000)) for i in range(n)]
     recs, in_total, out_total, aad_total = ptls_hip.layout_records([16000] * n, [5] * n, [0] * n, np.arange(n), align=16,
@@ -97,32 +98,34 @@ def test_partly_registered_input_falls_back_to_copy(engine, oracle):
     page = 4096
     raw = np.zeros(in_total + 3 * page, dtype=np.uint8)
     off = (-raw.ctypes.data) % page
-    buf = raw[off: off + in_total + page]  # page-aligned view; only its first half gets registered
+    buf = raw[off: off + in_total + page]  # page-aligned view; first only half of it gets registered
     for r, rec in zip(recs_in, recs):
         buf[rec["in_off"]: rec["in_off"] + len(r[4])] = np.frombuffer(r[4], np.uint8)
     half = (in_total // 2) // page * page
+    h_aad = torch.zeros(aad_total + 16, dtype=torch.uint8).pin_memory()
+    for r, rec in zip(recs_in, recs):
+        h_aad.numpy()[rec["aad_off"]: rec["aad_off"] + 5] = np.frombuffer(r[3], np.uint8)
+    h_out = torch.zeros(out_total + 16, dtype=torch.uint8).pin_memory()
+    pipe = ptls_hip.Pipeline(engine, 1 << 20)
     assert ptls_hip.lib().ptls_hip_host_register(buf.ctypes.data, half) == 0, ptls_hip.last_error()
     try:
-        h_aad = torch.zeros(aad_total + 16, dtype=torch.uint8).pin_memory()
-        for r, rec in zip(recs_in, recs):
-            h_aad.numpy()[rec["aad_off"]: rec["aad_off"] + 5] = np.frombuffer(r[3], np.uint8)
-        h_out = torch.zeros(out_total + 16, dtype=torch.uint8).pin_memory()
-        pipe = ptls_hip.Pipeline(engine, 1 << 20, transport=ptls_hip.TRANSPORT_MAPPED)
-        with pytest.raises(ptls_hip.HipError, match="pinned or registered"):
-            pipe.seal(ks, recs, buf, h_aad, h_out)
+        for tr in (ptls_hip.TRANSPORT_MAPPED, ptls_hip.TRANSPORT_AUTO, ptls_hip.TRANSPORT_COPY):
+            pipe.set_transport(tr)
+            with pytest.raises(ptls_hip.HipError, match="registered only in part"):
+                pipe.seal(ks, recs, buf, h_aad, h_out)
+    finally:
+        ptls_hip.lib().ptls_hip_host_unregister(buf.ctypes.data)
+    assert ptls_hip.lib().ptls_hip_host_register(buf.ctypes.data, len(buf)) == 0, ptls_hip.last_error()
+    try:
         pipe.set_transport(ptls_hip.TRANSPORT_AUTO)
         pipe.seal(ks, recs, buf, h_aad, h_out)
-        assert pipe.last_transport == ptls_hip.TRANSPORT_COPY
+        assert pipe.last_transport == ptls_hip.TRANSPORT_MAPPED
         hout = h_out.numpy()
         for r, rec in zip(recs_in, recs):
             assert hout[rec["out_off"]: rec["out_off"] + len(r[4]) + 16].tobytes() == oracle.seal(*r)
-        # a fully pinned input still takes the zero-copy path
-        h_in = torch.from_numpy(buf[:in_total].copy()).pin_memory()
-        pipe.seal(ks, recs, h_in, h_aad, h_out)
-        assert pipe.last_transport == ptls_hip.TRANSPORT_MAPPED
-        pipe.close()
     finally:
         ptls_hip.lib().ptls_hip_host_unregister(buf.ctypes.data)
+        pipe.close()
         ks.close()
 
 
