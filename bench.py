@@ -672,6 +672,9 @@ def main():
                          "seal_ghz_min_max_over_workgroups": [round(min(c[0][1] for c in kclk), 3),
                                                               round(max(c[0][2] for c in kclk), 3)],
                          "seal_span_ms_100mhz": round(float(np.median([c[0][3] for c in kclk])), 3),
+                         "seal_mcycles_per_launch": round(seal_ghz * seal_ms, 2),
+                         "cycles_note": "clock x kernel time = the launch's length in shader cycles: the work measure that does "
+                                        "not move with the box's clock (MI355X_MICROARCH.md DVFS)",
                          "stamped_seal_open_ms": round(seal_ms + open_ms, 3),
                          "timed_loop_seal_open_ms": round(timed_seal_open_ms, 3),
                          "source": "s_memtime / s_memrealtime at each workgroup's start and end, in the launches "

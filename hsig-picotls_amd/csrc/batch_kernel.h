@@ -1207,8 +1207,11 @@ __global__ void __launch_bounds__(WGT)
             const int na = (A + 15) >> 4, nc = (L + 15) >> 4;
             const int N = valid ? na + nc + 1 : 0;
             const int i0 = (r + na) & (G - 1);
-            /* the elements [e_lo, e_hi) this task handles; the lane's are i0 + m G for m in [m_lo, m_hi) */
-            const int e_lo = is_part && part == 1 ? N - split_tail(N) : 0, e_hi = is_part && part == 0 ? N - split_tail(N) : N;
+            /* the elements [e_lo, e_hi) this task handles; the lane's are i0 + m G for m in [m_lo, m_hi).  A split task's
+             * part B is the last B elements of every record of the task, B from the task's shortest record (its last
+             * record group: the chunk is sorted longest first), so both parts stay even across the task's records */
+            const int bsplit = is_part ? split_tail(__builtin_amdgcn_readlane(N, 64 - G)) : 0;
+            const int e_lo = is_part && part == 1 ? N - bsplit : 0, e_hi = is_part && part == 0 ? N - bsplit : N;
             const int m_lo = e_lo > i0 ? ((e_lo - 1 - i0) >> LOG2G) + 1 : 0;
             const int my_iters = e_hi > i0 ? ((e_hi - 1 - i0) >> LOG2G) + 1 : 0;
 
@@ -1495,7 +1498,7 @@ __global__ void __launch_bounds__(WGT)
                         sp = V4{__shfl(s.w0, src, 64), __shfl(s.w1, src, 64), __shfl(s.w2, src, 64), __shfl(s.w3, src, 64)};
                     }
                     sp = mul_by_plane<G>(sp, reinterpret_cast<const uint4 *>(basis) + (size_t)ch.key * BASIS_VECS +
-                                                 split_plane(N) * 128, r);
+                                                 split_plane_of_tail(bsplit) * 128, r);
                 } else {
                     sp = v4xor(sp, ek0);
                 }
@@ -1503,12 +1506,13 @@ __global__ void __launch_bounds__(WGT)
                     const uint32_t sl = (sbase + (uint32_t)tt) * R + (uint32_t)grp;
                     lds128_store(lds, LDS_SPLIT + sl * 32u + (uint32_t)part * 16u, sp);
                     /* the other part's ciphertext (header protection samples it) and partial are visible once its
-                     * counter increment is: release / acquire around the LDS atomic */
-                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+                     * counter increment is: release / acquire around the LDS atomic, workgroup scope (both parts run in
+                     * this workgroup, on this CU; agent scope would write back and invalidate the XCD's L2) */
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
                     const uint32_t arrived = __hip_atomic_fetch_add(reinterpret_cast<uint32_t *>(lds + LDS_SPLIT_CTR) + sl, 1u,
                                                                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                     if (arrived == 1) {
-                        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
                         const V4 tag = v4xor(sp, lds128(lds, LDS_SPLIT + sl * 32u + (uint32_t)(1 - part) * 16u));
                         if (OPEN) {
                             const V4 rt = load_full(in_p + L);
@@ -1517,8 +1521,8 @@ __global__ void __launch_bounds__(WGT)
                         } else {
                             store_full(out_p + L, tag);
                             if (supp != nullptr) { /* header protection after the whole record, tag included */
-                                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-                                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
                                 const ptls_hip_supp_t sp2 = supp[rec_i];
                                 if ((sp2.flags & PTLS_HIP_SUPP_ENABLE) && sp2.hp_key < hp_nslots) {
                                     const V4 sample = load_full(out + sp2.sample_off);
@@ -1545,10 +1549,10 @@ __global__ void __launch_bounds__(WGT)
             if (!OPEN && supp != nullptr) {
                 /* QUIC header protection (fusion's supp, lib/fusion.c:636-650): AES-ECB(hp key, 16 output bytes)
                  * computed after the record, because the sample may cover the tag.  The sample was written by
-                 * other lanes of this wave: the agent-scope release/acquire pair completes their stores and
-                 * invalidates this CU's L1 before the read. */
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                 * other lanes of this wave: the release/acquire pair completes their stores before the read.  Workgroup
+                 * scope: one CU, one L1 (agent scope would write back and invalidate the XCD's whole L2). */
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
                 if (valid && r == 0) {
                     const ptls_hip_supp_t sp = supp[rec_i];
                     if ((sp.flags & PTLS_HIP_SUPP_ENABLE) && sp.hp_key < hp_nslots) {

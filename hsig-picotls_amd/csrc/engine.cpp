@@ -505,11 +505,13 @@ static void plan_splits(const ptls_hip_record_t *recs, const std::vector<uint32_
                 uint32_t ns = 0;
                 for (uint32_t t = 0; (t + 1) * R <= ch[c].count && ns < 255; ++t) {
                     const uint32_t p0 = ch[c].first + t * R;
+                    /* B from the task's shortest (last) record, as the kernel takes it; every record keeps a part A past its AAD */
+                    const int bsplit = split_tail(elems(p0 + R - 1));
                     bool ok = elems(p0) > limit && slots + R <= (uint32_t)SPLIT_SLOTS;
                     for (uint32_t k = 0; ok && k < R; ++k) {
                         const ptls_hip_record_t &r = recs[order[p0 + k]];
                         const int n = elems(p0 + k), na = (int)((r.aad_len + 15) / 16);
-                        ok = n >= SPLIT_MIN_N && n <= SPLIT_MAX_N && n - split_tail(n) > na;
+                        ok = n >= SPLIT_MIN_N && n <= SPLIT_MAX_N && n - bsplit > na;
                     }
                     if (!ok)
                         break;
@@ -1857,6 +1859,8 @@ static void plugin_wait(hipStream_t stream, const uint8_t *word_p, uint32_t seq)
     }
 }
 
+static unsigned staging_flags(void);
+
 /* ---- CTR cipher for header protection (replaces lib/fusion.c:1050-1100) ---------------------------- */
 
 struct hip_ctr_state {
@@ -1942,7 +1946,7 @@ static hip_ctr_state *ecb_state_new(const void *key, size_t key_size)
     }
     st->ks = ptls_hip_keyset_new(eng, key_size, 1);
     void *d_stage = nullptr;
-    const bool ok = st->ks != nullptr && hipHostMalloc(&st->h_stage, 128, hipHostMallocCoherent) == hipSuccess &&
+    const bool ok = st->ks != nullptr && hipHostMalloc(&st->h_stage, 128, staging_flags()) == hipSuccess &&
                     hipHostGetDevicePointer(&d_stage, st->h_stage, 0) == hipSuccess &&
                     ptls_hip_keyset_set(st->ks, 0, 1, key, nullptr, st->stream) == 0;
     st->d_stage = static_cast<uint8_t *>(d_stage);
@@ -2046,6 +2050,19 @@ static int aes256ctr_setup(ptls_cipher_context_t *ctx, int is_enc, const void *k
     return aesctr_setup(ctx, is_enc, key, PTLS_AES256_KEY_SIZE);
 }
 
+/* allocation flags of the plugin's pinned staging: fine-grained (coherent) by default, whatever HIP_HOST_COHERENT says:
+ * the kernel reads the record and writes its output and the completion word there, and the next call rewrites the same
+ * bytes from the CPU without a stream synchronize.  PTLS_HIP_PLUGIN_STAGING=default (environment; for latency A/B
+ * measurements) takes hipHostMallocDefault instead. */
+static unsigned staging_flags(void)
+{
+    static const unsigned f = [] {
+        const char *e = getenv("PTLS_HIP_PLUGIN_STAGING");
+        return e != nullptr && std::strcmp(e, "default") == 0 ? (unsigned)hipHostMallocDefault : (unsigned)hipHostMallocCoherent;
+    }();
+    return f;
+}
+
 static uint8_t *mapped_or_die(uint8_t *h)
 {
     void *d = nullptr;
@@ -2071,9 +2088,7 @@ static void state_reserve(hip_aead_state *st, size_t len, size_t aadlen)
         plugin_check(hipHostFree(st->h_io), "hipHostFree");
     }
     st->h_io = nullptr;
-    /* fine-grained (coherent) whatever HIP_HOST_COHERENT says: the kernel reads the record and writes its output and the
-     * completion word there, and the next call rewrites the same bytes from the CPU without a stream synchronize */
-    plugin_check(hipHostMalloc(&st->h_io, cap + (cap + 16) + aad_cap, hipHostMallocCoherent), "hipHostMalloc(staging)");
+    plugin_check(hipHostMalloc(&st->h_io, cap + (cap + 16) + aad_cap, staging_flags()), "hipHostMalloc(staging)");
     st->d_io = mapped_or_die(st->h_io);
     st->cap = cap;
     st->aad_cap = aad_cap;
@@ -2310,7 +2325,7 @@ static hip_aead_state *state_new(const void *key, const void *iv, size_t key_siz
     }
     st->ks = ptls_hip_keyset_new(eng, key_size, 1);
     void *d_stage = nullptr;
-    bool ok = st->ks != nullptr && hipHostMalloc(&st->h_stage, 256, hipHostMallocCoherent) == hipSuccess &&
+    bool ok = st->ks != nullptr && hipHostMalloc(&st->h_stage, 256, staging_flags()) == hipSuccess &&
               hipHostGetDevicePointer(&d_stage, st->h_stage, 0) == hipSuccess &&
               ptls_hip_keyset_set(st->ks, 0, 1, key, iv, st->stream) == 0;
     if (!ok) {

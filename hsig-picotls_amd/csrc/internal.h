@@ -53,7 +53,7 @@ constexpr int WG_MAX = 1024;
 
 /* Split records (G >= 16, DESIGN.md §4.1 "split tasks"; planned in engine.cpp plan_splits): the planner may deal a key run's longest tasks as two part
  * tasks each, part A = GHASH elements [0, N - B) of the task's records, part B = [N - B, N), B = split_tail(N) a power
- * of two near N / 2.  Part A multiplies its partial GHASH by H^B (basis plane log2 B), each part leaves its partial in
+ * of two near N / 2 of the task's shortest record.  Part A multiplies its partial GHASH by H^B (basis plane log2 B), each part leaves its partial in
  * an LDS slot of the workgroup, and the part that finishes second XORs them into the tag.  The slots sit after the
  * tables and the task counter: SPLIT_SLOTS records of {partial A, partial B} (32 B) + a 4-byte arrival counter. */
 constexpr int SPLIT_SLOTS = 192;
@@ -63,9 +63,9 @@ constexpr int split_tail(int N)
 {
     return N >= 768 ? 512 : N >= 384 ? 256 : 128;
 }
-constexpr int split_plane(int N)
+constexpr int split_plane_of_tail(int B)
 {
-    return N >= 768 ? 9 : N >= 384 ? 8 : 7;
+    return B == 512 ? 9 : B == 256 ? 8 : 7;
 }
 
 struct KeySlot {

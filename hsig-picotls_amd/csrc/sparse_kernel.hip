@@ -377,8 +377,8 @@ __global__ void __launch_bounds__(SPARSE_WG)
         if (!OPEN && supp != nullptr) {
             /* QUIC header protection after the record (lib/fusion.c:636-650), as in aesgcm_batch_kernel: the
              * sample may cover the tag written by another lane of this wave */
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
             if (lane == 0) {
                 const ptls_hip_supp_t sp = supp[rec_i];
                 if ((sp.flags & PTLS_HIP_SUPP_ENABLE) && sp.hp_key < hp_nslots) {
