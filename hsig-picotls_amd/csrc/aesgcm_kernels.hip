@@ -78,6 +78,35 @@ __global__ void __launch_bounds__(256) aesecb_batch_kernel(const ptls_hip_supp_t
 }
 
 
+/* One AES-ECB block for the plugin's CTR / ECB objects (ptls_hip_aesecb_encrypt, the CTR cipher's do_init): the input
+ * block travels in the kernel arguments (no dependent read of host staging over PCIe), one wave builds only lane slot
+ * 0 of the T-tables (256 rows x {T0, T2}: every lane then reads the same slot, a broadcast), computes the block and
+ * stores it into the pinned staging, then the completion word the host spins on (system scope, after the block). */
+template <int ROUNDS>
+__global__ void __launch_bounds__(64) aesecb_one_kernel(uint4 blk, const KeySlot *__restrict__ slot, const uint32_t *__restrict__ t0,
+                                                        uint8_t *out, uint32_t *done, uint32_t done_seq)
+{
+    __shared__ __attribute__((aligned(16))) uint8_t lds[65536];
+    const int lane = threadIdx.x;
+    uint32_t t[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+        t[k] = t0[4 * lane + k];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const uint32_t row = (uint32_t)(4 * lane + k) * 256u;
+        *reinterpret_cast<uint32_t *>(lds + row) = t[k];
+        *reinterpret_cast<uint32_t *>(lds + row + 128) = (t[k] << 16) | (t[k] >> 16);
+    }
+    __syncthreads();
+    const V4 m = aes_encrypt<ROUNDS>(lds, 0u, slot->rk, V4{blk.x, blk.y, blk.z, blk.w});
+    if (lane == 0) {
+        store_full(out, m);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+        __hip_atomic_store(done, done_seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+
 #ifndef KEYSETUP_WIDE_MAX
 #define KEYSETUP_WIDE_MAX 4096 /* slots up to which key setup runs one wave per slot (keysetup_wide_kernel) */
 #endif
@@ -400,6 +429,19 @@ int launch_tls13_headers(const ptls_hip_record_t *recs, uint32_t n, uint8_t *hdr
 int launch_tls13_inner(const ptls_hip_record_t *recs, uint32_t n, const uint8_t *out, uint64_t *result, unsigned grid, void *stream)
 {
     hipLaunchKernelGGL(tls13_inner_kernel, dim3(grid), dim3(256), 0, static_cast<hipStream_t>(stream), recs, n, out, result);
+    return (int)hipGetLastError();
+}
+
+int launch_aesecb_one(int rounds, const uint8_t *blk, const KeySlot *slot, const uint32_t *t0, uint8_t *out, uint32_t *done,
+                      uint32_t done_seq, void *stream)
+{
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    uint4 b;
+    __builtin_memcpy(&b, blk, 16);
+    if (rounds == 10)
+        hipLaunchKernelGGL(aesecb_one_kernel<10>, dim3(1), dim3(64), 0, s, b, slot, t0, out, done, done_seq);
+    else
+        hipLaunchKernelGGL(aesecb_one_kernel<14>, dim3(1), dim3(64), 0, s, b, slot, t0, out, done, done_seq);
     return (int)hipGetLastError();
 }
 

@@ -82,9 +82,6 @@ __host__ __device__ constexpr uint32_t lds_bytes(int log2g)
                            * 2 (with DYN_DEAL=0) = key switches after the first neither wait nor rebuild; 3 = the same with
                            * dynamic dealing running on across keys */
 #endif
-#ifndef SPLIT_TASKS
-#define SPLIT_TASKS 1 /* G >= 16: the planner may deal a key run's longest tasks as two part tasks (split records) */
-#endif
 #ifndef DEAL_MUTANT
 #define DEAL_MUTANT 0 /* TEST-ONLY broken builds (tools/build_mutants.sh, tests/test_gpu_dealing.py): 1 = the task a wave
                          drew past one chunk is dropped at the next chunk of the key run, 2 = cbase is not advanced */
@@ -1073,13 +1070,14 @@ __device__ __forceinline__ Elem elem_of(int i, int N, int na, int nc, int L, int
     return e;
 }
 
-template <bool OPEN, bool ALIGNED>
+/* AAD_IN: an AAD element's block is already in in_blk (loaded before the AES, sparse kernel) */
+template <bool OPEN, bool ALIGNED, bool AAD_IN = false>
 __device__ __forceinline__ V4 finish_elem(const Elem &e, V4 in_blk, V4 ks, const uint8_t *aad_p, int A, int L, uint8_t *out_p,
                                           V4 &ek0)
 {
     V4 x = V4{0, 0, 0, 0};
     if (e.is_aad) {
-        x = load_block<ALIGNED>(aad_p + 16 * e.i, min(16, A - 16 * e.i));
+        x = AAD_IN ? in_blk : load_block<ALIGNED>(aad_p + 16 * e.i, min(16, A - 16 * e.i));
     } else if (e.is_c) {
         const V4 o = v4xor(in_blk, ks);
         if (OPEN) {

@@ -596,7 +596,7 @@ static void build_chunks(const ptls_hip_record_t *recs, size_t n, int lanes, uns
         all_aligned = all_aligned && (c.flags & 1u);
         ch.push_back(c);
     }
-    if (lanes >= 16)
+    if (SPLIT_TASKS && lanes >= 16)
         plan_splits(recs, order, ch, lanes);
 }
 
@@ -1888,26 +1888,24 @@ static const hip_ctr_state *ctr_state_of(const ptls_cipher_context_t *c)
     return reinterpret_cast<const hip_ctr_context *>(c)->st;
 }
 
-/* ECB staging (128 B pinned): supp descriptor @0, input block @32, output block @48, completion word @64 */
+/* ECB staging (128 B pinned): output block @48, completion word @64 (the input block travels in the kernel arguments) */
 static const size_t ECB_DONE = 64;
 
 /* one AES-ECB block on the device with the state's key (fusion: aesecb_encrypt, lib/fusion.c:322-334) */
 static void ecb_block(hip_ctr_state *st, const void *src, uint8_t dst[16])
 {
     DeviceGuard g(st->eng->device);
-    const ptls_hip_supp_t sp{32, 48, 0, PTLS_HIP_SUPP_ENABLE};
-    std::memcpy(st->h_stage, &sp, sizeof(sp));
-    std::memcpy(st->h_stage + 32, src, 16);
-    const int e = launch_aesecb(st->ks->key_size == 16 ? 10 : 14, reinterpret_cast<const ptls_hip_supp_t *>(st->d_stage), 1,
-                                st->d_stage, st->d_stage, st->ks->d_slots, 1, st->eng->d_t0, 1, st->stream,
-                                reinterpret_cast<uint32_t *>(st->d_stage + ECB_DONE), ++st->done_seq);
+    /* the block goes in the kernel arguments; the result comes back through the pinned staging (@48) */
+    const int e = launch_aesecb_one(st->ks->key_size == 16 ? 10 : 14, static_cast<const uint8_t *>(src), st->ks->d_slots,
+                                    st->eng->d_t0, st->d_stage + 48, reinterpret_cast<uint32_t *>(st->d_stage + ECB_DONE),
+                                    ++st->done_seq, st->stream);
     if (e != 0) {
         g_err = hipGetErrorString((hipError_t)e);
         plugin_die("ecb launch");
     }
     plugin_wait(st->stream, st->h_stage + ECB_DONE, st->done_seq);
     std::memcpy(dst, st->h_stage + 48, 16);
-    std::memset(st->h_stage + 32, 0, 32);
+    std::memset(st->h_stage + 48, 0, 16);
 }
 
 /* do_init: the keystream block AES-ECB(key, iv) on the device (fusion: aesecb_encrypt, :1057-1062) */

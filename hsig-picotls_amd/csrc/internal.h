@@ -3,7 +3,7 @@
  *
  * HBM layout:
  *   key slots    KeySlot[nslots]             512 B each: round keys, static IV, H powers
- *   GHASH basis  uint4[nslots][BASIS_VECS]   21 KiB per slot: P * x^e for P in {H, H^2, ..., H^512}, then H^1..H^64
+ *   GHASH basis  uint4[nslots][BASIS_VECS]   15 KiB per slot: P * x^e for P in {H, H^2, ..., H^64}, then H^1..H^64
  *                                            (HYBRID builds: then the bit-sliced round keys, bs8_aes.h)
  *   records      ptls_hip_record_t[n]        48 B descriptors (caller's order)
  *   chunks       Chunk[nchunks]              runs of <= CHUNK_RECS records sharing one key slot
@@ -25,10 +25,18 @@
 #endif
 #endif
 
+/* SPLIT_TASKS (measurement switch, DESIGN.md §4.7 "split records"; off in the product): at 16 and 32 lanes per record the
+ * planner deals a key run's longest wave tasks as two part tasks each.  Bit-exact (TEST-ONLY alternate build
+ * alt/libptls_hip_split.so, tests/test_gpu_split.py), but configs[3] loses 2-5 % with it, so off. */
+#ifndef SPLIT_TASKS
+#define SPLIT_TASKS 0
+#endif
+
 namespace ptls_hip {
 
-constexpr int NPOW = 10; /* H^1 .. H^16 (batch kernel main and tree tables), H^32 (batch kernel main table at G = 32), H^64
-                            (sparse kernel), H^128 .. H^512 (the shift of a split record's first part, batch_kernel.h) */
+constexpr int NPOW = SPLIT_TASKS ? 10 : 7; /* H^1 .. H^16 (batch kernel main and tree tables), H^32 (batch kernel main table
+                                              at G = 32), H^64 (sparse kernel); SPLIT_TASKS: H^128 .. H^512 (the shift of a
+                                              split record's first part, batch_kernel.h) */
 /* GHASH basis slot: NPOW x 128 vectors P * x^e, then H^1 .. H^64 (the sparse kernel's per-lane final powers) */
 constexpr int LANE_POWS = 64;
 /* HYBRID (measurement switch): this many waves per batch-kernel workgroup (the last ones) run their
@@ -40,7 +48,7 @@ constexpr int LANE_POWS = 64;
 /* with HYBRID, the slot also holds the bit-sliced round keys 1..rounds (bs8::slice_key: 32 words per round) */
 constexpr int BS_KEY_OFF = NPOW * 128 + LANE_POWS; /* uint4 offset in the slot */
 constexpr int BS_KEY_VECS = HYBRID ? 14 * 32 / 4 : 0;
-constexpr int BASIS_VECS = BS_KEY_OFF + BS_KEY_VECS; /* uint4 per key slot (21 KiB; 22.75 KiB with HYBRID) */
+constexpr int BASIS_VECS = BS_KEY_OFF + BS_KEY_VECS; /* uint4 per key slot (15 KiB; 16.75 KiB with HYBRID, 21 KiB with SPLIT_TASKS) */
 constexpr int MAX_LANES = 32;    /* lanes per record (G) of the batch kernel: 1, 2, 4, 8, 16, 32 */
 constexpr int SPARSE_LANES = 64; /* "lanes" value of the wave-per-record kernel (sparse_kernel.hip) */
 /* the planner picks that kernel when a batch's key runs hold fewer records than this on average */
@@ -135,6 +143,8 @@ int launch_keysetup(KeySlot *slots, uint32_t *basis, const uint8_t *keys, const 
 int launch_aesecb(int rounds, const ptls_hip_supp_t *supp, uint32_t n, const uint8_t *src, uint8_t *mask, const KeySlot *hp_slots,
                   uint32_t hp_nslots, const uint32_t *t0, unsigned grid, void *stream,
                   uint32_t *done = nullptr, uint32_t done_seq = 0);
+int launch_aesecb_one(int rounds, const uint8_t *blk, const KeySlot *slot, const uint32_t *t0, uint8_t *out, uint32_t *done,
+                      uint32_t done_seq, void *stream);
 int launch_tls13_headers(const ptls_hip_record_t *recs, uint32_t n, uint8_t *hdr, unsigned grid, void *stream);
 int launch_tls13_inner(const ptls_hip_record_t *recs, uint32_t n, const uint8_t *out, uint64_t *result, unsigned grid, void *stream);
 int launch_derive_traffic_keys(const uint8_t *secrets_in, uint8_t *secrets_out, uint32_t count, int hash_size, int key_size,

@@ -43,6 +43,9 @@ namespace ptls_hip {
 #ifndef SPARSE_PE
 #define SPARSE_PE 2 /* GHASH elements (AES blocks) per lane per main-loop iteration */
 #endif
+#ifndef BV_PREFETCH
+#define BV_PREFETCH 1 /* the single-record launch reads its first elements and touches its key material before the table build */
+#endif
 #ifndef STAMP_PHASES
 #define STAMP_PHASES 0 /* diagnostic build only (Makefile `diag`, tools/plugin_stamps.py): the single-record (plugin) launch
                           stamps the shader clock at its phase boundaries into clk[0 .. 11] (clk[14], clk[15]: the 100 MHz
@@ -139,8 +142,12 @@ __device__ __forceinline__ V4 ghash_combine(const uint4 *__restrict__ bs, int q,
     return z;
 }
 
-template <int ROUNDS, bool OPEN, bool ALIGNED>
-__global__ void __launch_bounds__(SPARSE_WG)
+/* BYVAL: the plugin's single-record launch (the record by value in the kernel arguments, recs_ord == nullptr); its own
+ * instantiation, so the batch one carries none of its prefetch registers.  It runs 256 threads (one wave per SIMD, the
+ * whole register file: no spills) since only wave 0 works on the record; the others help build the AES tables. */
+constexpr int BYVAL_WG = 256;
+template <int ROUNDS, bool OPEN, bool ALIGNED, bool BYVAL, int WG = BYVAL ? BYVAL_WG : SPARSE_WG>
+__global__ void __launch_bounds__(WG)
     aesgcm_sparse_kernel(const ptls_hip_record_t *__restrict__ recs_ord, const uint32_t *__restrict__ order,
                          const Chunk *__restrict__ chunks, uint32_t nchunks, const uint8_t *in, const uint8_t *__restrict__ aad,
                          uint8_t *out, uint64_t *__restrict__ result, const KeySlot *__restrict__ slots,
@@ -148,20 +155,43 @@ __global__ void __launch_bounds__(SPARSE_WG)
                          const KeySlot *__restrict__ hp_slots, uint32_t hp_nslots, uint8_t *mask, ptls_hip_record_t one,
                          uint32_t *done, uint32_t done_seq, uint64_t *__restrict__ clk)
 {
-    __shared__ __attribute__((aligned(16))) uint8_t lds[SP_TAB + (SPARSE_WG / 64) * 8192];
-    static_assert(SP_TAB + (SPARSE_WG / 64) * 8192 <= 163840, "AES tables + per-wave GHASH tables must fit the CU's 160 KiB");
+    __shared__ __attribute__((aligned(16))) uint8_t lds[SP_TAB + (WG / 64) * 8192];
+    static_assert(SP_TAB + (WG / 64) * 8192 <= 163840, "AES tables + per-wave GHASH tables must fit the CU's 160 KiB");
     const int lane = threadIdx.x & 63;
     const uint32_t lb_aes = (uint32_t)(lane & 31) * 4u; /* table base 0: byte 2 of the address is 0 */
     const uint32_t tab = __builtin_amdgcn_readfirstlane(SP_TAB + (uint32_t)(threadIdx.x >> 6) * 8192u); /* wave-uniform */
     /* one record by value (recs_ord == nullptr), or build_chunks' chunks with their records contiguous from 0 */
-    const bool by_value = recs_ord == nullptr;
+    constexpr bool by_value = BYVAL;
     const bool stamps = STAMP_PHASES && by_value && blockIdx.x == 0 && threadIdx.x < 64;
     phase_stamp(clk, stamps, lane, 0);
     if (!STAMP_PHASES)
         clock_stamp(clk, 0);
+    /* A single record (the plugin's launch, wave 0 of the one workgroup) reads its first two elements per lane (the
+     * AAD block or the data block, whole 16 bytes: the plugin's own pinned staging holds them) and touches its key slot
+     * and its lane's final power before the AES tables are built, so those PCIe / HBM latencies run under the build
+     * instead of after it (tools/plugin_stamps.py).  pre[m] = element lane + 64 m. */
+    V4 pre[2] = {V4{0, 0, 0, 0}, V4{0, 0, 0, 0}};
+    V4 touch = V4{0, 0, 0, 0};
+    const bool prefetch = BV_PREFETCH && by_value && blockIdx.x == 0 && threadIdx.x < 64;
+    if (prefetch) {
+        const int na1 = ((int)one.aad_len + 15) >> 4, nc1 = ((int)one.len + 15) >> 4;
+#pragma unroll
+        for (int m = 0; m < 2; ++m) {
+            const int i = lane + 64 * m;
+            if (i < na1)
+                pre[m] = load_full(aad + one.aad_off + 16 * (size_t)i);
+            else if (i < na1 + nc1)
+                pre[m] = load_full(in + one.in_off + 16 * (size_t)(i - na1));
+        }
+        const uint4 *bsk = reinterpret_cast<const uint4 *>(basis) + (size_t)one.key * BASIS_VECS;
+        const uint4 kv = reinterpret_cast<const uint4 *>(slots + one.key)[lane & 15];       /* round keys, IV: 256 B */
+        const uint4 pv = bsk[NPOW * 128 + ((na1 + nc1 - lane) & 63)];                        /* H^(q+1) of the combine */
+        touch = V4{kv.x ^ pv.x, kv.y ^ pv.y, kv.z ^ pv.z, kv.w ^ pv.w};
+    }
     if (!PLUGIN_PROBE)
-        build_aes_tables<SPARSE_WG>(lds, 0, t0); /* the batch kernel's layout at offset 0 */
+        build_aes_tables<WG>(lds, 0, t0); /* the batch kernel's layout at offset 0 */
     __syncthreads();
+    asm volatile("" ::"v"(touch.w0), "v"(touch.w1), "v"(touch.w2), "v"(touch.w3)); /* keep the touch loads */
     phase_stamp(clk, stamps, lane, 1);
     uint32_t nrecs = 1;
     if (!by_value) {
@@ -170,8 +200,8 @@ __global__ void __launch_bounds__(SPARSE_WG)
         const Chunk last = chunks[nchunks - 1];
         nrecs = last.first + last.count;
     }
-    const uint32_t waves = gridDim.x * (SPARSE_WG / 64);
-    const uint32_t w0 = __builtin_amdgcn_readfirstlane(blockIdx.x * (SPARSE_WG / 64) + (threadIdx.x >> 6));
+    const uint32_t waves = gridDim.x * (WG / 64);
+    const uint32_t w0 = __builtin_amdgcn_readfirstlane(blockIdx.x * (WG / 64) + (threadIdx.x >> 6));
 
     for (uint32_t pos = w0; pos < nrecs; pos += waves) {
         const ptls_hip_record_t rec = by_value ? one : recs_ord[pos];
@@ -222,8 +252,9 @@ __global__ void __launch_bounds__(SPARSE_WG)
         V4 y = V4{0, 0, 0, 0}, ek0 = V4{0, 0, 0, 0};
         /* generic elements m .. m + NE - 1 of the lane (past `mend`: skipped): partial / AAD / length blocks and
          * counters >= 2^16, their AES blocks interleaved (counter-mode shortcut unless a counter is that large) */
-        auto generic = [&](auto ne_tag, int m, int mend) __attribute__((always_inline)) {
+        auto generic = [&](auto ne_tag, auto pre_tag, int m, int mend) __attribute__((always_inline)) {
             constexpr int NE = decltype(ne_tag)::value;
+            constexpr bool USE_PRE = decltype(pre_tag)::value; /* the head range only: pre is dead after it */
             Elem e[NE];
             V4 inb[NE], ks[NE];
             uint32_t cw[NE];
@@ -232,11 +263,18 @@ __global__ void __launch_bounds__(SPARSE_WG)
             for (int b = 0; b < NE; ++b) {
                 e[b] = elem_of(m + b < mend ? lane + (m + b) * 64 : N, N, na, nc, L, N);
                 inb[b] = V4{0, 0, 0, 0};
+                /* the lane's first two elements of a single record were read at the start (pre) */
+                const bool have_pre = USE_PRE && prefetch && m + b < 2;
+                const V4 pv = m + b == 0 ? pre[0] : pre[1];
                 if (e[b].is_c) {
                     const bool tb = tflag && e[b].c == nc - 1; /* the block holding the content-type byte */
-                    inb[b] = load_block<ALIGNED>(in_p + 16 * (size_t)e[b].c, e[b].nbytes - (tb ? 1 : 0));
+                    const int nb = e[b].nbytes - (tb ? 1 : 0);
+                    inb[b] = have_pre ? mask_block(pv, nb) : load_block<ALIGNED>(in_p + 16 * (size_t)e[b].c, nb);
                     if (tb)
                         inb[b] = put_byte(inb[b], e[b].nbytes - 1, ttype);
+                } else if (e[b].is_aad) { /* loaded before the AES as well, not after it in finish_elem */
+                    const int nb = min(16, A - 16 * e[b].i);
+                    inb[b] = have_pre ? mask_block(pv, nb) : load_block<ALIGNED>(aad_p + 16 * e[b].i, nb);
                 }
                 /* keystream for data block c (counter inc32(J0) + c), E_K(J0) for the length-block lane */
                 cw[b] = e[b].is_c ? bswap32((uint32_t)e[b].c + 2u) : 0x01000000u;
@@ -254,19 +292,19 @@ __global__ void __launch_bounds__(SPARSE_WG)
             }
 #pragma unroll
             for (int b = 0; b < NE; ++b) {
-                const V4 x = finish_elem<OPEN, ALIGNED>(e[b], inb[b], ks[b], aad_p, A, L, out_p, ek0);
+                const V4 x = finish_elem<OPEN, ALIGNED, true>(e[b], inb[b], ks[b], aad_p, A, L, out_p, ek0);
                 if (m + b == 0)
                     y = x; /* 0 * P ^ x */
                 else if (SPARSE_ABLATE != 2 && e[b].active)
                     y = v4xor(gh_mul_nibble(lds, tab, y), x); /* y * H^64 ^ x */
             }
         };
-        auto generic_range = [&](int m0, int m1) __attribute__((always_inline)) {
+        auto generic_range = [&](auto pre_tag, int m0, int m1) __attribute__((always_inline)) {
             int m = m0;
             for (; m + 1 < m1; m += 2)
-                generic(std::integral_constant<int, 2>{}, m, m1);
+                generic(std::integral_constant<int, 2>{}, pre_tag, m, m1);
             if (m < m1)
-                generic(std::integral_constant<int, 1>{}, m, m1);
+                generic(std::integral_constant<int, 1>{}, pre_tag, m, m1);
         };
 
         /* the wave's "pure" elements m in [pm0, pm1): every lane's element is a full data block with a counter below
@@ -282,7 +320,7 @@ __global__ void __launch_bounds__(SPARSE_WG)
         const int pm1 = pm0 + npure * KP;
         /* without a stretch the head and tail are one range: element pairs straddling pm0 share one round trip to the
          * record's memory (a single record read over PCIe by the plugin: one load latency instead of two) */
-        generic_range(0, npure ? pm0 : iters);
+        generic_range(std::integral_constant<bool, BYVAL>{}, 0, npure ? pm0 : iters);
         phase_stamp(clk, stamps, lane, 4);
         if (npure) {
             const int c0 = 64 * pm0 + lane - na; /* the lane's first data block of the stretch */
@@ -354,7 +392,7 @@ __global__ void __launch_bounds__(SPARSE_WG)
         }
         phase_stamp(clk, stamps, lane, 5);
         if (npure)
-            generic_range(pm1, iters);
+            generic_range(std::false_type{}, pm1, iters);
         phase_stamp(clk, stamps, lane, 6);
 
         /* lane l's sum times H^(q+1), q = distance of its last element from the end of the GHASH input, on the
@@ -405,16 +443,24 @@ __global__ void __launch_bounds__(SPARSE_WG)
     }
 }
 
+template <int R, bool O, bool BV>
+static hipError_t launch_sparse_bv(unsigned grid, hipStream_t s, const KernelArgs &a, bool aligned)
+{
+    if (aligned)
+        hipLaunchKernelGGL((aesgcm_sparse_kernel<R, O, true, BV>), dim3(grid), dim3(BV ? BYVAL_WG : SPARSE_WG), 0, s, a.recs_ord, a.order, a.chunks,
+                           a.nchunks, a.in, a.aad, a.out, a.result, a.slots, a.basis, a.t0, a.supp, a.hp_slots, a.hp_nslots, a.mask, a.one,
+                           a.done, a.done_seq, a.clk);
+    else
+        hipLaunchKernelGGL((aesgcm_sparse_kernel<R, O, false, BV>), dim3(grid), dim3(BV ? BYVAL_WG : SPARSE_WG), 0, s, a.recs_ord, a.order, a.chunks,
+                           a.nchunks, a.in, a.aad, a.out, a.result, a.slots, a.basis, a.t0, a.supp, a.hp_slots, a.hp_nslots, a.mask, a.one,
+                           a.done, a.done_seq, a.clk);
+    return hipGetLastError();
+}
+
 template <int R, bool O>
 static hipError_t launch_sparse_one(unsigned grid, hipStream_t s, const KernelArgs &a, bool aligned)
 {
-    if (aligned)
-        hipLaunchKernelGGL((aesgcm_sparse_kernel<R, O, true>), dim3(grid), dim3(SPARSE_WG), 0, s, a.recs_ord, a.order, a.chunks,
-                           a.nchunks, a.in, a.aad, a.out, a.result, a.slots, a.basis, a.t0, a.supp, a.hp_slots, a.hp_nslots, a.mask, a.one, a.done, a.done_seq, a.clk);
-    else
-        hipLaunchKernelGGL((aesgcm_sparse_kernel<R, O, false>), dim3(grid), dim3(SPARSE_WG), 0, s, a.recs_ord, a.order, a.chunks,
-                           a.nchunks, a.in, a.aad, a.out, a.result, a.slots, a.basis, a.t0, a.supp, a.hp_slots, a.hp_nslots, a.mask, a.one, a.done, a.done_seq, a.clk);
-    return hipGetLastError();
+    return a.recs_ord == nullptr ? launch_sparse_bv<R, O, true>(grid, s, a, aligned) : launch_sparse_bv<R, O, false>(grid, s, a, aligned);
 }
 
 int launch_batch_sparse(int rounds, bool open, unsigned grid, void *stream, const KernelArgs &a, bool aligned)
