@@ -53,6 +53,30 @@ namespace ptls_hip {
 #endif
 constexpr uint32_t SP_TAB = 65536; /* per-wave nibble tables, 8 KiB each */
 
+/* batch launches (STAMP_PHASES builds): wave 0 of workgroup 0 sums the cycles of phases 2 .. 8 over its records */
+struct PhaseAcc {
+    uint64_t last, acc[9], n;
+};
+
+__device__ __forceinline__ void phase_acc(PhaseAcc &pa, bool on, int k)
+{
+#if STAMP_PHASES
+    if (on) {
+        uint64_t t;
+        __builtin_amdgcn_sched_barrier(0);
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+        __builtin_amdgcn_sched_barrier(0);
+        if (k > 1)
+            pa.acc[k] += t - pa.last;
+        else
+            ++pa.n;
+        pa.last = t;
+    }
+#else
+    (void)pa, (void)on, (void)k;
+#endif
+}
+
 /* phase stamp k of the by-value record's wave (STAMP_PHASES builds; the stamp and its LDS drain in one statement) */
 __device__ __forceinline__ void phase_stamp(uint64_t *__restrict__ clk, bool on, int lane, int k)
 {
@@ -88,19 +112,41 @@ __device__ __forceinline__ void wave_lds_sync()
  * laid out as gh_mul_nibble reads it: entry [p = 8w + j][v] = v at bits 4j..4j+3 of raw word w, times P.
  * Lane l writes position l/2, values 8(l&1) .. 8(l&1) + 7: load_wave_basis fetches the lane's four basis
  * vectors (issued early to hide their latency), store_wave_table writes the eight combinations. */
+#ifndef SPARSE_DERIVE
+#define SPARSE_DERIVE 1 /* 1: each lane loads ONE basis vector and derives the other three by multiplying by x (VALU): a
+                           quarter of the per-record basis reads (c4s: 4 KiB -> 1 KiB per record); 0: four loads */
+#endif
+
+/* v * x in GF(2^128), GCM bit order, raw byte order words: the 128-bit big-endian string shifted right by one bit,
+ * R = 0xE1 || 0^120 folded in when the last bit drops out (SP 800-38D) */
+__device__ __forceinline__ V4 mulx_raw(V4 v)
+{
+    const uint32_t a0 = bswap32(v.w0), a1 = bswap32(v.w1), a2 = bswap32(v.w2), a3 = bswap32(v.w3);
+    const uint32_t c = 0u - (a3 & 1u);
+    return V4{bswap32((a0 >> 1) ^ (c & 0xe1000000u)), bswap32(__builtin_amdgcn_alignbit(a0, a1, 1)),
+              bswap32(__builtin_amdgcn_alignbit(a1, a2, 1)), bswap32(__builtin_amdgcn_alignbit(a2, a3, 1))};
+}
+
 __device__ __forceinline__ void load_wave_basis(const uint4 *__restrict__ bp, int lane, V4 (&b)[4])
 {
     const int p = lane >> 1, w = p >> 3, j = p & 7;
+    /* the lane's four vectors are P x^(e0), P x^(e0 - 1), P x^(e0 - 2), P x^(e0 - 3) for one e0 (bits 4j .. 4j + 3 of
+     * word w lie in one byte): SPARSE_DERIVE loads the last and store_wave_table derives the others */
 #pragma unroll
-    for (int t = 0; t < 4; ++t) {
+    for (int t = SPARSE_DERIVE ? 3 : 0; t < 4; ++t) {
         const int u = 4 * j + t; /* bit u of little-endian word w = raw byte 4w + u/8, bit u%8 */
         const uint4 v = bp[8 * (4 * w + (u >> 3)) + 7 - (u & 7)];
         b[t] = V4{v.x, v.y, v.z, v.w};
     }
 }
 
-__device__ __forceinline__ void store_wave_table(uint8_t *lds, uint32_t tab, const V4 (&b)[4], int lane)
+__device__ __forceinline__ void store_wave_table(uint8_t *lds, uint32_t tab, V4 (&b)[4], int lane)
 {
+    if (SPARSE_DERIVE) {
+        b[2] = mulx_raw(b[3]);
+        b[1] = mulx_raw(b[2]);
+        b[0] = mulx_raw(b[1]);
+    }
     const int p = lane >> 1;
     const V4 hi = (lane & 1) ? b[3] : V4{0, 0, 0, 0};
     const uint32_t row = tab + (uint32_t)p * 256u + (uint32_t)(lane & 1) * 128u;
@@ -163,6 +209,16 @@ __global__ void __launch_bounds__(WG)
     /* one record by value (recs_ord == nullptr), or build_chunks' chunks with their records contiguous from 0 */
     constexpr bool by_value = BYVAL;
     const bool stamps = STAMP_PHASES && by_value && blockIdx.x == 0 && threadIdx.x < 64;
+    const bool bstamps = STAMP_PHASES && !by_value && blockIdx.x == 0 && threadIdx.x < 64;
+    PhaseAcc pa{};
+    uint64_t r_begin = 0, t_begin = 0;
+    (void)r_begin, (void)t_begin;
+#if STAMP_PHASES
+    if (bstamps) {
+        r_begin = __builtin_amdgcn_s_memrealtime();
+        t_begin = __builtin_amdgcn_s_memtime();
+    }
+#endif
     phase_stamp(clk, stamps, lane, 0);
     if (!STAMP_PHASES)
         clock_stamp(clk, 0);
@@ -204,6 +260,7 @@ __global__ void __launch_bounds__(WG)
     const uint32_t w0 = __builtin_amdgcn_readfirstlane(blockIdx.x * (WG / 64) + (threadIdx.x >> 6));
 
     for (uint32_t pos = w0; pos < nrecs; pos += waves) {
+        phase_acc(pa, bstamps, 1);
         const ptls_hip_record_t rec = by_value ? one : recs_ord[pos];
         const uint32_t rec_i = by_value ? 0u : order[pos];
         const uint32_t key = __builtin_amdgcn_readfirstlane(rec.key);
@@ -240,6 +297,7 @@ __global__ void __launch_bounds__(WG)
         cc.k23 = __builtin_amdgcn_readfirstlane(cc.k23);
         cc.r03 = __builtin_amdgcn_readfirstlane(cc.r03);
         phase_stamp(clk, stamps, lane, 2);
+        phase_acc(pa, bstamps, 2);
         wave_lds_sync(); /* the previous record's Horner reads of the table are done */
         if (horner) { /* (loading the basis during the previous record's VALU combine measured no faster: other waves hide it) */
             if (!by_value)
@@ -248,6 +306,7 @@ __global__ void __launch_bounds__(WG)
         }
         wave_lds_sync();
         phase_stamp(clk, stamps, lane, 3);
+        phase_acc(pa, bstamps, 3);
 
         V4 y = V4{0, 0, 0, 0}, ek0 = V4{0, 0, 0, 0};
         /* generic elements m .. m + NE - 1 of the lane (past `mend`: skipped): partial / AAD / length blocks and
@@ -322,6 +381,7 @@ __global__ void __launch_bounds__(WG)
          * record's memory (a single record read over PCIe by the plugin: one load latency instead of two) */
         generic_range(std::integral_constant<bool, BYVAL>{}, 0, npure ? pm0 : iters);
         phase_stamp(clk, stamps, lane, 4);
+        phase_acc(pa, bstamps, 4);
         if (npure) {
             const int c0 = 64 * pm0 + lane - na; /* the lane's first data block of the stretch */
             const uint8_t *src = in_p + 16 * (size_t)c0;
@@ -391,9 +451,11 @@ __global__ void __launch_bounds__(WG)
             }
         }
         phase_stamp(clk, stamps, lane, 5);
+        phase_acc(pa, bstamps, 5);
         if (npure)
             generic_range(std::false_type{}, pm1, iters);
         phase_stamp(clk, stamps, lane, 6);
+        phase_acc(pa, bstamps, 6);
 
         /* lane l's sum times H^(q+1), q = distance of its last element from the end of the GHASH input, on the
          * VALU; the XOR butterfly then sums the 64 lanes (ghash_combine) */
@@ -401,6 +463,7 @@ __global__ void __launch_bounds__(WG)
         if (SPARSE_ABLATE != 1)
             y = ghash_combine(bs, q, y);
         phase_stamp(clk, stamps, lane, 7);
+        phase_acc(pa, bstamps, 7);
         if (q == 0) {
             const V4 tag = v4xor(y, ek0);
             if (OPEN) {
@@ -412,6 +475,7 @@ __global__ void __launch_bounds__(WG)
             }
         }
         phase_stamp(clk, stamps, lane, 8);
+        phase_acc(pa, bstamps, 8);
         if (!OPEN && supp != nullptr) {
             /* QUIC header protection after the record (lib/fusion.c:636-650), as in aesgcm_batch_kernel: the
              * sample may cover the tag written by another lane of this wave */
@@ -437,6 +501,17 @@ __global__ void __launch_bounds__(WG)
             __hip_atomic_store(done, done_seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         phase_stamp(clk, stamps, lane, 11);
     }
+#if STAMP_PHASES
+    if (bstamps && clk != nullptr && lane == 0) { /* clk[16 + k] = cycles of phase k, [25] records, [26, 27] 100 MHz span */
+        for (int k = 2; k <= 8; ++k)
+            clk[16 + k] = pa.acc[k];
+        clk[25] = pa.n;
+        clk[26] = r_begin;
+        clk[27] = __builtin_amdgcn_s_memrealtime();
+        clk[28] = __builtin_amdgcn_s_memtime();
+        clk[29] = t_begin;
+    }
+#endif
     if (!STAMP_PHASES && clk != nullptr) { /* the workgroup's end: after its last wave */
         __syncthreads();
         clock_stamp(clk, 1);

@@ -15,14 +15,18 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ALT = os.path.join(os.path.dirname(HERE), "hsig-picotls_amd", "alt", "libptls_hip_split.so")
 
 
-def test_split_records_parity_on_the_alternate_build():
+@pytest.mark.parametrize("which,pct,ncases", [("runs", None, 5), ("chunks", "20", 2)])
+def test_split_records_parity_on_the_alternate_build(which, pct, ncases):
     if not os.path.exists(ALT):
         pytest.fail(f"{ALT} missing: build it with `make -C hsig-picotls_amd alts` (part of __graft_entry__.build())")
-    out = subprocess.run([sys.executable, os.path.join(HERE, "split_case.py")], env=dict(os.environ, PTLS_HIP_LIB=ALT),
-                         capture_output=True, text=True, timeout=600)
+    env = dict(os.environ, PTLS_HIP_LIB=ALT)
+    if pct is not None:
+        env["PTLS_HIP_SPLIT_PCT"] = pct
+    out = subprocess.run([sys.executable, os.path.join(HERE, "split_case.py"), which], env=env, capture_output=True, text=True,
+                         timeout=600)
     assert out.returncode == 0, out.stderr[-3000:]
     lines = [ln for ln in out.stdout.splitlines() if ln.startswith("MISMATCHES")]
-    assert len(lines) == 7 and f"DONE lib={ALT}" in out.stdout, out.stdout[-2000:]
+    assert len(lines) == ncases and f"DONE lib={ALT}" in out.stdout, out.stdout[-2000:]
     for ln in lines:
         assert int(re.search(r"split_tasks=(\d+)", ln).group(1)) > 0, ln
         assert ln.endswith("seal=0 open=0"), ln

@@ -17,6 +17,8 @@ done
 grep -v amdgpu.ids "$O/plugin.log"
 timeout -k 10 300 python tools/plugin_stamps.py > "$O/stamps.log" 2>&1 || { echo "stamps rc=$?"; tail -20 "$O/stamps.log"; exit 1; }
 tail -1 "$O/stamps.log"
+timeout -k 10 300 python tools/sparse_stamps.py > "$O/sparse_stamps.log" 2>&1 || { echo "sparse stamps rc=$?"; tail -20 "$O/sparse_stamps.log"; exit 1; }
+tail -1 "$O/sparse_stamps.log"
 for rep in 1 2; do
   for L in $R2 $P; do
     timeout -k 10 240 python tools/time_cfg.py $L --config c4s --clock --reps 11 >> "$O/ab.log" 2>&1 || exit 1
