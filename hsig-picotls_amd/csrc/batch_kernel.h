@@ -1199,7 +1199,7 @@ __global__ void __launch_bounds__(WGT)
              * result[] and supp[] at the end) */
             const uint32_t pos = ch.first + (valid ? ridx : 0);
             const ptls_hip_record_t rec = recs_ord[pos];
-            const uint32_t rec_i = order[pos];
+            const uint32_t rec_i = order != nullptr ? order[pos] : pos; /* no order array: the plan keeps the caller's order */
             const int L = valid ? (int)rec.len : 0;
             const int A = valid ? (int)rec.aad_len : 0;
             const int na = (A + 15) >> 4, nc = (L + 15) >> 4;

@@ -600,6 +600,11 @@ static void build_chunks(const ptls_hip_record_t *recs, size_t n, int lanes, uns
         plan_splits(recs, order, ch, lanes);
 }
 
+static bool identity_order(const std::vector<uint32_t> &order, size_t n);
+
+/* When the plan keeps the caller's order (equal lengths per key run, or already non-increasing: configs[1], [2], [4]),
+ * the kernels read the caller-order descriptors and no order array (record index = plan position): no second copy of
+ * the descriptors in HBM and 4 bytes per record less to read per launch. */
 static int plan_chunks(ptls_hip_batch_t *b)
 {
     std::vector<Chunk> ch;
@@ -623,6 +628,8 @@ static int plan_chunks(ptls_hip_batch_t *b)
         return 0;
     HIP_TRY(hipMalloc(&b->d_chunks, ch.size() * sizeof(Chunk)), PTLS_HIP_ENOMEM);
     HIP_TRY(hipMemcpy(b->d_chunks, ch.data(), ch.size() * sizeof(Chunk), hipMemcpyHostToDevice), PTLS_HIP_ENODEV);
+    if (identity_order(order, order.size()))
+        return 0; /* d_order and d_recs_ord stay null: run_batch passes d_recs and no order */
     HIP_TRY(hipMalloc(&b->d_order, order.size() * sizeof(uint32_t)), PTLS_HIP_ENOMEM);
     HIP_TRY(hipMemcpy(b->d_order, order.data(), order.size() * sizeof(uint32_t), hipMemcpyHostToDevice), PTLS_HIP_ENODEV);
     std::vector<ptls_hip_record_t> ord(order.size());
@@ -762,7 +769,7 @@ static int run_batch(ptls_hip_batch_t *b, ptls_hip_keyset_t *ks, const void *in,
     DeviceGuard g(b->eng->device);
     KernelArgs a{};
     a.recs = b->d_recs;
-    a.recs_ord = b->d_recs_ord;
+    a.recs_ord = b->d_recs_ord != nullptr ? b->d_recs_ord : b->d_recs;
     a.order = b->d_order;
     a.chunks = b->d_chunks;
     a.nchunks = b->nchunks;
@@ -1270,7 +1277,8 @@ static int pipeline_run_mapped(ptls_hip_pipeline_t *p, ptls_hip_keyset_t *ks, co
             HIP_TRY(hipMemcpyAsync(s.d_recs_ord, s.h_recs_ord, cnt * sizeof(ptls_hip_record_t), hipMemcpyHostToDevice, s.stream),
                     PTLS_HIP_ENODEV);
         }
-        HIP_TRY(hipMemcpyAsync(s.d_order, s.h_order, cnt * sizeof(uint32_t), hipMemcpyHostToDevice, s.stream), PTLS_HIP_ENODEV);
+        if (!ident)
+            HIP_TRY(hipMemcpyAsync(s.d_order, s.h_order, cnt * sizeof(uint32_t), hipMemcpyHostToDevice, s.stream), PTLS_HIP_ENODEV);
         HIP_TRY(hipMemcpyAsync(s.d_recs, s.h_recs, cnt * sizeof(ptls_hip_record_t), hipMemcpyHostToDevice, s.stream),
                 PTLS_HIP_ENODEV);
         HIP_TRY(hipMemcpyAsync(s.d_chunks, s.h_chunks, ch.size() * sizeof(Chunk), hipMemcpyHostToDevice, s.stream), PTLS_HIP_ENODEV);
@@ -1289,7 +1297,7 @@ static int pipeline_run_mapped(ptls_hip_pipeline_t *p, ptls_hip_keyset_t *ks, co
         KernelArgs a{};
         a.recs = s.d_recs;
         a.recs_ord = ident ? s.d_recs : s.d_recs_ord;
-        a.order = s.d_order;
+        a.order = ident ? nullptr : s.d_order;
         a.chunks = s.d_chunks;
         a.nchunks = (uint32_t)ch.size();
         a.in = d_in;
@@ -1507,7 +1515,8 @@ static int pipeline_run_copy(ptls_hip_pipeline_t *p, ptls_hip_keyset_t *ks, cons
             HIP_TRY(hipMemcpyAsync(s.d_recs_ord, s.h_recs_ord, cnt * sizeof(ptls_hip_record_t), hipMemcpyHostToDevice, s.stream),
                     PTLS_HIP_ENODEV);
         }
-        HIP_TRY(hipMemcpyAsync(s.d_order, s.h_order, cnt * sizeof(uint32_t), hipMemcpyHostToDevice, s.stream), PTLS_HIP_ENODEV);
+        if (!ident)
+            HIP_TRY(hipMemcpyAsync(s.d_order, s.h_order, cnt * sizeof(uint32_t), hipMemcpyHostToDevice, s.stream), PTLS_HIP_ENODEV);
         HIP_TRY(hipMemcpyAsync(s.d_recs, s.h_recs, cnt * sizeof(ptls_hip_record_t), hipMemcpyHostToDevice, s.stream),
                 PTLS_HIP_ENODEV);
         HIP_TRY(hipMemcpyAsync(s.d_chunks, s.h_chunks, ch.size() * sizeof(Chunk), hipMemcpyHostToDevice, s.stream), PTLS_HIP_ENODEV);
@@ -1525,7 +1534,7 @@ static int pipeline_run_copy(ptls_hip_pipeline_t *p, ptls_hip_keyset_t *ks, cons
         KernelArgs a{};
         a.recs = s.d_recs;
         a.recs_ord = ident ? s.d_recs : s.d_recs_ord;
-        a.order = s.d_order;
+        a.order = ident ? nullptr : s.d_order;
         a.chunks = s.d_chunks;
         a.nchunks = (uint32_t)ch.size();
         a.in = s.d_in;

@@ -262,7 +262,7 @@ __global__ void __launch_bounds__(WG)
     for (uint32_t pos = w0; pos < nrecs; pos += waves) {
         phase_acc(pa, bstamps, 1);
         const ptls_hip_record_t rec = by_value ? one : recs_ord[pos];
-        const uint32_t rec_i = by_value ? 0u : order[pos];
+        const uint32_t rec_i = by_value ? 0u : order != nullptr ? order[pos] : pos;
         const uint32_t key = __builtin_amdgcn_readfirstlane(rec.key);
         const KeySlot *__restrict__ slot = slots + key;
         const uint32_t *__restrict__ rk = slot->rk;

@@ -90,7 +90,7 @@ def supp_case(engine, oracle):
 
 def main():
     """`split_case.py runs`: configs[3]-shaped key runs at 16 / 32 lanes and header protection (the default threshold);
-    `split_case.py chunks` (run with PTLS_HIP_SPLIT_PCT=20, a low threshold): key runs of 40 / 80 tasks that span two
+    `split_case.py chunks` (run with PTLS_HIP_SPLIT_PCT=20, a low threshold): key runs of 40 tasks that span two
     chunks of one workgroup (grid capped at 2), so the split slots are numbered across chunks"""
     import torch
     assert torch.cuda.is_available()  # torch's HIP runtime first (tests/dealing_case.py)
@@ -107,7 +107,7 @@ def main():
         print(f"MISMATCHES case=supp key_len=16 lanes=16 split_tasks={ns} seal={s} open={p}", flush=True)
     else:
         for lanes in (16, 32):
-            ns, s, p = parity_case(eng, o, 32, lanes, max_wg=2, runs=3, per_run=160 if lanes == 16 else 320, max_len=12000)
+            ns, s, p = parity_case(eng, o, 32, lanes, max_wg=2, runs=3, per_run=160 if lanes == 16 else 80, max_len=12000)
             print(f"MISMATCHES case=chunks key_len=32 lanes={lanes} split_tasks={ns} seal={s} open={p}", flush=True)
     eng.close()
     print(f"DONE lib={ptls_hip.LIB_PATH}", flush=True)

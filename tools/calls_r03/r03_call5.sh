@@ -26,3 +26,9 @@ for rep in 1 2; do
   done
 done
 grep -v amdgpu.ids "$O/ab.log"
+for rep in 1 2; do
+  for L in $R2 $P; do
+    timeout -k 10 240 python tools/supp_probe.py $R/$L >> "$O/supp.log" 2>&1 || { echo "supp rc=$?"; exit 1; }
+  done
+done
+grep -v amdgpu.ids "$O/supp.log"
