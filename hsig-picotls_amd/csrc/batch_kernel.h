@@ -772,18 +772,20 @@ __device__ __forceinline__ V4 ld_basis(const uint32_t *b, int e)
  * of all its chunks issued first (one global-load latency instead of one per entry: what a single-record launch
  * waits on); consecutive threads write consecutive 16-B chunks (conflict-free). */
 template <int NT>
-__device__ __forceinline__ void build_aes_tables(uint8_t *lds, uint32_t base, const uint32_t *__restrict__ t0)
+__device__ __forceinline__ void build_aes_tables(uint8_t *lds, uint32_t base, const uint32_t *__restrict__ t0, int tid = -1)
 {
     constexpr int IT = (256 * 16 + NT - 1) / NT;
+    if (tid < 0)
+        tid = (int)threadIdx.x;
     uint32_t t[IT];
 #pragma unroll
     for (int k = 0; k < IT; ++k) {
-        const int c = (int)threadIdx.x + k * NT;
+        const int c = tid + k * NT;
         t[k] = c < 256 * 16 ? t0[c >> 4] : 0u;
     }
 #pragma unroll
     for (int k = 0; k < IT; ++k) {
-        const int c = (int)threadIdx.x + k * NT;
+        const int c = tid + k * NT;
         if (c < 256 * 16) {
             const uint32_t x = (c & 15) < 8 ? t[k] : (t[k] << 16) | (t[k] >> 16);
             lds128_store(lds, base + (uint32_t)(c >> 4) * 256u + (uint32_t)(c & 15) * 16u, V4{x, x, x, x});

@@ -244,8 +244,14 @@ __global__ void __launch_bounds__(WG)
         const uint4 pv = bsk[NPOW * 128 + ((na1 + nc1 - lane) & 63)];                        /* H^(q+1) of the combine */
         touch = V4{kv.x ^ pv.x, kv.y ^ pv.y, kv.z ^ pv.z, kv.w ^ pv.w};
     }
-    if (!PLUGIN_PROBE)
-        build_aes_tables<WG>(lds, 0, t0); /* the batch kernel's layout at offset 0 */
+    /* the single record's wave 0 leaves the table build to the other waves: its prefetch loads are older than any T0
+     * load it would issue, and vmcnt retires loads in order, so it would wait for its PCIe reads before its table stores */
+    if (!PLUGIN_PROBE) {
+        if (!BYVAL)
+            build_aes_tables<WG>(lds, 0, t0); /* the batch kernel's layout at offset 0 */
+        else if (threadIdx.x >= 64)
+            build_aes_tables<WG - 64>(lds, 0, t0, (int)threadIdx.x - 64);
+    }
     __syncthreads();
     asm volatile("" ::"v"(touch.w0), "v"(touch.w1), "v"(touch.w2), "v"(touch.w3)); /* keep the touch loads */
     phase_stamp(clk, stamps, lane, 1);
@@ -373,17 +379,33 @@ __global__ void __launch_bounds__(WG)
         constexpr int KP = SPARSE_PE;
         const int nf = (L - (tflag ? 1 : 0)) >> 4;              /* full blocks that are all input bytes */
         const int lastc = min(nf, 65534) - 1;                   /* last data block allowed in the stretch */
-        const int pm0 = (na + 63) >> 6;                         /* first m whose element is data on lane 0 */
-        const int mhi = lastc + na - 63 >= 0 ? ((lastc + na - 63) >> 6) + 1 : 0; /* m < mhi: lane 63's block <= lastc */
-        const int npure = SPARSE_PURE && mhi > pm0 ? (mhi - pm0) / KP : 0;
-        const int pm1 = pm0 + npure * KP;
-        /* without a stretch the head and tail are one range: element pairs straddling pm0 share one round trip to the
-         * record's memory (a single record read over PCIe by the plugin: one load latency instead of two) */
-        generic_range(std::integral_constant<bool, BYVAL>{}, 0, npure ? pm0 : iters);
+        /* Each lane starts the stretch at its own first data element (m = 1 on the lanes holding the AAD block, 0 on the
+         * others) and ends where its blocks stop being full: the stretch is the shortest lane's, the AAD elements before
+         * it are hashed only, and the record's generic head (one full AES per lane for one AAD block, 17 % of a c4s
+         * record, tools/sparse_stamps.py) is gone. */
+        const int ml = lane < na ? (na - lane + 63) >> 6 : 0;                          /* the lane's first data element */
+        const int mhl = lastc + na - lane >= 0 ? ((lastc + na - lane) >> 6) + 1 : 0;  /* its elements m < mhl: full blocks */
+        const int npure = SPARSE_PURE ? -wave_max(-max(mhl - ml, 0)) / KP : 0;
+        const int iters_l = lane < N ? ((N - 1 - lane) >> 6) + 1 : 0;                /* the lane's elements */
+        const int pm1 = ml + npure * KP;                                              /* the lane's first after the stretch */
+        if (!npure) { /* head and tail are one range: elements share one round trip to the record's memory (the plugin) */
+            generic_range(std::integral_constant<bool, BYVAL>{}, 0, iters);
+        } else { /* the lane's AAD elements: GHASH only */
+            const int naad = wave_max(ml);
+            for (int j = 0; j < naad; ++j) {
+                if (j < ml) {
+                    const int i = lane + 64 * j;
+                    const int nb = min(16, A - 16 * i);
+                    const V4 x = (BYVAL && prefetch && j < 2) ? mask_block(j == 0 ? pre[0] : pre[1], nb)
+                                                              : load_block<ALIGNED>(aad_p + 16 * i, nb);
+                    y = j == 0 ? x : v4xor(gh_mul_nibble(lds, tab, y), x);
+                }
+            }
+        }
         phase_stamp(clk, stamps, lane, 4);
         phase_acc(pa, bstamps, 4);
         if (npure) {
-            const int c0 = 64 * pm0 + lane - na; /* the lane's first data block of the stretch */
+            const int c0 = 64 * ml + lane - na; /* the lane's first data block of the stretch */
             const uint8_t *src = in_p + 16 * (size_t)c0;
             uint8_t *dst = out_p + 16 * (size_t)c0;
             V4 pend[KP], bufA[KP], bufB[KP];
@@ -452,8 +474,14 @@ __global__ void __launch_bounds__(WG)
         }
         phase_stamp(clk, stamps, lane, 5);
         phase_acc(pa, bstamps, 5);
-        if (npure)
-            generic_range(std::false_type{}, pm1, iters);
+        if (npure) { /* the rest of each lane's elements from its own position (partial, length and leftover blocks) */
+            const int rest = wave_max(max(iters_l - pm1, 0));
+            int j = 0;
+            for (; j + 1 < rest; j += 2)
+                generic(std::integral_constant<int, 2>{}, std::false_type{}, pm1 + j, iters_l);
+            if (j < rest)
+                generic(std::integral_constant<int, 1>{}, std::false_type{}, pm1 + j, iters_l);
+        }
         phase_stamp(clk, stamps, lane, 6);
         phase_acc(pa, bstamps, 6);
 
