@@ -239,6 +239,7 @@ extern "C" int ptls_hip_engine_cu_count(ptls_hip_engine_t *e)
 /* ---------------------------------------------------------------------------------------------- */
 
 static const size_t BASIS_WORDS_PER_SLOT = (size_t)BASIS_VECS * 4;
+static void worker_quiesce(void); /* the plugin worker leaves before key material changes (below, plugin section) */
 
 extern "C" ptls_hip_keyset_t *ptls_hip_keyset_new(ptls_hip_engine_t *eng, size_t key_size, size_t nslots)
 {
@@ -290,6 +291,7 @@ extern "C" int ptls_hip_keyset_set(ptls_hip_keyset_t *ks, size_t first, size_t c
         return fail(PTLS_HIP_EINVAL, "keyset_set: bad arguments");
     if (count == 0)
         return 0;
+    worker_quiesce();
     std::vector<uint8_t> zero_ivs;
     if (ivs == nullptr) { /* header-protection / ECB-only keys carry no IV */
         zero_ivs.assign(count * 12, 0);
@@ -331,6 +333,7 @@ static int keyset_from_secrets(ptls_hip_keyset_t *ks, size_t first, size_t count
         return fail(PTLS_HIP_EINVAL, "keyset_%s_secrets: bad arguments", update ? "update" : "set");
     if (count == 0)
         return 0;
+    worker_quiesce();
     DeviceGuard g(ks->eng->device);
     hipStream_t s = static_cast<hipStream_t>(stream);
     const size_t sbytes = count * hash_size, kbytes = count * ks->key_size, ibytes = count * 12;
@@ -386,6 +389,7 @@ extern "C" int ptls_hip_keyset_set_iv(ptls_hip_keyset_t *ks, size_t slot, const 
 {
     if (ks == nullptr || slot >= ks->nslots)
         return fail(PTLS_HIP_EINVAL, "keyset_set_iv: bad slot");
+    worker_quiesce();
     DeviceGuard g(ks->eng->device);
     std::memcpy(&ks->ivs[slot * 12], iv, 12);
     hipStream_t s = static_cast<hipStream_t>(stream);
@@ -998,14 +1002,37 @@ static int engine_self_check(ptls_hip_engine_t *e)
         if (hipMemcpy(d, buf, sizeof(buf), hipMemcpyHostToDevice) != hipSuccess)
             rc = fail(PTLS_HIP_ENODEV, "self-check: upload failed");
     }
+    /* the single-record kernel the plugin launches (record by value), and the batch kernel's table tree (8 lanes) and VALU
+     * combination (32 lanes) at 512 threads per workgroup: not the instantiations a 768-thread batch launch uses, so the
+     * self-check leaves no small dispatch in a profile of the batch kernels */
     static const int lanes[] = {SPARSE_LANES, 8, 32};
     for (int li = 0; rc == 0 && li < 3; ++li) {
         const ptls_hip_record_t seal{0, 256, 128, 0, 85, 20, 0, 0}, open{256, 384, 128, 0, 85, 20, 0, 0};
-        ptls_hip_batch_t *bs = ptls_hip_batch_new(e, &seal, 1, nullptr), *bo = ptls_hip_batch_new(e, &open, 1, nullptr);
-        if (bs == nullptr || bo == nullptr || ptls_hip_batch_set_lanes(bs, lanes[li]) != 0 || ptls_hip_batch_set_lanes(bo, lanes[li]) != 0 ||
-            hipMemset(d + 256, 0, 256) != hipSuccess || ptls_hip_aesgcm_seal_batch(bs, ks, d, d, d, nullptr) != 0 ||
-            ptls_hip_aesgcm_open_batch(bo, ks, d, d, d, reinterpret_cast<uint64_t *>(d + 480), nullptr) != 0 ||
-            hipMemcpy(buf, d, sizeof(buf), hipMemcpyDeviceToHost) != hipSuccess) {
+        bool ok = hipMemset(d + 256, 0, 256) == hipSuccess;
+        if (lanes[li] == SPARSE_LANES) {
+            for (int o = 0; ok && o < 2; ++o) {
+                KernelArgs a{};
+                a.one = o ? open : seal;
+                a.in = a.aad = d;
+                a.out = d;
+                a.result = reinterpret_cast<uint64_t *>(d + 480);
+                a.slots = ks->d_slots;
+                a.basis = ks->d_basis;
+                a.t0 = e->d_t0;
+                ok = launch_batch(SPARSE_LANES, 10, o != 0, 0, 1, nullptr, a, true) == 0 && hipStreamSynchronize(nullptr) == hipSuccess;
+            }
+            ok = ok && hipMemcpy(buf, d, sizeof(buf), hipMemcpyDeviceToHost) == hipSuccess;
+        } else {
+            ptls_hip_batch_t *bs = ptls_hip_batch_new(e, &seal, 1, nullptr), *bo = ptls_hip_batch_new(e, &open, 1, nullptr);
+            ok = ok && bs != nullptr && bo != nullptr && ptls_hip_batch_set_lanes(bs, lanes[li]) == 0 &&
+                 ptls_hip_batch_set_lanes(bo, lanes[li]) == 0 && ptls_hip_batch_set_workgroup(bs, 512) == 0 &&
+                 ptls_hip_batch_set_workgroup(bo, 512) == 0 && ptls_hip_aesgcm_seal_batch(bs, ks, d, d, d, nullptr) == 0 &&
+                 ptls_hip_aesgcm_open_batch(bo, ks, d, d, d, reinterpret_cast<uint64_t *>(d + 480), nullptr) == 0 &&
+                 hipMemcpy(buf, d, sizeof(buf), hipMemcpyDeviceToHost) == hipSuccess;
+            ptls_hip_batch_free(bs);
+            ptls_hip_batch_free(bo);
+        }
+        if (!ok) {
             rc = fail(PTLS_HIP_ENODEV, "self-check: launch failed (%s)", g_err.c_str());
         } else {
             uint64_t res = 0;
@@ -1013,8 +1040,6 @@ static int engine_self_check(ptls_hip_engine_t *e)
             if (std::memcmp(buf + 256, expected, sizeof(expected)) != 0 || res != 85 || std::memcmp(buf + 384, pt, sizeof(pt)) != 0)
                 rc = fail(PTLS_HIP_ENODEV, "gcm_basic (t/fusion.c:251-273) sealed or opened wrong at %d lanes per record", lanes[li]);
         }
-        ptls_hip_batch_free(bs);
-        ptls_hip_batch_free(bo);
     }
     if (d != nullptr) {
         (void)hipMemset(d, 0, sizeof(buf));
@@ -1870,6 +1895,140 @@ static void plugin_wait(hipStream_t stream, const uint8_t *word_p, uint32_t seq)
 
 static unsigned staging_flags(void);
 
+/* ---- the plugin worker (sparse_kernel.hip plugin_worker_kernel) ------------------------------------------------- *
+ * A plugin call launches nothing while the worker is resident: it writes its request into the worker's mailbox (pinned,
+ * fine-grained), then waits on its completion word as a launched call does.  Calls are serialized on the worker (one
+ * request at a time; the mutex is held for the whole call).  The worker leaves after WORKER_IDLE_US without a request
+ * or after WORKER_LIFE_US, and a call that finds it gone relaunches it (the launch a call without the worker pays each
+ * time).  Opt-in while it is being validated: PTLS_HIP_PLUGIN_WORKER=1 (environment); otherwise one launch per call. */
+static const uint64_t WORKER_IDLE_US = 200, WORKER_LIFE_US = 2000;
+
+struct PluginWorker {
+    std::mutex mu;
+    ptls_hip_engine_t *eng = nullptr;
+    hipStream_t stream = nullptr;
+    WorkerSlot *h_mb = nullptr, *d_mb = nullptr;
+    uint32_t epoch = 0; /* of the last worker launched; h_mb->exited == epoch: it has left */
+    uint32_t seq = 0;
+    bool launched = false;
+};
+static PluginWorker g_worker;
+
+static bool worker_enabled(void)
+{
+    static const bool on = [] {
+        const char *e = getenv("PTLS_HIP_PLUGIN_WORKER");
+        return e != nullptr && atoi(e) != 0;
+    }();
+    return on;
+}
+
+static uint32_t load_acquire(const uint32_t *p)
+{
+    return __atomic_load_n(p, __ATOMIC_ACQUIRE);
+}
+
+/* at process exit (atexit: before the HIP runtime's own teardown): ask a resident worker to leave and wait for it, with
+ * host memory only, so no kernel is running when the process ends */
+static void worker_atexit(void)
+{
+    PluginWorker &w = g_worker;
+    if (w.h_mb == nullptr || !w.launched)
+        return;
+    __atomic_store_n(&w.h_mb->quit, 1u, __ATOMIC_RELEASE);
+    const auto t0 = std::chrono::steady_clock::now();
+    while (load_acquire(&w.h_mb->exited) != w.epoch && std::chrono::steady_clock::now() - t0 < std::chrono::milliseconds(50))
+        std::this_thread::yield();
+}
+
+/* under w.mu: the worker's mailbox and stream on the plugin engine's device, and a resident worker */
+static bool worker_launch(PluginWorker &w)
+{
+    if (w.h_mb == nullptr) {
+        void *d = nullptr;
+        if (hipStreamCreateWithFlags(&w.stream, hipStreamNonBlocking) != hipSuccess ||
+            hipHostMalloc(&w.h_mb, sizeof(WorkerSlot), hipHostMallocCoherent) != hipSuccess ||
+            hipHostGetDevicePointer(&d, w.h_mb, 0) != hipSuccess)
+            return false;
+        std::memset(w.h_mb, 0, sizeof(WorkerSlot));
+        w.d_mb = static_cast<WorkerSlot *>(d);
+        atexit(worker_atexit);
+    }
+    /* a worker that has not left yet keeps serving: a second one on the same mailbox would serve its requests twice */
+    if (w.launched && load_acquire(&w.h_mb->exited) != w.epoch)
+        return true;
+    ++w.epoch;
+    const int e = launch_plugin_worker(w.d_mb, w.epoch, w.eng->d_t0, WORKER_IDLE_US * 100, WORKER_LIFE_US * 100, w.stream);
+    if (e != 0) {
+        g_err = hipGetErrorString((hipError_t)e);
+        return false;
+    }
+    w.launched = true;
+    return true;
+}
+
+/* Before key material changes (a keyset's keys, IVs or secrets): a resident worker leaves, so the next call's fresh
+ * dispatch reads the new slot contents (a dispatch starts with its caches invalidated; a running wave's scalar cache
+ * could still hold a slot's old round keys or IV, and a freed slot's address may come back for a new context). */
+static void worker_quiesce(void)
+{
+    PluginWorker &w = g_worker;
+    std::lock_guard<std::mutex> lk(w.mu);
+    if (w.h_mb == nullptr || !w.launched || load_acquire(&w.h_mb->exited) == w.epoch)
+        return;
+    __atomic_store_n(&w.h_mb->quit, 1u, __ATOMIC_RELEASE);
+    const auto t0 = std::chrono::steady_clock::now();
+    while (load_acquire(&w.h_mb->exited) != w.epoch) {
+        if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(2)) {
+            g_err = "the plugin worker did not leave";
+            plugin_die("worker_quiesce");
+        }
+        std::this_thread::yield();
+    }
+    __atomic_store_n(&w.h_mb->quit, 0u, __ATOMIC_RELEASE);
+}
+
+/* one request through the worker; returns once the call's completion word shows done_seq (the same protocol as a
+ * launched call, plugin_wait).  A worker that left without serving the request is relaunched (its successor serves it:
+ * seq != served); without any progress for 2 s the process aborts like a launched call's device fault would. */
+static void worker_call(const WorkerReq &req, const uint8_t *word_p)
+{
+    PluginWorker &w = g_worker;
+    DeviceGuard g(w.eng->device);
+    if (!worker_launch(w))
+        plugin_die("plugin worker launch");
+    w.h_mb->req = req;
+    __atomic_store_n(&w.h_mb->seq, ++w.seq, __ATOMIC_RELEASE);
+    const uint32_t *word = reinterpret_cast<const uint32_t *>(word_p);
+    auto t0 = std::chrono::steady_clock::now();
+    for (uint32_t spin = 1;; ++spin) {
+        if (load_acquire(word) == req.done_seq)
+            return;
+#if defined(__x86_64__) || defined(__i386__)
+        __builtin_ia32_pause();
+#else
+        std::this_thread::yield();
+#endif
+        if ((spin & 1023) == 0) {
+            if (load_acquire(&w.h_mb->exited) == w.epoch && load_acquire(&w.h_mb->served) != w.seq) {
+                if (!worker_launch(w)) /* it left (idle / lifetime) just before the request: its successor serves it */
+                    plugin_die("plugin worker relaunch");
+                t0 = std::chrono::steady_clock::now();
+            } else if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(2)) {
+                plugin_check(hipStreamSynchronize(w.stream), "plugin worker");
+                static char msg[256];
+                snprintf(msg, sizeof(msg),
+                         "the plugin worker stopped serving (request %u, served %u, seen %u, epoch %u, started %u, exited %u, "
+                         "word %u of %u)",
+                         w.seq, load_acquire(&w.h_mb->served), load_acquire(&w.h_mb->seen), w.epoch,
+                         load_acquire(&w.h_mb->started), load_acquire(&w.h_mb->exited), load_acquire(word), req.done_seq);
+                g_err = msg;
+                plugin_die("worker_call");
+            }
+        }
+    }
+}
+
 /* ---- CTR cipher for header protection (replaces lib/fusion.c:1050-1100) ---------------------------- */
 
 struct hip_ctr_state {
@@ -1904,6 +2063,24 @@ static const size_t ECB_DONE = 64;
 static void ecb_block(hip_ctr_state *st, const void *src, uint8_t dst[16])
 {
     DeviceGuard g(st->eng->device);
+    if (worker_enabled()) {
+        WorkerReq rq{};
+        rq.out = st->d_stage + 48;
+        rq.slots = st->ks->d_slots;
+        rq.done = reinterpret_cast<uint32_t *>(st->d_stage + ECB_DONE);
+        rq.done_seq = ++st->done_seq;
+        rq.flags = WREQ_ECB | (st->ks->key_size == 32 ? WREQ_AES256 : 0u);
+        std::memcpy(rq.blk, src, 16);
+        {
+            std::lock_guard<std::mutex> lk(g_worker.mu);
+            g_worker.eng = st->eng;
+            worker_call(rq, st->h_stage + ECB_DONE);
+        }
+        std::memcpy(dst, st->h_stage + 48, 16);
+        std::memset(st->h_stage + 48, 0, 16);
+        std::memset(rq.blk, 0, sizeof(rq.blk));
+        return;
+    }
     /* the block goes in the kernel arguments; the result comes back through the pinned staging (@48) */
     const int e = launch_aesecb_one(st->ks->key_size == 16 ? 10 : 14, static_cast<const uint8_t *>(src), st->ks->d_slots,
                                     st->eng->d_t0, st->d_stage + 48, reinterpret_cast<uint32_t *>(st->d_stage + ECB_DONE),
@@ -2101,6 +2278,9 @@ static void state_reserve(hip_aead_state *st, size_t len, size_t aadlen)
     st->aad_cap = aad_cap;
 }
 
+#ifndef STAMP_PHASES
+#define STAMP_PHASES 0 /* diagnostic build only (Makefile `diag`) */
+#endif
 #if STAMP_PHASES
 /* diagnostic build (Makefile `diag`): the last plugin call's phase stamps (sparse_kernel.hip phase_stamp) */
 static uint64_t *g_diag_stamps = nullptr;
@@ -2171,17 +2351,37 @@ static uint64_t plugin_run(hip_aead_state *st, bool open, void *output, const vo
     }
     a.done = reinterpret_cast<uint32_t *>(st->d_stage + ST_DONE);
     a.done_seq = ++st->done_seq;
+    if (worker_enabled() && !STAMP_PHASES) {
+        WorkerReq rq{};
+        rq.rec = rec;
+        rq.in = a.in;
+        rq.aad = a.aad;
+        rq.out = a.out;
+        rq.result = a.result;
+        rq.slots = a.slots;
+        rq.basis = a.basis;
+        rq.supp = a.supp;
+        rq.hp_slots = a.hp_slots;
+        rq.mask = a.mask;
+        rq.done = a.done;
+        rq.done_seq = a.done_seq;
+        rq.flags = (open ? WREQ_OPEN : 0u) | (st->ks->key_size == 32 ? WREQ_AES256 : 0u);
+        std::lock_guard<std::mutex> lk(g_worker.mu);
+        g_worker.eng = st->eng;
+        worker_call(rq, st->h_stage + ST_DONE);
+    } else {
 #if STAMP_PHASES
-    if (g_diag_stamps == nullptr)
-        plugin_check(hipMalloc(&g_diag_stamps, 16 * sizeof(uint64_t)), "hipMalloc(stamps)");
-    a.clk = g_diag_stamps;
+        if (g_diag_stamps == nullptr)
+            plugin_check(hipMalloc(&g_diag_stamps, 16 * sizeof(uint64_t)), "hipMalloc(stamps)");
+        a.clk = g_diag_stamps;
 #endif
-    const int e = launch_batch(SPARSE_LANES, st->ks->key_size == 16 ? 10 : 14, open, 0, 1, st->stream, a, true);
-    if (e != 0) {
-        g_err = hipGetErrorString((hipError_t)e);
-        plugin_die("launch");
+        const int e = launch_batch(SPARSE_LANES, st->ks->key_size == 16 ? 10 : 14, open, 0, 1, st->stream, a, true);
+        if (e != 0) {
+            g_err = hipGetErrorString((hipError_t)e);
+            plugin_die("launch");
+        }
+        plugin_wait(st->stream, st->h_stage + ST_DONE, a.done_seq);
     }
-    plugin_wait(st->stream, st->h_stage + ST_DONE, a.done_seq);
     uint64_t result = len;
     if (open) {
         if (len != 0)

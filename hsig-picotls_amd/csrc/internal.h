@@ -129,7 +129,43 @@ struct KernelArgs {
     uint64_t *clk;
 };
 
+/* The plugin worker (sparse_kernel.hip plugin_worker_kernel, engine.cpp): a resident one-wave kernel that serves the
+ * plugin's single-record calls from a mailbox in fine-grained pinned host memory instead of one kernel launch per call.
+ * The host writes the request, then (release) seq; the wave serves it, stores the call's completion word (as a launched
+ * call's kernel does), then `served`. */
+enum : uint32_t { WREQ_OPEN = 1, WREQ_AES256 = 2, WREQ_ECB = 4 };
+struct WorkerReq {
+    ptls_hip_record_t rec;    /* by value: offsets into in / aad / out */
+    const uint8_t *in, *aad;  /* device addresses of the context's pinned staging */
+    uint8_t *out;
+    uint64_t *result;         /* open: the verification result */
+    const KeySlot *slots;     /* the context's key slot (and its basis) */
+    const uint32_t *basis;
+    const ptls_hip_supp_t *supp; /* optional header protection */
+    const KeySlot *hp_slots;
+    uint8_t *mask;
+    uint32_t *done;           /* the call's completion word */
+    uint32_t done_seq;
+    uint32_t flags;           /* WREQ_* */
+    uint32_t blk[4];          /* WREQ_ECB: the input block (the output goes to `out`) */
+    uint32_t pad[10];
+};
+static_assert(sizeof(WorkerReq) == 192, "WorkerReq: 192 bytes");
+struct WorkerSlot {
+    uint32_t seq;    /* host -> worker: the request number, written after the request */
+    uint32_t quit;   /* host -> worker: leave */
+    uint32_t pad0[30];
+    uint32_t served;  /* worker -> host: the last request served */
+    uint32_t exited;  /* worker -> host: the epoch of the worker wave that left */
+    uint32_t started; /* worker -> host: the epoch of the worker wave that started (diagnostics) */
+    uint32_t seen;    /* worker -> host: the last request number it read (diagnostics) */
+    uint32_t pad1[28];
+    WorkerReq req;
+};
+static_assert(sizeof(WorkerSlot) == 448, "WorkerSlot: seq / quit, served / exited, request on separate 128-B lines");
+
 /* host-side launchers, defined next to the kernels (aesgcm_kernels.hip, batch_g*.hip) */
+int launch_plugin_worker(WorkerSlot *mb, uint32_t epoch, const uint32_t *t0, uint64_t idle_ticks, uint64_t life_ticks, void *stream);
 int launch_batch_g1(int rounds, bool open, int wg, unsigned grid, void *stream, const KernelArgs &a, bool aligned);
 int launch_batch_g2(int rounds, bool open, int wg, unsigned grid, void *stream, const KernelArgs &a, bool aligned);
 int launch_batch_g4(int rounds, bool open, int wg, unsigned grid, void *stream, const KernelArgs &a, bool aligned);

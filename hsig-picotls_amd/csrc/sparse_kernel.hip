@@ -188,6 +188,271 @@ __device__ __forceinline__ V4 ghash_combine(const uint4 *__restrict__ bs, int q,
     return z;
 }
 
+/* One record on one wave (the sparse-key kernel's per-record body, also the plugin worker's): its counter-mode
+ * constants, its per-wave H^64 table, the elements (generic head / branch-free stretch / generic tail), the lane
+ * combination, the tag, header protection.  pre / prefetch: a single record's first two elements per lane, read before
+ * (BYVAL: the plugin's launch and the worker). */
+template <int ROUNDS, bool OPEN, bool ALIGNED, bool BYVAL>
+__device__ __forceinline__ void sparse_record(uint8_t *lds, int lane, uint32_t lb_aes, uint32_t tab, const ptls_hip_record_t &rec,
+                                              uint32_t rec_i, const uint8_t *in, const uint8_t *__restrict__ aad, uint8_t *out,
+                                              uint64_t *__restrict__ result, const KeySlot *__restrict__ slots,
+                                              const uint32_t *__restrict__ basis, const ptls_hip_supp_t *__restrict__ supp,
+                                              const KeySlot *__restrict__ hp_slots, uint32_t hp_nslots, uint8_t *mask, bool prefetch,
+                                              const V4 (&pre)[2], uint64_t *__restrict__ clk, bool stamps, bool bstamps, PhaseAcc &pa)
+{
+    constexpr bool by_value = BYVAL;
+    (void)by_value, (void)clk, (void)stamps, (void)bstamps, (void)pa;
+    const uint32_t key = __builtin_amdgcn_readfirstlane(rec.key);
+    const KeySlot *__restrict__ slot = slots + key;
+    const uint32_t *__restrict__ rk = slot->rk;
+    const uint4 *__restrict__ bs = reinterpret_cast<const uint4 *>(basis) + (size_t)key * BASIS_VECS;
+    const int L = (int)__builtin_amdgcn_readfirstlane(rec.len);
+    const int A = (int)__builtin_amdgcn_readfirstlane(rec.aad_len);
+    const int na = (A + 15) >> 4, nc = (L + 15) >> 4;
+    const int N = na + nc + 1;
+    const bool tflag = !OPEN && (rec.flags & 1u) != 0 && L > 0;
+    const uint32_t ttype = (rec.flags >> 8) & 0xffu;
+    const uint8_t *in_p = in + rec.in_off;
+    uint8_t *out_p = out + rec.out_off;
+    const uint8_t *aad_p = aad + rec.aad_off;
+    const uint32_t n0 = __builtin_amdgcn_readfirstlane(slot->iv[0]),
+                   n1 = __builtin_amdgcn_readfirstlane(slot->iv[1] ^ bswap32((uint32_t)(rec.seq >> 32))),
+                   n2 = __builtin_amdgcn_readfirstlane(slot->iv[2] ^ bswap32((uint32_t)rec.seq));
+    const int iters = (N + 63) >> 6;
+    const bool horner = SPARSE_ABLATE != 3 && iters > 1; /* N <= 64: one element per lane, no Horner step */
+    V4 b[4];
+    /* a single record (the plugin's launch): the H^64 basis loads go out before the counter-mode constants, so their
+     * memory latency overlaps that LDS chain (in batches other waves hide it; there the early loads cost c4s open
+     * 2.5 %, measured) */
+    if (horner && by_value)
+        load_wave_basis(bs + 6 * 128, lane, b); /* H^64 */
+    /* the record (and so its counter-mode constants) is the wave's alone: keep them in SGPRs */
+    CtrConst cc = ctr_const(lds, lb_aes, rk, n0, n1, n2);
+    cc.k10 = __builtin_amdgcn_readfirstlane(cc.k10);
+    cc.k11 = __builtin_amdgcn_readfirstlane(cc.k11);
+    cc.k20 = __builtin_amdgcn_readfirstlane(cc.k20);
+    cc.k21 = __builtin_amdgcn_readfirstlane(cc.k21);
+    cc.k22 = __builtin_amdgcn_readfirstlane(cc.k22);
+    cc.k23 = __builtin_amdgcn_readfirstlane(cc.k23);
+    cc.r03 = __builtin_amdgcn_readfirstlane(cc.r03);
+    phase_stamp(clk, stamps, lane, 2);
+    phase_acc(pa, bstamps, 2);
+    wave_lds_sync(); /* the previous record's Horner reads of the table are done */
+    if (horner) { /* (loading the basis during the previous record's VALU combine measured no faster: other waves hide it) */
+        if (!by_value)
+            load_wave_basis(bs + 6 * 128, lane, b); /* H^64 */
+        store_wave_table(lds, tab, b, lane);
+    }
+    wave_lds_sync();
+    phase_stamp(clk, stamps, lane, 3);
+    phase_acc(pa, bstamps, 3);
+
+    V4 y = V4{0, 0, 0, 0}, ek0 = V4{0, 0, 0, 0};
+    /* generic elements m .. m + NE - 1 of the lane (past `mend`: skipped): partial / AAD / length blocks and
+     * counters >= 2^16, their AES blocks interleaved (counter-mode shortcut unless a counter is that large) */
+    auto generic = [&](auto ne_tag, auto pre_tag, int m, int mend) __attribute__((always_inline)) {
+        constexpr int NE = decltype(ne_tag)::value;
+        constexpr bool USE_PRE = decltype(pre_tag)::value; /* the head range only: pre is dead after it */
+        Elem e[NE];
+        V4 inb[NE], ks[NE];
+        uint32_t cw[NE];
+        int big = 0;
+#pragma unroll
+        for (int b = 0; b < NE; ++b) {
+            e[b] = elem_of(m + b < mend ? lane + (m + b) * 64 : N, N, na, nc, L, N);
+            inb[b] = V4{0, 0, 0, 0};
+            /* the lane's first two elements of a single record were read at the start (pre) */
+            const bool have_pre = USE_PRE && prefetch && m + b < 2;
+            const V4 pv = m + b == 0 ? pre[0] : pre[1];
+            if (e[b].is_c) {
+                const bool tb = tflag && e[b].c == nc - 1; /* the block holding the content-type byte */
+                const int nb = e[b].nbytes - (tb ? 1 : 0);
+                inb[b] = have_pre ? mask_block(pv, nb) : load_block<ALIGNED>(in_p + 16 * (size_t)e[b].c, nb);
+                if (tb)
+                    inb[b] = put_byte(inb[b], e[b].nbytes - 1, ttype);
+            } else if (e[b].is_aad) { /* loaded before the AES as well, not after it in finish_elem */
+                const int nb = min(16, A - 16 * e[b].i);
+                inb[b] = have_pre ? mask_block(pv, nb) : load_block<ALIGNED>(aad_p + 16 * e[b].i, nb);
+            }
+            /* keystream for data block c (counter inc32(J0) + c), E_K(J0) for the length-block lane */
+            cw[b] = e[b].is_c ? bswap32((uint32_t)e[b].c + 2u) : 0x01000000u;
+            ks[b] = V4{n0, n1, n2, cw[b]};
+            big |= (e[b].is_c && e[b].c >= 65534) ? 1 : 0;
+        }
+        if (wave_max(big)) {
+            aes_encrypt_n<ROUNDS, NE>(lds, lb_aes, rk, ks);
+        } else if (!SPARSE_GEN_SKEW) {
+            aes_ctr_n<ROUNDS, NE>(lds, lb_aes, rk, cc, cw, ks);
+        } else {
+            const V4 nohash[NE] = {};
+            V4 ydummy = V4{0, 0, 0, 0};
+            ctr_ghash_skewed<ROUNDS, NE, false>(lds, lb_aes, rk, cc, cw, ks, ydummy, nohash, GhNibble{tab});
+        }
+#pragma unroll
+        for (int b = 0; b < NE; ++b) {
+            const V4 x = finish_elem<OPEN, ALIGNED, true>(e[b], inb[b], ks[b], aad_p, A, L, out_p, ek0);
+            if (m + b == 0)
+                y = x; /* 0 * P ^ x */
+            else if (SPARSE_ABLATE != 2 && e[b].active)
+                y = v4xor(gh_mul_nibble(lds, tab, y), x); /* y * H^64 ^ x */
+        }
+    };
+    auto generic_range = [&](auto pre_tag, int m0, int m1) __attribute__((always_inline)) {
+        int m = m0;
+        for (; m + 1 < m1; m += 2)
+            generic(std::integral_constant<int, 2>{}, pre_tag, m, m1);
+        if (m < m1)
+            generic(std::integral_constant<int, 1>{}, pre_tag, m, m1);
+    };
+
+    /* the wave's "pure" elements m in [pm0, pm1): every lane's element is a full data block with a counter below
+     * 2^16 (lane l, element m = data block 64 m + l - na).  There the body is branch-free, KP blocks per lane per
+     * iteration, the counter-mode AES of the blocks skewed against the H^64 multiplies of the previous iteration's
+     * ciphertext (seal) or of the input ciphertext (open), the next iteration's plaintext prefetched. */
+    constexpr int KP = SPARSE_PE;
+    const int nf = (L - (tflag ? 1 : 0)) >> 4;              /* full blocks that are all input bytes */
+    const int lastc = min(nf, 65534) - 1;                   /* last data block allowed in the stretch */
+    /* Each lane starts the stretch at its own first data element (m = 1 on the lanes holding the AAD block, 0 on the
+     * others) and ends where its blocks stop being full: the stretch is the shortest lane's, the AAD elements before
+     * it are hashed only, and the record's generic head (one full AES per lane for one AAD block, 17 % of a c4s
+     * record, tools/sparse_stamps.py) is gone. */
+    const int ml = lane < na ? (na - lane + 63) >> 6 : 0;                          /* the lane's first data element */
+    const int mhl = lastc + na - lane >= 0 ? ((lastc + na - lane) >> 6) + 1 : 0;  /* its elements m < mhl: full blocks */
+    const int npure = SPARSE_PURE ? -wave_max(-max(mhl - ml, 0)) / KP : 0;
+    const int iters_l = lane < N ? ((N - 1 - lane) >> 6) + 1 : 0;                /* the lane's elements */
+    const int pm1 = ml + npure * KP;                                              /* the lane's first after the stretch */
+    if (!npure) { /* head and tail are one range: elements share one round trip to the record's memory (the plugin) */
+        generic_range(std::integral_constant<bool, BYVAL>{}, 0, iters);
+    } else { /* the lane's AAD elements: GHASH only */
+        const int naad = wave_max(ml);
+        for (int j = 0; j < naad; ++j) {
+            if (j < ml) {
+                const int i = lane + 64 * j;
+                const int nb = min(16, A - 16 * i);
+                const V4 x = (BYVAL && prefetch && j < 2) ? mask_block(j == 0 ? pre[0] : pre[1], nb)
+                                                          : load_block<ALIGNED>(aad_p + 16 * i, nb);
+                y = j == 0 ? x : v4xor(gh_mul_nibble(lds, tab, y), x);
+            }
+        }
+    }
+    phase_stamp(clk, stamps, lane, 4);
+    phase_acc(pa, bstamps, 4);
+    if (npure) {
+        const int c0 = 64 * ml + lane - na; /* the lane's first data block of the stretch */
+        const uint8_t *src = in_p + 16 * (size_t)c0;
+        uint8_t *dst = out_p + 16 * (size_t)c0;
+        V4 pend[KP], bufA[KP], bufB[KP];
+        /* open hashes its input in the iteration that loads it: the next iteration's blocks are prefetched into the
+         * other buffer.  Seal uses its plaintext only after the iteration's AES, so it loads at the top of the
+         * iteration into one buffer (8 VGPRs fewer: the seal instantiations stay within 168 without scratch). */
+#pragma unroll
+        for (int b = 0; b < KP; ++b)
+            bufA[b] = load_full(src + 1024 * b);
+        auto pure_iter = [&](int it, bool hash_pending, V4(&d)[KP], V4(&dn)[KP]) __attribute__((always_inline)) {
+            const size_t o = (size_t)it * KP * 1024;
+            const size_t on = (size_t)min(it + 1, npure - 1) * KP * 1024;
+            V4 k[KP];
+            uint32_t cw[KP];
+#pragma unroll
+            for (int b = 0; b < KP; ++b) {
+                if (OPEN)
+                    dn[b] = load_full(src + on + 1024 * b);
+                else if (it != 0)
+                    d[b] = load_full(src + o + 1024 * b);
+                cw[b] = bswap32((uint32_t)(c0 + 2 + (it * KP + b) * 64));
+                k[b] = V4{n0, n1, n2, cw[b]};
+            }
+            __builtin_amdgcn_sched_barrier(0); /* keep the loads at the top of the iteration */
+            if (SPARSE_ABLATE == 2) {
+                ctr_ghash_skewed<ROUNDS, KP, false>(lds, lb_aes, rk, cc, cw, k, y, d, GhNibble{tab});
+#pragma unroll
+                for (int b = 0; b < KP; ++b) {
+                    pend[b] = v4xor(d[b], k[b]);
+                    store_full(dst + o + 1024 * b, pend[b]);
+                }
+            } else if (OPEN) {
+                ctr_ghash_skewed<ROUNDS, KP, true>(lds, lb_aes, rk, cc, cw, k, y, d, GhNibble{tab});
+#pragma unroll
+                for (int b = 0; b < KP; ++b)
+                    store_full(dst + o + 1024 * b, v4xor(d[b], k[b]));
+            } else {
+                if (hash_pending)
+                    ctr_ghash_skewed<ROUNDS, KP, true>(lds, lb_aes, rk, cc, cw, k, y, pend, GhNibble{tab});
+                else
+                    ctr_ghash_skewed<ROUNDS, KP, false>(lds, lb_aes, rk, cc, cw, k, y, pend, GhNibble{tab});
+#pragma unroll
+                for (int b = 0; b < KP; ++b) {
+                    pend[b] = v4xor(d[b], k[b]);
+                    store_full(dst + o + 1024 * b, pend[b]);
+                }
+            }
+        };
+        if (OPEN) {
+            pure_iter(0, false, bufA, bufB);
+            int it = 1;
+            for (; it + 1 < npure; it += 2) {
+                pure_iter(it, true, bufB, bufA);
+                pure_iter(it + 1, true, bufA, bufB);
+            }
+            if (it < npure)
+                pure_iter(it, true, bufB, bufA);
+        } else {
+            pure_iter(0, false, bufA, bufA);
+            for (int it = 1; it < npure; ++it)
+                pure_iter(it, true, bufA, bufA);
+#pragma unroll
+            for (int b = 0; b < KP; ++b)
+                y = v4xor(gh_mul_nibble(lds, tab, y), pend[b]);
+        }
+    }
+    phase_stamp(clk, stamps, lane, 5);
+    phase_acc(pa, bstamps, 5);
+    if (npure) { /* the rest of each lane's elements from its own position (partial, length and leftover blocks) */
+        const int rest = wave_max(max(iters_l - pm1, 0));
+        int j = 0;
+        for (; j + 1 < rest; j += 2)
+            generic(std::integral_constant<int, 2>{}, std::false_type{}, pm1 + j, iters_l);
+        if (j < rest)
+            generic(std::integral_constant<int, 1>{}, std::false_type{}, pm1 + j, iters_l);
+    }
+    phase_stamp(clk, stamps, lane, 6);
+    phase_acc(pa, bstamps, 6);
+
+    /* lane l's sum times H^(q+1), q = distance of its last element from the end of the GHASH input, on the
+     * VALU; the XOR butterfly then sums the 64 lanes (ghash_combine) */
+    const int q = (N - 1 - lane) & 63;
+    if (SPARSE_ABLATE != 1)
+        y = ghash_combine(bs, q, y);
+    phase_stamp(clk, stamps, lane, 7);
+    phase_acc(pa, bstamps, 7);
+    if (q == 0) {
+        const V4 tag = v4xor(y, ek0);
+        if (OPEN) {
+            const V4 rt = load_block<false>(in_p + L, 16);
+            const bool ok = rt.w0 == tag.w0 && rt.w1 == tag.w1 && rt.w2 == tag.w2 && rt.w3 == tag.w3;
+            result[rec_i] = ok ? (uint64_t)L : ~(uint64_t)0;
+        } else {
+            store_full(out_p + L, tag);
+        }
+    }
+    phase_stamp(clk, stamps, lane, 8);
+    phase_acc(pa, bstamps, 8);
+    if (!OPEN && supp != nullptr) {
+        /* QUIC header protection after the record (lib/fusion.c:636-650), as in aesgcm_batch_kernel: the
+         * sample may cover the tag written by another lane of this wave */
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        if (lane == 0) {
+            const ptls_hip_supp_t sp = supp[rec_i];
+            if ((sp.flags & PTLS_HIP_SUPP_ENABLE) && sp.hp_key < hp_nslots) {
+                const V4 sample = load_full(out + sp.sample_off);
+                const V4 mk = aes_encrypt<ROUNDS>(lds, lb_aes, hp_slots[sp.hp_key].rk, sample);
+                store_full(mask + sp.mask_off, mk);
+            }
+        }
+    }
+}
+
 /* BYVAL: the plugin's single-record launch (the record by value in the kernel arguments, recs_ord == nullptr); its own
  * instantiation, so the batch one carries none of its prefetch registers.  It runs 256 threads (one wave per SIMD, the
  * whole register file: no spills) since only wave 0 works on the record; the others help build the AES tables. */
@@ -269,255 +534,8 @@ __global__ void __launch_bounds__(WG)
         phase_acc(pa, bstamps, 1);
         const ptls_hip_record_t rec = by_value ? one : recs_ord[pos];
         const uint32_t rec_i = by_value ? 0u : order != nullptr ? order[pos] : pos;
-        const uint32_t key = __builtin_amdgcn_readfirstlane(rec.key);
-        const KeySlot *__restrict__ slot = slots + key;
-        const uint32_t *__restrict__ rk = slot->rk;
-        const uint4 *__restrict__ bs = reinterpret_cast<const uint4 *>(basis) + (size_t)key * BASIS_VECS;
-        const int L = (int)__builtin_amdgcn_readfirstlane(rec.len);
-        const int A = (int)__builtin_amdgcn_readfirstlane(rec.aad_len);
-        const int na = (A + 15) >> 4, nc = (L + 15) >> 4;
-        const int N = na + nc + 1;
-        const bool tflag = !OPEN && (rec.flags & 1u) != 0 && L > 0;
-        const uint32_t ttype = (rec.flags >> 8) & 0xffu;
-        const uint8_t *in_p = in + rec.in_off;
-        uint8_t *out_p = out + rec.out_off;
-        const uint8_t *aad_p = aad + rec.aad_off;
-        const uint32_t n0 = __builtin_amdgcn_readfirstlane(slot->iv[0]),
-                       n1 = __builtin_amdgcn_readfirstlane(slot->iv[1] ^ bswap32((uint32_t)(rec.seq >> 32))),
-                       n2 = __builtin_amdgcn_readfirstlane(slot->iv[2] ^ bswap32((uint32_t)rec.seq));
-        const int iters = (N + 63) >> 6;
-        const bool horner = SPARSE_ABLATE != 3 && iters > 1; /* N <= 64: one element per lane, no Horner step */
-        V4 b[4];
-        /* a single record (the plugin's launch): the H^64 basis loads go out before the counter-mode constants, so their
-         * memory latency overlaps that LDS chain (in batches other waves hide it; there the early loads cost c4s open
-         * 2.5 %, measured) */
-        if (horner && by_value)
-            load_wave_basis(bs + 6 * 128, lane, b); /* H^64 */
-        /* the record (and so its counter-mode constants) is the wave's alone: keep them in SGPRs */
-        CtrConst cc = ctr_const(lds, lb_aes, rk, n0, n1, n2);
-        cc.k10 = __builtin_amdgcn_readfirstlane(cc.k10);
-        cc.k11 = __builtin_amdgcn_readfirstlane(cc.k11);
-        cc.k20 = __builtin_amdgcn_readfirstlane(cc.k20);
-        cc.k21 = __builtin_amdgcn_readfirstlane(cc.k21);
-        cc.k22 = __builtin_amdgcn_readfirstlane(cc.k22);
-        cc.k23 = __builtin_amdgcn_readfirstlane(cc.k23);
-        cc.r03 = __builtin_amdgcn_readfirstlane(cc.r03);
-        phase_stamp(clk, stamps, lane, 2);
-        phase_acc(pa, bstamps, 2);
-        wave_lds_sync(); /* the previous record's Horner reads of the table are done */
-        if (horner) { /* (loading the basis during the previous record's VALU combine measured no faster: other waves hide it) */
-            if (!by_value)
-                load_wave_basis(bs + 6 * 128, lane, b); /* H^64 */
-            store_wave_table(lds, tab, b, lane);
-        }
-        wave_lds_sync();
-        phase_stamp(clk, stamps, lane, 3);
-        phase_acc(pa, bstamps, 3);
-
-        V4 y = V4{0, 0, 0, 0}, ek0 = V4{0, 0, 0, 0};
-        /* generic elements m .. m + NE - 1 of the lane (past `mend`: skipped): partial / AAD / length blocks and
-         * counters >= 2^16, their AES blocks interleaved (counter-mode shortcut unless a counter is that large) */
-        auto generic = [&](auto ne_tag, auto pre_tag, int m, int mend) __attribute__((always_inline)) {
-            constexpr int NE = decltype(ne_tag)::value;
-            constexpr bool USE_PRE = decltype(pre_tag)::value; /* the head range only: pre is dead after it */
-            Elem e[NE];
-            V4 inb[NE], ks[NE];
-            uint32_t cw[NE];
-            int big = 0;
-#pragma unroll
-            for (int b = 0; b < NE; ++b) {
-                e[b] = elem_of(m + b < mend ? lane + (m + b) * 64 : N, N, na, nc, L, N);
-                inb[b] = V4{0, 0, 0, 0};
-                /* the lane's first two elements of a single record were read at the start (pre) */
-                const bool have_pre = USE_PRE && prefetch && m + b < 2;
-                const V4 pv = m + b == 0 ? pre[0] : pre[1];
-                if (e[b].is_c) {
-                    const bool tb = tflag && e[b].c == nc - 1; /* the block holding the content-type byte */
-                    const int nb = e[b].nbytes - (tb ? 1 : 0);
-                    inb[b] = have_pre ? mask_block(pv, nb) : load_block<ALIGNED>(in_p + 16 * (size_t)e[b].c, nb);
-                    if (tb)
-                        inb[b] = put_byte(inb[b], e[b].nbytes - 1, ttype);
-                } else if (e[b].is_aad) { /* loaded before the AES as well, not after it in finish_elem */
-                    const int nb = min(16, A - 16 * e[b].i);
-                    inb[b] = have_pre ? mask_block(pv, nb) : load_block<ALIGNED>(aad_p + 16 * e[b].i, nb);
-                }
-                /* keystream for data block c (counter inc32(J0) + c), E_K(J0) for the length-block lane */
-                cw[b] = e[b].is_c ? bswap32((uint32_t)e[b].c + 2u) : 0x01000000u;
-                ks[b] = V4{n0, n1, n2, cw[b]};
-                big |= (e[b].is_c && e[b].c >= 65534) ? 1 : 0;
-            }
-            if (wave_max(big)) {
-                aes_encrypt_n<ROUNDS, NE>(lds, lb_aes, rk, ks);
-            } else if (!SPARSE_GEN_SKEW) {
-                aes_ctr_n<ROUNDS, NE>(lds, lb_aes, rk, cc, cw, ks);
-            } else {
-                const V4 nohash[NE] = {};
-                V4 ydummy = V4{0, 0, 0, 0};
-                ctr_ghash_skewed<ROUNDS, NE, false>(lds, lb_aes, rk, cc, cw, ks, ydummy, nohash, GhNibble{tab});
-            }
-#pragma unroll
-            for (int b = 0; b < NE; ++b) {
-                const V4 x = finish_elem<OPEN, ALIGNED, true>(e[b], inb[b], ks[b], aad_p, A, L, out_p, ek0);
-                if (m + b == 0)
-                    y = x; /* 0 * P ^ x */
-                else if (SPARSE_ABLATE != 2 && e[b].active)
-                    y = v4xor(gh_mul_nibble(lds, tab, y), x); /* y * H^64 ^ x */
-            }
-        };
-        auto generic_range = [&](auto pre_tag, int m0, int m1) __attribute__((always_inline)) {
-            int m = m0;
-            for (; m + 1 < m1; m += 2)
-                generic(std::integral_constant<int, 2>{}, pre_tag, m, m1);
-            if (m < m1)
-                generic(std::integral_constant<int, 1>{}, pre_tag, m, m1);
-        };
-
-        /* the wave's "pure" elements m in [pm0, pm1): every lane's element is a full data block with a counter below
-         * 2^16 (lane l, element m = data block 64 m + l - na).  There the body is branch-free, KP blocks per lane per
-         * iteration, the counter-mode AES of the blocks skewed against the H^64 multiplies of the previous iteration's
-         * ciphertext (seal) or of the input ciphertext (open), the next iteration's plaintext prefetched. */
-        constexpr int KP = SPARSE_PE;
-        const int nf = (L - (tflag ? 1 : 0)) >> 4;              /* full blocks that are all input bytes */
-        const int lastc = min(nf, 65534) - 1;                   /* last data block allowed in the stretch */
-        /* Each lane starts the stretch at its own first data element (m = 1 on the lanes holding the AAD block, 0 on the
-         * others) and ends where its blocks stop being full: the stretch is the shortest lane's, the AAD elements before
-         * it are hashed only, and the record's generic head (one full AES per lane for one AAD block, 17 % of a c4s
-         * record, tools/sparse_stamps.py) is gone. */
-        const int ml = lane < na ? (na - lane + 63) >> 6 : 0;                          /* the lane's first data element */
-        const int mhl = lastc + na - lane >= 0 ? ((lastc + na - lane) >> 6) + 1 : 0;  /* its elements m < mhl: full blocks */
-        const int npure = SPARSE_PURE ? -wave_max(-max(mhl - ml, 0)) / KP : 0;
-        const int iters_l = lane < N ? ((N - 1 - lane) >> 6) + 1 : 0;                /* the lane's elements */
-        const int pm1 = ml + npure * KP;                                              /* the lane's first after the stretch */
-        if (!npure) { /* head and tail are one range: elements share one round trip to the record's memory (the plugin) */
-            generic_range(std::integral_constant<bool, BYVAL>{}, 0, iters);
-        } else { /* the lane's AAD elements: GHASH only */
-            const int naad = wave_max(ml);
-            for (int j = 0; j < naad; ++j) {
-                if (j < ml) {
-                    const int i = lane + 64 * j;
-                    const int nb = min(16, A - 16 * i);
-                    const V4 x = (BYVAL && prefetch && j < 2) ? mask_block(j == 0 ? pre[0] : pre[1], nb)
-                                                              : load_block<ALIGNED>(aad_p + 16 * i, nb);
-                    y = j == 0 ? x : v4xor(gh_mul_nibble(lds, tab, y), x);
-                }
-            }
-        }
-        phase_stamp(clk, stamps, lane, 4);
-        phase_acc(pa, bstamps, 4);
-        if (npure) {
-            const int c0 = 64 * ml + lane - na; /* the lane's first data block of the stretch */
-            const uint8_t *src = in_p + 16 * (size_t)c0;
-            uint8_t *dst = out_p + 16 * (size_t)c0;
-            V4 pend[KP], bufA[KP], bufB[KP];
-            /* open hashes its input in the iteration that loads it: the next iteration's blocks are prefetched into the
-             * other buffer.  Seal uses its plaintext only after the iteration's AES, so it loads at the top of the
-             * iteration into one buffer (8 VGPRs fewer: the seal instantiations stay within 168 without scratch). */
-#pragma unroll
-            for (int b = 0; b < KP; ++b)
-                bufA[b] = load_full(src + 1024 * b);
-            auto pure_iter = [&](int it, bool hash_pending, V4(&d)[KP], V4(&dn)[KP]) __attribute__((always_inline)) {
-                const size_t o = (size_t)it * KP * 1024;
-                const size_t on = (size_t)min(it + 1, npure - 1) * KP * 1024;
-                V4 k[KP];
-                uint32_t cw[KP];
-#pragma unroll
-                for (int b = 0; b < KP; ++b) {
-                    if (OPEN)
-                        dn[b] = load_full(src + on + 1024 * b);
-                    else if (it != 0)
-                        d[b] = load_full(src + o + 1024 * b);
-                    cw[b] = bswap32((uint32_t)(c0 + 2 + (it * KP + b) * 64));
-                    k[b] = V4{n0, n1, n2, cw[b]};
-                }
-                __builtin_amdgcn_sched_barrier(0); /* keep the loads at the top of the iteration */
-                if (SPARSE_ABLATE == 2) {
-                    ctr_ghash_skewed<ROUNDS, KP, false>(lds, lb_aes, rk, cc, cw, k, y, d, GhNibble{tab});
-#pragma unroll
-                    for (int b = 0; b < KP; ++b) {
-                        pend[b] = v4xor(d[b], k[b]);
-                        store_full(dst + o + 1024 * b, pend[b]);
-                    }
-                } else if (OPEN) {
-                    ctr_ghash_skewed<ROUNDS, KP, true>(lds, lb_aes, rk, cc, cw, k, y, d, GhNibble{tab});
-#pragma unroll
-                    for (int b = 0; b < KP; ++b)
-                        store_full(dst + o + 1024 * b, v4xor(d[b], k[b]));
-                } else {
-                    if (hash_pending)
-                        ctr_ghash_skewed<ROUNDS, KP, true>(lds, lb_aes, rk, cc, cw, k, y, pend, GhNibble{tab});
-                    else
-                        ctr_ghash_skewed<ROUNDS, KP, false>(lds, lb_aes, rk, cc, cw, k, y, pend, GhNibble{tab});
-#pragma unroll
-                    for (int b = 0; b < KP; ++b) {
-                        pend[b] = v4xor(d[b], k[b]);
-                        store_full(dst + o + 1024 * b, pend[b]);
-                    }
-                }
-            };
-            if (OPEN) {
-                pure_iter(0, false, bufA, bufB);
-                int it = 1;
-                for (; it + 1 < npure; it += 2) {
-                    pure_iter(it, true, bufB, bufA);
-                    pure_iter(it + 1, true, bufA, bufB);
-                }
-                if (it < npure)
-                    pure_iter(it, true, bufB, bufA);
-            } else {
-                pure_iter(0, false, bufA, bufA);
-                for (int it = 1; it < npure; ++it)
-                    pure_iter(it, true, bufA, bufA);
-#pragma unroll
-                for (int b = 0; b < KP; ++b)
-                    y = v4xor(gh_mul_nibble(lds, tab, y), pend[b]);
-            }
-        }
-        phase_stamp(clk, stamps, lane, 5);
-        phase_acc(pa, bstamps, 5);
-        if (npure) { /* the rest of each lane's elements from its own position (partial, length and leftover blocks) */
-            const int rest = wave_max(max(iters_l - pm1, 0));
-            int j = 0;
-            for (; j + 1 < rest; j += 2)
-                generic(std::integral_constant<int, 2>{}, std::false_type{}, pm1 + j, iters_l);
-            if (j < rest)
-                generic(std::integral_constant<int, 1>{}, std::false_type{}, pm1 + j, iters_l);
-        }
-        phase_stamp(clk, stamps, lane, 6);
-        phase_acc(pa, bstamps, 6);
-
-        /* lane l's sum times H^(q+1), q = distance of its last element from the end of the GHASH input, on the
-         * VALU; the XOR butterfly then sums the 64 lanes (ghash_combine) */
-        const int q = (N - 1 - lane) & 63;
-        if (SPARSE_ABLATE != 1)
-            y = ghash_combine(bs, q, y);
-        phase_stamp(clk, stamps, lane, 7);
-        phase_acc(pa, bstamps, 7);
-        if (q == 0) {
-            const V4 tag = v4xor(y, ek0);
-            if (OPEN) {
-                const V4 rt = load_block<false>(in_p + L, 16);
-                const bool ok = rt.w0 == tag.w0 && rt.w1 == tag.w1 && rt.w2 == tag.w2 && rt.w3 == tag.w3;
-                result[rec_i] = ok ? (uint64_t)L : ~(uint64_t)0;
-            } else {
-                store_full(out_p + L, tag);
-            }
-        }
-        phase_stamp(clk, stamps, lane, 8);
-        phase_acc(pa, bstamps, 8);
-        if (!OPEN && supp != nullptr) {
-            /* QUIC header protection after the record (lib/fusion.c:636-650), as in aesgcm_batch_kernel: the
-             * sample may cover the tag written by another lane of this wave */
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-            if (lane == 0) {
-                const ptls_hip_supp_t sp = supp[rec_i];
-                if ((sp.flags & PTLS_HIP_SUPP_ENABLE) && sp.hp_key < hp_nslots) {
-                    const V4 sample = load_full(out + sp.sample_off);
-                    const V4 mk = aes_encrypt<ROUNDS>(lds, lb_aes, hp_slots[sp.hp_key].rk, sample);
-                    store_full(mask + sp.mask_off, mk);
-                }
-            }
-        }
+        sparse_record<ROUNDS, OPEN, ALIGNED, BYVAL>(lds, lane, lb_aes, tab, rec, rec_i, in, aad, out, result, slots, basis, supp,
+                                                   hp_slots, hp_nslots, mask, prefetch, pre, clk, stamps, bstamps, pa);
     }
     if (done != nullptr && w0 == 0) {
         /* the by-value record's wave: every store above (the whole wave's, s_waitcnt is wave-wide) reaches system
@@ -544,6 +562,110 @@ __global__ void __launch_bounds__(WG)
         __syncthreads();
         clock_stamp(clk, 1);
     }
+}
+
+/* The plugin worker: one wave stays resident and serves the mailbox (internal.h WorkerSlot, fine-grained pinned host
+ * memory): it polls seq over PCIe, reads the request, runs the record through sparse_record (the single-record path of a
+ * launched call: prefetched first elements, the wave's H^64 table, the VALU combination) or one ECB block, stores the
+ * call's completion word after all its output (system scope) and then `served`.  The AES tables are built once for the
+ * worker's life instead of once per call, and no launch sits between the caller and the kernel.  The wave leaves when
+ * the host asks (quit), after idle_ticks without a request or after life_ticks (100 MHz counter) — so the kernel always
+ * ends, and a stream that shares its hardware queue waits at most life_ticks — storing its epoch in `exited`. */
+__global__ void __launch_bounds__(64)
+    plugin_worker_kernel(WorkerSlot *mb, uint32_t epoch, const uint32_t *__restrict__ t0, uint64_t idle_ticks, uint64_t life_ticks)
+{
+    __shared__ __attribute__((aligned(16))) uint8_t lds[SP_TAB + 8192];
+    const int lane = threadIdx.x & 63;
+    const uint32_t lb_aes = (uint32_t)(lane & 31) * 4u;
+    const uint32_t tab = SP_TAB;
+    build_aes_tables<64>(lds, 0, t0);
+    __syncthreads();
+    WorkerSlot *ms = mb;
+    const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
+    uint64_t t_last = t_start;
+    uint32_t last = __builtin_amdgcn_readfirstlane(__hip_atomic_load(&ms->served, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
+    if (lane == 0)
+        __hip_atomic_store(&ms->started, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    PhaseAcc pa{};
+    for (;;) {
+        const uint32_t seq = __builtin_amdgcn_readfirstlane(__hip_atomic_load(&ms->seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
+        if (seq == last) {
+            const uint32_t quit = __builtin_amdgcn_readfirstlane(__hip_atomic_load(&ms->quit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
+            const uint64_t now = __builtin_amdgcn_s_memrealtime();
+            if (quit != 0 || now - t_last > idle_ticks || now - t_start > life_ticks)
+                break;
+            __builtin_amdgcn_s_sleep(4);
+            continue;
+        }
+        /* the request was written before seq; it sits in fine-grained (uncached) host memory, so ordering the loads is
+         * enough: no cache invalidation (key material is never modified while a worker is resident: engine.cpp
+         * worker_quiesce, so the worker's caches cannot hold a stale key slot) */
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        if (lane == 0)
+            __hip_atomic_store(&ms->seen, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        const WorkerReq &rq = ms->req;
+        const ptls_hip_record_t rec = rq.rec;
+        const uint32_t flags = __builtin_amdgcn_readfirstlane(rq.flags);
+        const uint8_t *in = rq.in, *aad = rq.aad;
+        uint8_t *out = rq.out;
+        const KeySlot *slots = rq.slots;
+        uint32_t *done = rq.done;
+        const uint32_t done_seq = __builtin_amdgcn_readfirstlane(rq.done_seq);
+        if (flags & WREQ_ECB) {
+            const V4 blk = V4{rq.blk[0], rq.blk[1], rq.blk[2], rq.blk[3]};
+            const V4 m = (flags & WREQ_AES256) ? aes_encrypt<14>(lds, lb_aes, slots->rk, blk) : aes_encrypt<10>(lds, lb_aes, slots->rk, blk);
+            if (lane == 0)
+                store_full(out, m);
+        } else {
+            /* the record's first two elements per lane, as the launched single-record kernel reads them */
+            V4 pre[2] = {V4{0, 0, 0, 0}, V4{0, 0, 0, 0}};
+            const int na1 = ((int)rec.aad_len + 15) >> 4, nc1 = ((int)rec.len + 15) >> 4;
+#pragma unroll
+            for (int m = 0; m < 2; ++m) {
+                const int i = lane + 64 * m;
+                if (i < na1)
+                    pre[m] = load_full(aad + rec.aad_off + 16 * (size_t)i);
+                else if (i < na1 + nc1)
+                    pre[m] = load_full(in + rec.in_off + 16 * (size_t)(i - na1));
+            }
+            const ptls_hip_supp_t *supp = rq.supp;
+            const KeySlot *hp_slots = rq.hp_slots;
+            uint8_t *mask = rq.mask;
+            uint64_t *result = rq.result;
+            const uint32_t *basis = rq.basis;
+            const bool open = (flags & WREQ_OPEN) != 0, a256 = (flags & WREQ_AES256) != 0;
+            if (open && a256)
+                sparse_record<14, true, true, true>(lds, lane, lb_aes, tab, rec, 0, in, aad, out, result, slots, basis, supp,
+                                                    hp_slots, 1, mask, true, pre, nullptr, false, false, pa);
+            else if (open)
+                sparse_record<10, true, true, true>(lds, lane, lb_aes, tab, rec, 0, in, aad, out, result, slots, basis, supp,
+                                                    hp_slots, 1, mask, true, pre, nullptr, false, false, pa);
+            else if (a256)
+                sparse_record<14, false, true, true>(lds, lane, lb_aes, tab, rec, 0, in, aad, out, result, slots, basis, supp,
+                                                     hp_slots, 1, mask, true, pre, nullptr, false, false, pa);
+            else
+                sparse_record<10, false, true, true>(lds, lane, lb_aes, tab, rec, 0, in, aad, out, result, slots, basis, supp,
+                                                     hp_slots, 1, mask, true, pre, nullptr, false, false, pa);
+        }
+        /* every store of the call reaches system scope before its completion word; then the slot is free again */
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+        if (lane == 0) {
+            __hip_atomic_store(done, done_seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(&ms->served, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+        last = seq;
+        t_last = __builtin_amdgcn_s_memrealtime();
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+    if (lane == 0)
+        __hip_atomic_store(&ms->exited, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+int launch_plugin_worker(WorkerSlot *mb, uint32_t epoch, const uint32_t *t0, uint64_t idle_ticks, uint64_t life_ticks, void *stream)
+{
+    hipLaunchKernelGGL(plugin_worker_kernel, dim3(1), dim3(64), 0, static_cast<hipStream_t>(stream), mb, epoch, t0, idle_ticks,
+                       life_ticks);
+    return (int)hipGetLastError();
 }
 
 template <int R, bool O, bool BV>

@@ -1,0 +1,110 @@
+"""The plugin worker (engine.cpp worker_call, sparse_kernel.hip plugin_worker_kernel): a resident one-wave kernel that
+serves plugin calls from a pinned mailbox instead of one launch per call.  Its lifecycle is exercised through the
+reference's own picotls lifecycle code (tests/plugin_driver.py) and every output is compared with lib/fusion.c
+(oracle/_ref): calls separated by gaps longer than the worker's idle timeout (it leaves, the next call relaunches it),
+IV changes (ptls_aead_xor_iv: the worker leaves before the key slot's IV is rewritten), contexts created and freed
+between calls (a freed key slot's address comes back with other keys), header-protection ECB blocks interleaved with
+AEAD calls on one worker, and two threads sharing it.  Each case runs in its own process, with the worker on and off
+(PTLS_HIP_PLUGIN_WORKER=0: one launch per call)."""
+import os
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+_CASE = r"""
+import sys, time, threading
+sys.path[:0] = {paths!r}
+import numpy as np
+import plugin_driver
+from oracle_lib import Ref, Oracle, tls_aad
+drv, ref, o = plugin_driver.PluginDriver(), Ref(), Oracle()
+rng = np.random.default_rng(11)
+
+def rnd(n):
+    return rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+
+def check(ctx_e, ctx_d, key, iv, seq, L, tag):
+    pt, aad = rnd(L), tls_aad(L)
+    ct = drv.encrypt(ctx_e, pt, seq, aad)
+    assert ct == ref.seal(key, iv, seq, aad, pt), (tag, seq, L)
+    assert drv.decrypt(ctx_d, ct, seq, aad) == pt, (tag, seq, L)
+
+for bits in (128, 256):
+    key, iv = rnd(bits // 8), rnd(12)
+    enc, dec = drv.new(bits, key, iv, 1), drv.new(bits, key, iv, 0)
+    # gaps longer than the idle timeout (200 us) and the lifetime (2 ms): every call may find the worker gone
+    for i, gap in enumerate((0, 0.0005, 0, 0.003, 0.0002, 0, 0.01, 0)):
+        time.sleep(gap)
+        check(enc, dec, key, iv, i, int(rng.integers(0, 2000)), "gap")
+    # IV changes between back-to-back calls
+    for i in range(6):
+        x = rnd(int(rng.integers(1, 13)))
+        drv.xor_iv(enc, x)
+        drv.xor_iv(dec, x)
+        iv = bytes(a ^ b for a, b in zip(iv, x + bytes(12 - len(x))))
+        check(enc, dec, key, iv, 100 + i, int(rng.integers(0, 1500)), "xor_iv")
+    drv.free(enc)
+    drv.free(dec)
+    # contexts created and freed between calls: slots (and their addresses) change hands under a busy worker
+    for i in range(12):
+        k2, iv2 = rnd(bits // 8), rnd(12)
+        e2, d2 = drv.new(bits, k2, iv2, 1), drv.new(bits, k2, iv2, 0)
+        check(e2, d2, k2, iv2, i, int(rng.integers(0, 600)), "churn")
+        drv.free(e2)
+        drv.free(d2)
+    # header protection: ECB blocks and fused supp calls interleaved with AEAD calls
+    hp_key = rnd(bits // 8)
+    cctx = drv.cipher_new(bits, hp_key)
+    key, iv = rnd(bits // 8), rnd(12)
+    actx = drv.new(bits, key, iv)
+    for i in range(20):
+        civ = rnd(16)
+        assert drv.cipher_encrypt(cctx, civ, bytes(16)) == o.aes_ecb(hp_key, civ), ("ecb", i)
+        L = int(rng.integers(20, 1300))
+        text, aad = rnd(L), rnd(20)
+        out, supp = drv.encrypt_s(actx, text, i, aad, cctx, 3)
+        assert (out, supp) == ref.seal_supp(key, iv, i, aad, text, hp_key, 3), ("supp", i)
+    drv.free(actx)
+    drv.cipher_free(cctx)
+
+# two threads, each with its own contexts, calling through the one worker at once
+errors = []
+def worker_thread(t):
+    try:
+        r = np.random.default_rng(100 + t)
+        key, iv = r.integers(0, 256, 16, dtype=np.uint8).tobytes(), r.integers(0, 256, 12, dtype=np.uint8).tobytes()
+        e, d = drv.new(128, key, iv, 1), drv.new(128, key, iv, 0)
+        for i in range(150):
+            L = int(r.integers(0, 1500))
+            pt, aad = r.integers(0, 256, L, dtype=np.uint8).tobytes(), tls_aad(L)
+            ct = drv.encrypt(e, pt, i, aad)
+            assert ct == ref.seal(key, iv, i, aad, pt), ("thread", t, i)
+            assert drv.decrypt(d, ct, i, aad) == pt, ("thread", t, i)
+        drv.free(e)
+        drv.free(d)
+    except Exception as ex:  # noqa: BLE001
+        errors.append(repr(ex))
+ts = [threading.Thread(target=worker_thread, args=(t,)) for t in range(2)]
+for t in ts:
+    t.start()
+for t in ts:
+    t.join()
+assert not errors, errors
+print("ok")
+"""
+
+
+@pytest.mark.parametrize("worker", ["1", "0"])
+def test_plugin_worker_lifecycle(worker):
+    from oracle_lib import Ref
+    if not Ref.available:
+        pytest.skip("oracle/_ref not built")
+    paths = [os.path.join(ROOT, "tests"), os.path.join(ROOT, "hsig-picotls_amd"), ROOT]
+    env = dict(os.environ, PTLS_HIP_PLUGIN_WORKER=worker)
+    r = subprocess.run([sys.executable, "-c", _CASE.format(paths=paths)], env=env, capture_output=True, text=True,
+                       timeout=240)
+    assert r.returncode == 0 and r.stdout.strip().endswith("ok"), (r.returncode, r.stdout[-2000:], r.stderr[-3000:])

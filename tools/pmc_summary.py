@@ -8,13 +8,18 @@ from collections import defaultdict
 
 out = sys.argv[1]
 vals = defaultdict(list)
+sys.path.insert(0, __import__("os").path.dirname(__import__("os").path.abspath(__file__)))
+from bench_dispatches import bench_dispatches  # noqa: E402
 for f in sorted(glob.glob(f"{out}/pass*/run_counter_collection.csv")):
-    rows = [r for r in csv.DictReader(open(f)) if r["Kernel_Name"].startswith("aesgcm")]
-    ids = sorted({int(r["Dispatch_Id"]) for r in rows})
-    seal_ids = set(ids[0::2])  # seal, open, seal, open, ...
-    for r in rows:
-        if int(r["Dispatch_Id"]) in seal_ids:
-            vals[r["Counter_Name"]].append(float(r["Counter_Value"]))
+    rows = list(csv.DictReader(open(f)))
+    names = {r["Counter_Name"] for r in rows}
+    key = "GRBM_GUI_ACTIVE" if "GRBM_GUI_ACTIVE" in names else sorted(names)[0] if names else None
+    if key is None:
+        continue
+    seal, _ = bench_dispatches(f, key)
+    for v in seal:
+        for c, x in v.items():
+            vals[c].append(x)
 avg = {k: sum(v) / len(v) for k, v in vals.items()}
 for k in sorted(avg):
     print(f"{k:28s} {avg[k]:18.1f}")

@@ -9,15 +9,12 @@ out, cfg = sys.argv[1], sys.argv[2]
 
 
 def per_launch(counter):
+    """average counter value per seal and per open launch of the bench's own dispatches (tools/bench_dispatches.py)"""
+    sys.path.insert(0, __import__("os").path.dirname(__import__("os").path.abspath(__file__)))
+    from bench_dispatches import bench_dispatches
     f = glob.glob(f"{out}/pmc_{counter}/**/run_counter_collection.csv", recursive=True)
-    rows = [r for r in csv.DictReader(open(f[0])) if r["Kernel_Name"].startswith(("aesgcm_batch_kernel", "aesgcm_sparse_kernel"))]
-    ids = sorted({int(r["Dispatch_Id"]) for r in rows})
-    by = {}
-    for r in rows:
-        by[int(r["Dispatch_Id"])] = by.get(int(r["Dispatch_Id"]), 0.0) + float(r["Counter_Value"])
-    seal = [by[i] for i in ids[0::2]]
-    opn = [by[i] for i in ids[1::2]]
-    return sum(seal) / len(seal), sum(opn) / len(opn)
+    seal, opn = bench_dispatches(f[0], counter)
+    return sum(v[counter] for v in seal) / len(seal), sum(v[counter] for v in opn) / len(opn)
 
 
 def bench_line(log):
