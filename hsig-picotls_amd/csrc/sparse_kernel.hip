@@ -597,10 +597,12 @@ __global__ void __launch_bounds__(64)
             __builtin_amdgcn_s_sleep(4);
             continue;
         }
-        /* the request was written before seq; it sits in fine-grained (uncached) host memory, so ordering the loads is
-         * enough: no cache invalidation (key material is never modified while a worker is resident: engine.cpp
-         * worker_quiesce, so the worker's caches cannot hold a stale key slot) */
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        /* the request (and the record in the caller's pinned staging) was written before seq.  Ordering the loads is not
+         * enough: the vector L1 keeps the previous request's lines at the same addresses (measured: a workgroup-scope
+         * acquire served request 2 with request 1's completion pointer), so the acquire is at system scope, which
+         * invalidates the L1 and the L2's lines of host memory.  Device key material is never modified while a worker is
+         * resident (engine.cpp worker_quiesce), so no cache can hold a stale key slot. */
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
         if (lane == 0)
             __hip_atomic_store(&ms->seen, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         const WorkerReq &rq = ms->req;
