@@ -759,6 +759,117 @@ __device__ __forceinline__ V4 gf_mul_valu(V4 xr, V4 yr)
     return V4{bswap32(z0), bswap32(z1), bswap32(z2), bswap32(z3)};
 }
 
+/* v * x in GF(2^128) on big-endian words (bit 0 of the GCM string = bit 31 of v[0]) */
+__device__ __forceinline__ void mulx_be(uint32_t (&v)[4])
+{
+    const uint32_t c = (uint32_t)__builtin_amdgcn_sbfe((int)v[3], 0u, 1u);
+    v[3] = __builtin_amdgcn_alignbit(v[2], v[3], 1);
+    v[2] = __builtin_amdgcn_alignbit(v[1], v[2], 1);
+    v[1] = __builtin_amdgcn_alignbit(v[0], v[1], 1);
+    v[0] = (v[0] >> 1) ^ (c & 0xe1000000u);
+}
+
+/* x * y in GF(2^128), GCM bit order, both operands per lane: gf_mul_valu's product with 4-bit windows over x (Shoup)
+ * and a per-lane table of y in LDS instead of 128 single-bit steps.
+ *   T[n] = n3 y + n2 y x + n1 y x^2 + n0 y x^3 (n3 = the nibble's first GCM bit); lane l keeps its NT entries at
+ *   tab + l * NT * 16, entry n in slot (n + l) mod NT, so the 8 lanes of a ds_write_b128 group hit 8 bank quads.
+ *   NT = 8 holds T[0..7] and folds n3 y in on the VALU (8 KiB per wave: the sparse kernel's per-wave table area).
+ *   Z = T[nib_31]; Z = Z x^4 + T[nib_j] for j = 30 .. 0.  The 4 bits each shift drops (positions 128..131) are
+ *   collected in one overflow word and folded back every 8 shifts with x^128 = 1 + x + x^2 + x^7.
+ * About 500 VALU + NT ds_write_b128 + 32 ds_read_b128 against gf_mul_valu's 1 408 VALU.  The caller owns the table
+ * area; the wave's LDS operations complete in order, so no barrier is needed around it. */
+template <int NT>
+struct Win4 {
+    uint32_t base, rot; /* the lane's table and its slot rotation */
+    uint32_t y[4];      /* NT = 8: y itself (big-endian words), folded in for the nibble's first bit */
+};
+
+template <int NT>
+__device__ __forceinline__ Win4<NT> gf_win4_build(uint8_t *lds, uint32_t tab, int lane, V4 yr)
+{
+    static_assert(NT == 8 || NT == 16, "4-bit windows: 8 or 16 table entries per lane");
+    uint32_t m[4][4]; /* m[k] = y x^k */
+    m[0][0] = bswap32(yr.w0), m[0][1] = bswap32(yr.w1), m[0][2] = bswap32(yr.w2), m[0][3] = bswap32(yr.w3);
+#pragma unroll
+    for (int k = 1; k < 4; ++k) {
+#pragma unroll
+        for (int w = 0; w < 4; ++w)
+            m[k][w] = m[k - 1][w];
+        mulx_be(m[k]);
+    }
+    Win4<NT> t;
+    uint32_t ln = (uint32_t)lane;
+    asm volatile("" : "+v"(ln)); /* keeps the lane's slot arithmetic here: hoisted out of a record loop, its 8-16 values
+                                    stay live across the whole kernel (the sparse batch kernel spilled 200 B per lane) */
+    t.base = tab + ln * (uint32_t)(NT * 16);
+    t.rot = ln & (uint32_t)(NT - 1);
+#pragma unroll
+    for (int w = 0; w < 4; ++w)
+        t.y[w] = m[0][w];
+#pragma unroll
+    for (int n = 0; n < NT; ++n) {
+        uint32_t e[4] = {0, 0, 0, 0};
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            if ((n >> (3 - k)) & 1)
+#pragma unroll
+                for (int w = 0; w < 4; ++w)
+                    e[w] ^= m[k][w];
+        lds128_store(lds, t.base + (((uint32_t)n + t.rot) & (uint32_t)(NT - 1)) * 16u, V4{e[0], e[1], e[2], e[3]});
+    }
+    return t;
+}
+
+template <int NT, int LB = 8>
+__device__ __forceinline__ V4 gf_win4_mul(const uint8_t *lds, const Win4<NT> &tb, V4 xr)
+{
+    static_assert(LB == 8 || LB == 4 || LB == 2, "lookups in flight: 8, 4 or 2");
+    const uint32_t x[4] = {bswap32(xr.w0), bswap32(xr.w1), bswap32(xr.w2), bswap32(xr.w3)};
+    uint32_t z0 = 0, z1 = 0, z2 = 0, z3 = 0, ov = 0;
+#pragma unroll
+    for (int g = 0; g < 32 / LB; ++g) { /* nibbles j = 31 - g LB down to 32 - (g + 1) LB */
+        const int j0 = 31 - g * LB, w = j0 >> 3, i0 = 8 * w + 7 - j0;
+        V4 t[LB];
+#pragma unroll
+        for (int ii = 0; ii < LB; ++ii) { /* nibble j = 8 w + 7 - i: bits 4 i .. 4 i + 3 from the bottom of word w */
+            const int i = i0 + ii;
+            const uint32_t nib = (x[w] >> (4 * i)) & 15u;
+            t[ii] = lds128(lds, tb.base + ((nib + tb.rot) & (uint32_t)(NT - 1)) * 16u);
+            if (NT == 8) {
+                const uint32_t mk = 0u - (nib >> 3);
+                t[ii] = V4{t[ii].w0 ^ (mk & tb.y[0]), t[ii].w1 ^ (mk & tb.y[1]), t[ii].w2 ^ (mk & tb.y[2]), t[ii].w3 ^ (mk & tb.y[3])};
+            }
+        }
+#pragma unroll
+        for (int ii = 0; ii < LB; ++ii) {
+            const int j = 8 * w + 7 - (i0 + ii);
+            if (j != 31) { /* Z * x^4, the dropped nibble into the overflow word */
+                ov = __builtin_amdgcn_alignbit(z3, ov, 4);
+                z3 = __builtin_amdgcn_alignbit(z2, z3, 4);
+                z2 = __builtin_amdgcn_alignbit(z1, z2, 4);
+                z1 = __builtin_amdgcn_alignbit(z0, z1, 4);
+                z0 >>= 4;
+                if (((31 - j) & 7) == 0) { /* 8 shifts: positions 128..159 folded back */
+                    z0 ^= ov ^ (ov >> 1) ^ (ov >> 2) ^ (ov >> 7);
+                    z1 ^= (ov << 31) ^ (ov << 30) ^ (ov << 25);
+                    ov = 0;
+                }
+            }
+            z0 ^= t[ii].w0, z1 ^= t[ii].w1, z2 ^= t[ii].w2, z3 ^= t[ii].w3;
+        }
+        __builtin_amdgcn_sched_barrier(0); /* LB lookups in flight at a time (4 LB VGPRs) */
+    }
+    z0 ^= ov ^ (ov >> 1) ^ (ov >> 2) ^ (ov >> 7); /* the last 7 shifts' bits */
+    z1 ^= (ov << 31) ^ (ov << 30) ^ (ov << 25);
+    return V4{bswap32(z0), bswap32(z1), bswap32(z2), bswap32(z3)};
+}
+
+template <int NT, int LB = 8>
+__device__ __forceinline__ V4 gf_mul_win4(uint8_t *lds, uint32_t tab, int lane, V4 xr, V4 yr)
+{
+    return gf_win4_mul<NT, LB>(lds, gf_win4_build<NT>(lds, tab, lane, yr), xr);
+}
+
 /* ---------------- table construction in LDS ---------------- */
 
 __device__ __forceinline__ V4 ld_basis(const uint32_t *b, int e)

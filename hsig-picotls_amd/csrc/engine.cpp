@@ -1941,19 +1941,30 @@ static void worker_atexit(void)
         std::this_thread::yield();
 }
 
-/* under w.mu: the worker's mailbox and stream on the plugin engine's device, and a resident worker */
-static bool worker_launch(PluginWorker &w)
+/* under w.mu: the worker's mailbox (fine-grained pinned host memory) and stream on the plugin engine's device */
+static WorkerSlot *worker_mailbox(PluginWorker &w)
 {
     if (w.h_mb == nullptr) {
         void *d = nullptr;
+        WorkerSlot *h = nullptr;
         if (hipStreamCreateWithFlags(&w.stream, hipStreamNonBlocking) != hipSuccess ||
-            hipHostMalloc(&w.h_mb, sizeof(WorkerSlot), hipHostMallocCoherent) != hipSuccess ||
-            hipHostGetDevicePointer(&d, w.h_mb, 0) != hipSuccess)
-            return false;
-        std::memset(w.h_mb, 0, sizeof(WorkerSlot));
+            hipHostMalloc(reinterpret_cast<void **>(&h), sizeof(WorkerSlot), hipHostMallocCoherent) != hipSuccess ||
+            hipHostGetDevicePointer(&d, h, 0) != hipSuccess) {
+            g_err = "plugin worker mailbox";
+            plugin_die("worker_mailbox");
+        }
+        std::memset(h, 0, sizeof(WorkerSlot));
+        w.h_mb = h;
         w.d_mb = static_cast<WorkerSlot *>(d);
         atexit(worker_atexit);
     }
+    return w.h_mb;
+}
+
+/* under w.mu: a resident worker */
+static bool worker_launch(PluginWorker &w)
+{
+    worker_mailbox(w);
     /* a worker that has not left yet keeps serving: a second one on the same mailbox would serve its requests twice */
     if (w.launched && load_acquire(&w.h_mb->exited) != w.epoch)
         return true;
@@ -2311,6 +2322,10 @@ static uint64_t plugin_run(hip_aead_state *st, bool open, void *output, const vo
     DeviceGuard g(st->eng->device);
     const size_t in_len = open ? len + 16 : len;
     state_reserve(st, in_len, aadlen);
+    /* through the worker, a record that fits goes inline into the mailbox instead of the context's staging */
+    const size_t aad_pad = (aadlen + 15) & ~(size_t)15;
+    const bool use_worker = worker_enabled() && !STAMP_PHASES;
+    const bool inline_rec = use_worker && aad_pad + in_len <= (size_t)WORKER_DATA;
     if (st->iv_dirty) {
         if (ptls_hip_keyset_set_iv(st->ks, 0, st->iv, st->stream) != 0)
             plugin_die("set_iv");
@@ -2324,15 +2339,21 @@ static uint64_t plugin_run(hip_aead_state *st, bool open, void *output, const vo
     rec.aad_len = (uint32_t)aadlen;
     const ptls_hip_supp_t sp{ps != nullptr ? ps->sample_off : 0, 0, 0, PTLS_HIP_SUPP_ENABLE};
     std::memcpy(st->h_stage + ST_SUPP, &sp, sizeof(sp));
-    if (tag != nullptr) { /* open with a detached tag (ptls_fusion_aesgcm_decrypt, lib/fusion.c:660-661) */
-        if (len != 0)
-            std::memcpy(h_in, input, len);
-        std::memcpy(h_in + len, tag, 16);
-    } else if (in_len != 0) {
-        std::memcpy(h_in, input, in_len);
-    }
-    if (aadlen != 0)
-        std::memcpy(h_aad, aad, aadlen);
+    /* the record's input (with a detached tag: ptls_fusion_aesgcm_decrypt, lib/fusion.c:660-661) and AAD into pinned
+     * memory the kernel reads */
+    auto stage = [&](uint8_t *dst_in, uint8_t *dst_aad) {
+        if (tag != nullptr) {
+            if (len != 0)
+                std::memcpy(dst_in, input, len);
+            std::memcpy(dst_in + len, tag, 16);
+        } else if (in_len != 0) {
+            std::memcpy(dst_in, input, in_len);
+        }
+        if (aadlen != 0)
+            std::memcpy(dst_aad, aad, aadlen);
+    };
+    if (!inline_rec)
+        stage(h_in, h_aad);
     KernelArgs a{};
     a.one = rec; /* by value in the kernel arguments (recs_ord stays null): the kernel's first dependent host read is
                     the record's own bytes */
@@ -2351,7 +2372,7 @@ static uint64_t plugin_run(hip_aead_state *st, bool open, void *output, const vo
     }
     a.done = reinterpret_cast<uint32_t *>(st->d_stage + ST_DONE);
     a.done_seq = ++st->done_seq;
-    if (worker_enabled() && !STAMP_PHASES) {
+    if (use_worker) {
         WorkerReq rq{};
         rq.rec = rec;
         rq.in = a.in;
@@ -2368,7 +2389,17 @@ static uint64_t plugin_run(hip_aead_state *st, bool open, void *output, const vo
         rq.flags = (open ? WREQ_OPEN : 0u) | (st->ks->key_size == 32 ? WREQ_AES256 : 0u);
         std::lock_guard<std::mutex> lk(g_worker.mu);
         g_worker.eng = st->eng;
+        if (inline_rec) {
+            WorkerSlot *mb = worker_mailbox(g_worker);
+            stage(mb->data + aad_pad, mb->data);
+            rq.rec.aad_off = 0;
+            rq.rec.in_off = aad_pad;
+            rq.in = rq.aad = g_worker.d_mb->data;
+            rq.flags |= WREQ_INLINE;
+        }
         worker_call(rq, st->h_stage + ST_DONE);
+        if (inline_rec) /* the record's bytes do not stay in the mailbox */
+            std::memset(g_worker.h_mb->data, 0, aad_pad + in_len);
     } else {
 #if STAMP_PHASES
         if (g_diag_stamps == nullptr)
@@ -2393,7 +2424,8 @@ static uint64_t plugin_run(hip_aead_state *st, bool open, void *output, const vo
     if (ps != nullptr)
         std::memcpy(ps->output, st->h_stage + ST_MASK, 16);
     /* the record's bytes do not stay in the staging */
-    std::memset(h_in, 0, in_len);
+    if (!inline_rec)
+        std::memset(h_in, 0, in_len);
     std::memset(h_out, 0, open ? len : len + 16);
     return result;
 }

@@ -133,7 +133,11 @@ struct KernelArgs {
  * plugin's single-record calls from a mailbox in fine-grained pinned host memory instead of one kernel launch per call.
  * The host writes the request, then (release) seq; the wave serves it, stores the call's completion word (as a launched
  * call's kernel does), then `served`. */
-enum : uint32_t { WREQ_OPEN = 1, WREQ_AES256 = 2, WREQ_ECB = 4 };
+enum : uint32_t { WREQ_OPEN = 1, WREQ_AES256 = 2, WREQ_ECB = 4, WREQ_INLINE = 8 };
+/* WREQ_INLINE: the record sits in the mailbox's data area (AAD padded to 16 bytes, then the input: element i of the GHASH
+ * input at data + 16 i), read in the same PCIe round trip as the request.  Records that do not fit stay in the caller's
+ * pinned staging. */
+constexpr int WORKER_DATA = 16384 + 512;
 struct WorkerReq {
     ptls_hip_record_t rec;    /* by value: offsets into in / aad / out */
     const uint8_t *in, *aad;  /* device addresses of the context's pinned staging */
@@ -161,8 +165,10 @@ struct WorkerSlot {
     uint32_t seen;    /* worker -> host: the last request number it read (diagnostics) */
     uint32_t pad1[28];
     WorkerReq req;
+    uint8_t data[WORKER_DATA]; /* WREQ_INLINE records */
 };
-static_assert(sizeof(WorkerSlot) == 448, "WorkerSlot: seq / quit, served / exited, request on separate 128-B lines");
+static_assert(sizeof(WorkerSlot) == 448 + WORKER_DATA, "WorkerSlot: seq / quit, served / exited, request on separate 128-B lines");
+static_assert(__builtin_offsetof(WorkerSlot, quit) == 4, "the worker polls {seq, quit} as one 8-byte word");
 
 /* host-side launchers, defined next to the kernels (aesgcm_kernels.hip, batch_g*.hip) */
 int launch_plugin_worker(WorkerSlot *mb, uint32_t epoch, const uint32_t *t0, uint64_t idle_ticks, uint64_t life_ticks, void *stream);

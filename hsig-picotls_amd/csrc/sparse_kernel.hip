@@ -147,6 +147,8 @@ __device__ __forceinline__ void store_wave_table(uint8_t *lds, uint32_t tab, V4 
         b[1] = mulx_raw(b[2]);
         b[0] = mulx_raw(b[1]);
     }
+    asm volatile("" : "+v"(lane)); /* the entries' masks and slots are computed here, not hoisted out of the record loop
+                                      (32 lane-invariant values live across the kernel: scratch beside the lane combination) */
     const int p = lane >> 1;
     const V4 hi = (lane & 1) ? b[3] : V4{0, 0, 0, 0};
     const uint32_t row = tab + (uint32_t)p * 256u + (uint32_t)(lane & 1) * 128u;
@@ -172,12 +174,17 @@ __device__ __forceinline__ void store_wave_table(uint8_t *lds, uint32_t tab, V4 
     }
 }
 
-/* sum over the wave of (lane's GHASH sum) * H^(q+1): one VALU multiply by the lane's own power (keysetup's
- * H^1..H^64 table), then an XOR butterfly; every lane ends with the total */
-__device__ __forceinline__ V4 ghash_combine(const uint4 *__restrict__ bs, int q, V4 y)
+#ifndef SPARSE_WIN
+#define SPARSE_WIN 1 /* the lane combination's multiply: 1 = 4-bit windows over a per-lane table in LDS (gf_mul_win4, ~500 VALU
+                        + 8 / 16 stores + 32 lookups), 0 = gf_mul_valu (1 408 VALU) */
+#endif
+#ifndef SPARSE_WIN_LB
+#define SPARSE_WIN_LB 4 /* the batch instantiations' lookups in flight per group (8: 32 VGPRs, spills at 168) */
+#endif
+
+/* XOR butterfly over the wave: every lane ends with the sum of the 64 lanes' values */
+__device__ __forceinline__ V4 wave_xor(V4 z)
 {
-    const uint4 hp = bs[NPOW * 128 + q]; /* H^(q+1) */
-    V4 z = gf_mul_valu(y, V4{hp.x, hp.y, hp.z, hp.w});
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
         z.w0 ^= __shfl_xor(z.w0, o, 64);
@@ -186,6 +193,19 @@ __device__ __forceinline__ V4 ghash_combine(const uint4 *__restrict__ bs, int q,
         z.w3 ^= __shfl_xor(z.w3, o, 64);
     }
     return z;
+}
+
+/* sum over the wave of (lane's GHASH sum) * H^(q+1): one multiply by the lane's own power (keysetup's H^1..H^64 table),
+ * then the XOR butterfly; every lane ends with the total.  SPARSE_WIN: the multiply's table is the lane's 8 multiples of
+ * H^(q+1) in the wave's own 8 KiB table area (the H^64 Horner table is dead by now). */
+__device__ __forceinline__ V4 ghash_combine(uint8_t *lds, uint32_t tab, int lane, const uint4 *__restrict__ bs, int q, V4 y)
+{
+    /* q made opaque here: the power's load and the table arithmetic stay after the record's elements instead of being
+     * hoisted above the stretch (where their registers pushed the batch instantiations into scratch) */
+    asm volatile("" : "+v"(q));
+    const uint4 hp = bs[NPOW * 128 + q]; /* H^(q+1) */
+    const V4 p = V4{hp.x, hp.y, hp.z, hp.w};
+    return wave_xor(SPARSE_WIN ? gf_mul_win4<8, SPARSE_WIN_LB>(lds, tab, lane, y, p) : gf_mul_valu(y, p));
 }
 
 /* One record on one wave (the sparse-key kernel's per-record body, also the plugin worker's): its counter-mode
@@ -198,7 +218,8 @@ __device__ __forceinline__ void sparse_record(uint8_t *lds, int lane, uint32_t l
                                               uint64_t *__restrict__ result, const KeySlot *__restrict__ slots,
                                               const uint32_t *__restrict__ basis, const ptls_hip_supp_t *__restrict__ supp,
                                               const KeySlot *__restrict__ hp_slots, uint32_t hp_nslots, uint8_t *mask, bool prefetch,
-                                              const V4 (&pre)[2], uint64_t *__restrict__ clk, bool stamps, bool bstamps, PhaseAcc &pa)
+                                              const V4 (&pre)[2], uint64_t *__restrict__ clk, bool stamps, bool bstamps, PhaseAcc &pa,
+                                              uint32_t ctab)
 {
     constexpr bool by_value = BYVAL;
     (void)by_value, (void)clk, (void)stamps, (void)bstamps, (void)pa;
@@ -224,6 +245,13 @@ __device__ __forceinline__ void sparse_record(uint8_t *lds, int lane, uint32_t l
     /* a single record (the plugin's launch): the H^64 basis loads go out before the counter-mode constants, so their
      * memory latency overlaps that LDS chain (in batches other waves hide it; there the early loads cost c4s open
      * 2.5 %, measured) */
+    const int q = (N - 1 - lane) & 63;
+    /* a single record builds its lane-combination table (the 16 multiples of H^(q+1)) early, in an LDS area of its own
+     * (ctab), so that only the lookups remain after its last element */
+    constexpr bool early_win = BYVAL && SPARSE_WIN;
+    uint4 hpe = uint4{0, 0, 0, 0};
+    if (early_win)
+        hpe = bs[NPOW * 128 + q]; /* H^(q+1) */
     if (horner && by_value)
         load_wave_basis(bs + 6 * 128, lane, b); /* H^64 */
     /* the record (and so its counter-mode constants) is the wave's alone: keep them in SGPRs */
@@ -235,6 +263,10 @@ __device__ __forceinline__ void sparse_record(uint8_t *lds, int lane, uint32_t l
     cc.k22 = __builtin_amdgcn_readfirstlane(cc.k22);
     cc.k23 = __builtin_amdgcn_readfirstlane(cc.k23);
     cc.r03 = __builtin_amdgcn_readfirstlane(cc.r03);
+    Win4<16> w4{};
+    if (early_win)
+        w4 = gf_win4_build<16>(lds, ctab, lane, V4{hpe.x, hpe.y, hpe.z, hpe.w});
+    (void)w4, (void)ctab;
     phase_stamp(clk, stamps, lane, 2);
     phase_acc(pa, bstamps, 2);
     wave_lds_sync(); /* the previous record's Horner reads of the table are done */
@@ -420,9 +452,12 @@ __device__ __forceinline__ void sparse_record(uint8_t *lds, int lane, uint32_t l
 
     /* lane l's sum times H^(q+1), q = distance of its last element from the end of the GHASH input, on the
      * VALU; the XOR butterfly then sums the 64 lanes (ghash_combine) */
-    const int q = (N - 1 - lane) & 63;
-    if (SPARSE_ABLATE != 1)
-        y = ghash_combine(bs, q, y);
+    if (SPARSE_ABLATE != 1) {
+        if (early_win)
+            y = wave_xor(gf_win4_mul<16>(lds, w4, y));
+        else
+            y = ghash_combine(lds, tab, lane, bs, q, y);
+    }
     phase_stamp(clk, stamps, lane, 7);
     phase_acc(pa, bstamps, 7);
     if (q == 0) {
@@ -534,8 +569,9 @@ __global__ void __launch_bounds__(WG)
         phase_acc(pa, bstamps, 1);
         const ptls_hip_record_t rec = by_value ? one : recs_ord[pos];
         const uint32_t rec_i = by_value ? 0u : order != nullptr ? order[pos] : pos;
+        /* a single record's wave 0 takes the unused table areas of waves 1 and 2 for its lane-combination table */
         sparse_record<ROUNDS, OPEN, ALIGNED, BYVAL>(lds, lane, lb_aes, tab, rec, rec_i, in, aad, out, result, slots, basis, supp,
-                                                   hp_slots, hp_nslots, mask, prefetch, pre, clk, stamps, bstamps, pa);
+                                                   hp_slots, hp_nslots, mask, prefetch, pre, clk, stamps, bstamps, pa, SP_TAB + 8192u);
     }
     if (done != nullptr && w0 == 0) {
         /* the by-value record's wave: every store above (the whole wave's, s_waitcnt is wave-wide) reaches system
@@ -566,15 +602,27 @@ __global__ void __launch_bounds__(WG)
 
 /* The plugin worker: one wave stays resident and serves the mailbox (internal.h WorkerSlot, fine-grained pinned host
  * memory): it polls seq over PCIe, reads the request, runs the record through sparse_record (the single-record path of a
- * launched call: prefetched first elements, the wave's H^64 table, the VALU combination) or one ECB block, stores the
- * call's completion word after all its output (system scope) and then `served`.  The AES tables are built once for the
- * worker's life instead of once per call, and no launch sits between the caller and the kernel.  The wave leaves when
- * the host asks (quit), after idle_ticks without a request or after life_ticks (100 MHz counter) — so the kernel always
- * ends, and a stream that shares its hardware queue waits at most life_ticks — storing its epoch in `exited`. */
+ * launched call: prefetched first elements, the wave's H^64 table, the early lane-combination table) or one ECB block,
+ * stores the call's completion word after all its output (system scope) and then `served`.  The AES tables are built
+ * once for the worker's life instead of once per call, and no launch sits between the caller and the kernel.
+ *   - Polling keeps WORKER_POLLS loads of {seq, quit} in flight (a PCIe read takes ~2 us): a new request is seen about one
+ *     read latency after it is written, not up to two.
+ *   - A record the host put inline (WREQ_INLINE: AAD padded to 16 bytes, then the input, in the mailbox's data area) is
+ *     read in the same round trip as the request: the first two elements of every lane lie at fixed offsets there.
+ * The wave leaves when the host asks (quit), after idle_ticks without a request or after life_ticks (100 MHz counter) —
+ * so the kernel always ends, and a stream that shares its hardware queue waits at most life_ticks — storing its epoch
+ * in `exited`. */
+constexpr int WORKER_POLLS = 4;
+
+__device__ __forceinline__ uint64_t poll_word(const WorkerSlot *ms)
+{
+    return __hip_atomic_load(reinterpret_cast<const uint64_t *>(&ms->seq), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 __global__ void __launch_bounds__(64)
     plugin_worker_kernel(WorkerSlot *mb, uint32_t epoch, const uint32_t *__restrict__ t0, uint64_t idle_ticks, uint64_t life_ticks)
 {
-    __shared__ __attribute__((aligned(16))) uint8_t lds[SP_TAB + 8192];
+    __shared__ __attribute__((aligned(16))) uint8_t lds[SP_TAB + 8192 + 16384];
     const int lane = threadIdx.x & 63;
     const uint32_t lb_aes = (uint32_t)(lane & 31) * 4u;
     const uint32_t tab = SP_TAB;
@@ -587,25 +635,45 @@ __global__ void __launch_bounds__(64)
     if (lane == 0)
         __hip_atomic_store(&ms->started, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     PhaseAcc pa{};
-    for (;;) {
-        const uint32_t seq = __builtin_amdgcn_readfirstlane(__hip_atomic_load(&ms->seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
-        if (seq == last) {
-            const uint32_t quit = __builtin_amdgcn_readfirstlane(__hip_atomic_load(&ms->quit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
+    uint64_t ring[WORKER_POLLS];
+#pragma unroll
+    for (int k = 0; k < WORKER_POLLS; ++k) {
+        ring[k] = poll_word(ms);
+        __builtin_amdgcn_s_sleep(8);
+    }
+    bool leave = false;
+    while (!leave) {
+        uint32_t seq = last;
+#pragma unroll
+        for (int k = 0; k < WORKER_POLLS; ++k) { /* the oldest read in flight (vmcnt retires in order), then a new one */
+            const uint64_t v = ring[k];
+            const uint32_t s = __builtin_amdgcn_readfirstlane((uint32_t)v), quit = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+            /* a read issued before the last request was served may still return the one before it: only a later
+             * request number counts (the host numbers them consecutively) */
+            if (seq == last && (int32_t)(s - last) > 0)
+                seq = s;
             const uint64_t now = __builtin_amdgcn_s_memrealtime();
-            if (quit != 0 || now - t_last > idle_ticks || now - t_start > life_ticks)
-                break;
-            __builtin_amdgcn_s_sleep(4);
-            continue;
+            if (seq == last && (quit != 0 || now - t_last > idle_ticks || now - t_start > life_ticks))
+                leave = true;
+            ring[k] = poll_word(ms);
+            __builtin_amdgcn_s_sleep(2);
         }
-        /* the request (and the record in the caller's pinned staging) was written before seq.  Ordering the loads is not
-         * enough: the vector L1 keeps the previous request's lines at the same addresses (measured: a workgroup-scope
-         * acquire served request 2 with request 1's completion pointer), so the acquire is at system scope, which
-         * invalidates the L1 and the L2's lines of host memory.  Device key material is never modified while a worker is
-         * resident (engine.cpp worker_quiesce), so no cache can hold a stale key slot. */
+        if (leave || seq == last)
+            continue;
+        /* the request (and the record, inline or in the caller's pinned staging) was written before seq.  Ordering the
+         * loads is not enough: the vector L1 keeps the previous request's lines at the same addresses (measured: a
+         * workgroup-scope acquire served request 2 with request 1's completion pointer), so the acquire is at system
+         * scope, which invalidates the L1 and the L2's lines of host memory.  Device key material is never modified
+         * while a worker is resident (engine.cpp worker_quiesce), so no cache can hold a stale key slot. */
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
         if (lane == 0)
             __hip_atomic_store(&ms->seen, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         const WorkerReq &rq = ms->req;
+        /* an inline record's first two elements per lane, loaded with the request (unused otherwise) */
+        V4 pin[2];
+#pragma unroll
+        for (int m = 0; m < 2; ++m)
+            pin[m] = load_full(ms->data + 16 * (size_t)(lane + 64 * m));
         const ptls_hip_record_t rec = rq.rec;
         const uint32_t flags = __builtin_amdgcn_readfirstlane(rq.flags);
         const uint8_t *in = rq.in, *aad = rq.aad;
@@ -621,14 +689,19 @@ __global__ void __launch_bounds__(64)
         } else {
             /* the record's first two elements per lane, as the launched single-record kernel reads them */
             V4 pre[2] = {V4{0, 0, 0, 0}, V4{0, 0, 0, 0}};
-            const int na1 = ((int)rec.aad_len + 15) >> 4, nc1 = ((int)rec.len + 15) >> 4;
+            if (flags & WREQ_INLINE) {
+                pre[0] = pin[0];
+                pre[1] = pin[1];
+            } else {
+                const int na1 = ((int)rec.aad_len + 15) >> 4, nc1 = ((int)rec.len + 15) >> 4;
 #pragma unroll
-            for (int m = 0; m < 2; ++m) {
-                const int i = lane + 64 * m;
-                if (i < na1)
-                    pre[m] = load_full(aad + rec.aad_off + 16 * (size_t)i);
-                else if (i < na1 + nc1)
-                    pre[m] = load_full(in + rec.in_off + 16 * (size_t)(i - na1));
+                for (int m = 0; m < 2; ++m) {
+                    const int i = lane + 64 * m;
+                    if (i < na1)
+                        pre[m] = load_full(aad + rec.aad_off + 16 * (size_t)i);
+                    else if (i < na1 + nc1)
+                        pre[m] = load_full(in + rec.in_off + 16 * (size_t)(i - na1));
+                }
             }
             const ptls_hip_supp_t *supp = rq.supp;
             const KeySlot *hp_slots = rq.hp_slots;
@@ -636,18 +709,19 @@ __global__ void __launch_bounds__(64)
             uint64_t *result = rq.result;
             const uint32_t *basis = rq.basis;
             const bool open = (flags & WREQ_OPEN) != 0, a256 = (flags & WREQ_AES256) != 0;
+            const uint32_t ctab = SP_TAB + 8192u;
             if (open && a256)
                 sparse_record<14, true, true, true>(lds, lane, lb_aes, tab, rec, 0, in, aad, out, result, slots, basis, supp,
-                                                    hp_slots, 1, mask, true, pre, nullptr, false, false, pa);
+                                                    hp_slots, 1, mask, true, pre, nullptr, false, false, pa, ctab);
             else if (open)
                 sparse_record<10, true, true, true>(lds, lane, lb_aes, tab, rec, 0, in, aad, out, result, slots, basis, supp,
-                                                    hp_slots, 1, mask, true, pre, nullptr, false, false, pa);
+                                                    hp_slots, 1, mask, true, pre, nullptr, false, false, pa, ctab);
             else if (a256)
                 sparse_record<14, false, true, true>(lds, lane, lb_aes, tab, rec, 0, in, aad, out, result, slots, basis, supp,
-                                                     hp_slots, 1, mask, true, pre, nullptr, false, false, pa);
+                                                     hp_slots, 1, mask, true, pre, nullptr, false, false, pa, ctab);
             else
                 sparse_record<10, false, true, true>(lds, lane, lb_aes, tab, rec, 0, in, aad, out, result, slots, basis, supp,
-                                                     hp_slots, 1, mask, true, pre, nullptr, false, false, pa);
+                                                     hp_slots, 1, mask, true, pre, nullptr, false, false, pa, ctab);
         }
         /* every store of the call reaches system scope before its completion word; then the slot is free again */
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
