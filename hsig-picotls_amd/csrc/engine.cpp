@@ -1900,7 +1900,7 @@ static unsigned staging_flags(void);
  * fine-grained), then waits on its completion word as a launched call does.  Calls are serialized on the worker (one
  * request at a time; the mutex is held for the whole call).  The worker leaves after WORKER_IDLE_US without a request
  * or after WORKER_LIFE_US, and a call that finds it gone relaunches it (the launch a call without the worker pays each
- * time).  Opt-in while it is being validated: PTLS_HIP_PLUGIN_WORKER=1 (environment); otherwise one launch per call. */
+ * time).  On by default; PTLS_HIP_PLUGIN_WORKER=0 (environment) makes every call launch its own kernel instead. */
 static const uint64_t WORKER_IDLE_US = 200, WORKER_LIFE_US = 2000;
 
 struct PluginWorker {
@@ -1918,7 +1918,7 @@ static bool worker_enabled(void)
 {
     static const bool on = [] {
         const char *e = getenv("PTLS_HIP_PLUGIN_WORKER");
-        return e != nullptr && atoi(e) != 0;
+        return e == nullptr || atoi(e) != 0;
     }();
     return on;
 }
@@ -1999,6 +1999,27 @@ static void worker_quiesce(void)
     __atomic_store_n(&w.h_mb->quit, 0u, __ATOMIC_RELEASE);
 }
 
+#ifndef WORKER_STAMPS
+#define WORKER_STAMPS 0 /* diagnostic build only (Makefile `diag`) */
+#endif
+#if WORKER_STAMPS
+/* diagnostic build: the worker's phase stamps of the last request and the host's wall-clock microseconds of that call */
+static double g_worker_call_us = 0;
+extern "C" int ptls_hip_diag_worker_stamps(uint64_t *out, double *call_us)
+{
+    if (g_worker.h_mb == nullptr)
+        return -1;
+    for (int i = 0; i < 5; ++i)
+        out[i] = __atomic_load_n(&g_worker.h_mb->stamps[i], __ATOMIC_ACQUIRE);
+    /* the record's phase stamps (shader cycles): clk[1] request loaded, clk[2..8] sparse_record's phases, clk[9] done */
+    const uint64_t *clk = reinterpret_cast<const uint64_t *>(g_worker.h_mb->data + WORKER_DATA - 128);
+    for (int i = 0; i < 10; ++i)
+        out[5 + i] = __atomic_load_n(&clk[i], __ATOMIC_ACQUIRE);
+    *call_us = g_worker_call_us;
+    return 0;
+}
+#endif
+
 /* one request through the worker; returns once the call's completion word shows done_seq (the same protocol as a
  * launched call, plugin_wait).  A worker that left without serving the request is relaunched (its successor serves it:
  * seq != served); without any progress for 2 s the process aborts like a launched call's device fault would. */
@@ -2009,12 +2030,18 @@ static void worker_call(const WorkerReq &req, const uint8_t *word_p)
     if (!worker_launch(w))
         plugin_die("plugin worker launch");
     w.h_mb->req = req;
+    const auto tc = std::chrono::steady_clock::now();
     __atomic_store_n(&w.h_mb->seq, ++w.seq, __ATOMIC_RELEASE);
     const uint32_t *word = reinterpret_cast<const uint32_t *>(word_p);
     auto t0 = std::chrono::steady_clock::now();
     for (uint32_t spin = 1;; ++spin) {
-        if (load_acquire(word) == req.done_seq)
+        if (load_acquire(word) == req.done_seq) {
+#if WORKER_STAMPS
+            g_worker_call_us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - tc).count();
+#endif
+            (void)tc;
             return;
+        }
 #if defined(__x86_64__) || defined(__i386__)
         __builtin_ia32_pause();
 #else

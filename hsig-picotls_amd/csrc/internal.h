@@ -163,7 +163,8 @@ struct WorkerSlot {
     uint32_t exited;  /* worker -> host: the epoch of the worker wave that left */
     uint32_t started; /* worker -> host: the epoch of the worker wave that started (diagnostics) */
     uint32_t seen;    /* worker -> host: the last request number it read (diagnostics) */
-    uint32_t pad1[28];
+    uint32_t pad1[2];
+    uint64_t stamps[13]; /* worker -> host: WORKER_STAMPS builds' phase stamps of the last request (100 MHz counter) */
     WorkerReq req;
     uint8_t data[WORKER_DATA]; /* WREQ_INLINE records */
 };

@@ -614,6 +614,28 @@ __global__ void __launch_bounds__(WG)
  * in `exited`. */
 constexpr int WORKER_POLLS = 4;
 
+/* a pointer the worker read from its mailbox, marked as global memory: without it the compiler cannot infer the address
+ * space, emits flat loads / stores and waits for every flat store's completion (a PCIe write round trip per output store
+ * into pinned host memory) before the next LDS access */
+template <typename T>
+__device__ __forceinline__ T *as_global(T *p)
+{
+    uint64_t v = (uint64_t)(uintptr_t)p;
+    asm volatile("" : "+v"(v)); /* an opaque integer: the global pointer made from it cannot be folded back to a flat one */
+    return (T *)((__attribute__((address_space(1))) T *)v);
+}
+#ifndef WORKER_STAMPS
+#define WORKER_STAMPS 0 /* diagnostic builds only (Makefile `diag`, tools/worker_stamps.py): the worker stamps the 100 MHz counter
+                           at its phase boundaries into WorkerSlot::stamps (seen, request read, record done, released) */
+#endif
+
+/* a stamp of the 100 MHz counter after everything the wave issued so far has completed */
+__device__ __forceinline__ uint64_t worker_stamp()
+{
+    __builtin_amdgcn_s_waitcnt(0);
+    return __builtin_amdgcn_s_memrealtime();
+}
+
 __device__ __forceinline__ uint64_t poll_word(const WorkerSlot *ms)
 {
     return __hip_atomic_load(reinterpret_cast<const uint64_t *>(&ms->seq), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -665,7 +687,12 @@ __global__ void __launch_bounds__(64)
          * workgroup-scope acquire served request 2 with request 1's completion pointer), so the acquire is at system
          * scope, which invalidates the L1 and the L2's lines of host memory.  Device key material is never modified
          * while a worker is resident (engine.cpp worker_quiesce), so no cache can hold a stale key slot. */
+        uint64_t st[5] = {0, 0, 0, 0, 0};
+        if (WORKER_STAMPS)
+            st[0] = worker_stamp();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+        if (WORKER_STAMPS)
+            st[1] = worker_stamp();
         if (lane == 0)
             __hip_atomic_store(&ms->seen, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         const WorkerReq &rq = ms->req;
@@ -676,11 +703,21 @@ __global__ void __launch_bounds__(64)
             pin[m] = load_full(ms->data + 16 * (size_t)(lane + 64 * m));
         const ptls_hip_record_t rec = rq.rec;
         const uint32_t flags = __builtin_amdgcn_readfirstlane(rq.flags);
-        const uint8_t *in = rq.in, *aad = rq.aad;
-        uint8_t *out = rq.out;
-        const KeySlot *slots = rq.slots;
-        uint32_t *done = rq.done;
+        const uint8_t *in = as_global(rq.in), *aad = as_global(rq.aad);
+        uint8_t *out = as_global(rq.out);
+        const KeySlot *slots = as_global(rq.slots);
+        uint32_t *done = as_global(rq.done);
         const uint32_t done_seq = __builtin_amdgcn_readfirstlane(rq.done_seq);
+        if (WORKER_STAMPS)
+            st[2] = worker_stamp();
+        /* WORKER_STAMPS builds (with STAMP_PHASES): the record's phase stamps (shader cycles) go to the end of the data area,
+         * clk[1] = the request loaded, clk[9] = the record done */
+        uint64_t *wclk = WORKER_STAMPS ? reinterpret_cast<uint64_t *>(ms->data + WORKER_DATA - 128) : nullptr;
+        if (WORKER_STAMPS) {
+            const uint64_t t = __builtin_amdgcn_s_memtime();
+            if (lane == 0)
+                wclk[1] = t;
+        }
         if (flags & WREQ_ECB) {
             const V4 blk = V4{rq.blk[0], rq.blk[1], rq.blk[2], rq.blk[3]};
             const V4 m = (flags & WREQ_AES256) ? aes_encrypt<14>(lds, lb_aes, slots->rk, blk) : aes_encrypt<10>(lds, lb_aes, slots->rk, blk);
@@ -703,28 +740,41 @@ __global__ void __launch_bounds__(64)
                         pre[m] = load_full(in + rec.in_off + 16 * (size_t)(i - na1));
                 }
             }
-            const ptls_hip_supp_t *supp = rq.supp;
-            const KeySlot *hp_slots = rq.hp_slots;
-            uint8_t *mask = rq.mask;
-            uint64_t *result = rq.result;
-            const uint32_t *basis = rq.basis;
+            const ptls_hip_supp_t *supp = rq.supp != nullptr ? as_global(rq.supp) : nullptr;
+            const KeySlot *hp_slots = rq.hp_slots != nullptr ? as_global(rq.hp_slots) : nullptr;
+            uint8_t *mask = rq.mask != nullptr ? as_global(rq.mask) : nullptr;
+            uint64_t *result = as_global(rq.result);
+            const uint32_t *basis = as_global(rq.basis);
             const bool open = (flags & WREQ_OPEN) != 0, a256 = (flags & WREQ_AES256) != 0;
             const uint32_t ctab = SP_TAB + 8192u;
             if (open && a256)
                 sparse_record<14, true, true, true>(lds, lane, lb_aes, tab, rec, 0, in, aad, out, result, slots, basis, supp,
-                                                    hp_slots, 1, mask, true, pre, nullptr, false, false, pa, ctab);
+                                                    hp_slots, 1, mask, true, pre, wclk, WORKER_STAMPS, false, pa, ctab);
             else if (open)
                 sparse_record<10, true, true, true>(lds, lane, lb_aes, tab, rec, 0, in, aad, out, result, slots, basis, supp,
-                                                    hp_slots, 1, mask, true, pre, nullptr, false, false, pa, ctab);
+                                                    hp_slots, 1, mask, true, pre, wclk, WORKER_STAMPS, false, pa, ctab);
             else if (a256)
                 sparse_record<14, false, true, true>(lds, lane, lb_aes, tab, rec, 0, in, aad, out, result, slots, basis, supp,
-                                                     hp_slots, 1, mask, true, pre, nullptr, false, false, pa, ctab);
+                                                     hp_slots, 1, mask, true, pre, wclk, WORKER_STAMPS, false, pa, ctab);
             else
                 sparse_record<10, false, true, true>(lds, lane, lb_aes, tab, rec, 0, in, aad, out, result, slots, basis, supp,
-                                                     hp_slots, 1, mask, true, pre, nullptr, false, false, pa, ctab);
+                                                     hp_slots, 1, mask, true, pre, wclk, WORKER_STAMPS, false, pa, ctab);
+        }
+        if (WORKER_STAMPS) {
+            st[3] = worker_stamp();
+            const uint64_t t = __builtin_amdgcn_s_memtime();
+            if (lane == 0)
+                wclk[9] = t;
         }
         /* every store of the call reaches system scope before its completion word; then the slot is free again */
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+        if (WORKER_STAMPS) {
+            st[4] = worker_stamp();
+            if (lane < 5)
+                __hip_atomic_store(&ms->stamps[lane], lane == 0 ? st[0] : lane == 1 ? st[1] : lane == 2 ? st[2] : lane == 3 ? st[3] : st[4],
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+        }
         if (lane == 0) {
             __hip_atomic_store(done, done_seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             __hip_atomic_store(&ms->served, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
