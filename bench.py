@@ -126,7 +126,9 @@ def make_workload(cfg, rank, world=1, scaling="weak", n_full=None):
         seq = (idx // K).astype(np.uint64)
     lens = record_lengths(cfg, idx)
     aad_len = 5 if cfg["aad"] == "tls" else 13
-    recs, in_total, out_total, _ = ptls_hip.layout_records(lens, np.full(n, aad_len), keyslot, seq, align=16)
+    # records at 16-byte aligned offsets; PTLS_BENCH_ALIGN (environment, for traffic A/B) overrides the alignment
+    align = int(os.environ.get("PTLS_BENCH_ALIGN", "16"))
+    recs, in_total, out_total, _ = ptls_hip.layout_records(lens, np.full(n, aad_len), keyslot, seq, align=align)
     recs["aad_off"] = np.arange(n, dtype=np.uint64) * np.uint64(16)
     return idx, recs, in_total, out_total, lens
 

@@ -262,7 +262,8 @@ __global__ void keysetup_kernel(KeySlot *slots, uint32_t *basis, const uint8_t *
             b = gf_mulx(b);
         }
     }
-    /* H^1 .. H^64 (the sparse kernel's lane q multiplies its partial sum by H^(q+1)) */
+    /* H^1 .. H^128 (the sparse kernel's lane q multiplies its partial sum by H^(q+1); a two-wave single record element i
+     * by H^(N - i)) */
     const U128 hh = u128_from_raw(h);
     U128 pk = hh;
     for (int q = 0; q < LANE_POWS; ++q) {
@@ -284,7 +285,7 @@ __global__ void keysetup_kernel(KeySlot *slots, uint32_t *basis, const uint8_t *
 __global__ void __launch_bounds__(64) keysetup_wide_kernel(KeySlot *slots, uint32_t *basis, const uint8_t *keys,
                                                            const uint8_t *ivs, uint32_t first, int key_size, const uint32_t *t0)
 {
-    static_assert(LANE_POWS == 64 && NPOW >= 7, "one lane power per lane; H^(j+1) from the squares H^(2^t), t < 7");
+    static_assert(LANE_POWS == 128 && NPOW >= 7, "two lane powers per lane; H^(j+1), H^(j+65) from the squares H^(2^t), t < 7");
     const uint32_t k = blockIdx.x;
     const int j = (int)threadIdx.x;
     KeySlot *slot = slots + first + k;
@@ -329,6 +330,8 @@ __global__ void __launch_bounds__(64) keysetup_wide_kernel(KeySlot *slots, uint3
         }
     }
     bs[NPOW * 128 + j] = make_uint4(acc.w0, acc.w1, acc.w2, acc.w3);
+    acc = gf_mul_valu(acc, pw[6]); /* H^(j + 65) = H^(j + 1) * H^64 */
+    bs[NPOW * 128 + 64 + j] = make_uint4(acc.w0, acc.w1, acc.w2, acc.w3);
 }
 
 /* ======================================================================================= *

@@ -2101,24 +2101,8 @@ static const size_t ECB_DONE = 64;
 static void ecb_block(hip_ctr_state *st, const void *src, uint8_t dst[16])
 {
     DeviceGuard g(st->eng->device);
-    if (worker_enabled()) {
-        WorkerReq rq{};
-        rq.out = st->d_stage + 48;
-        rq.slots = st->ks->d_slots;
-        rq.done = reinterpret_cast<uint32_t *>(st->d_stage + ECB_DONE);
-        rq.done_seq = ++st->done_seq;
-        rq.flags = WREQ_ECB | (st->ks->key_size == 32 ? WREQ_AES256 : 0u);
-        std::memcpy(rq.blk, src, 16);
-        {
-            std::lock_guard<std::mutex> lk(g_worker.mu);
-            g_worker.eng = st->eng;
-            worker_call(rq, st->h_stage + ECB_DONE);
-        }
-        std::memcpy(dst, st->h_stage + 48, 16);
-        std::memset(st->h_stage + 48, 0, 16);
-        std::memset(rq.blk, 0, sizeof(rq.blk));
-        return;
-    }
+    /* one launch per block even with the plugin worker resident: measured faster than a worker request (9.5 against
+     * 11.2 us per block): the kernel's block travels in its arguments, while a request adds a PCIe read of the mailbox */
     /* the block goes in the kernel arguments; the result comes back through the pinned staging (@48) */
     const int e = launch_aesecb_one(st->ks->key_size == 16 ? 10 : 14, static_cast<const uint8_t *>(src), st->ks->d_slots,
                                     st->eng->d_t0, st->d_stage + 48, reinterpret_cast<uint32_t *>(st->d_stage + ECB_DONE),

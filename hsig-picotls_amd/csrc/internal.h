@@ -37,8 +37,9 @@ namespace ptls_hip {
 constexpr int NPOW = SPLIT_TASKS ? 10 : 7; /* H^1 .. H^16 (batch kernel main and tree tables), H^32 (batch kernel main table
                                               at G = 32), H^64 (sparse kernel); SPLIT_TASKS: H^128 .. H^512 (the shift of a
                                               split record's first part, batch_kernel.h) */
-/* GHASH basis slot: NPOW x 128 vectors P * x^e, then H^1 .. H^64 (the sparse kernel's per-lane final powers) */
-constexpr int LANE_POWS = 64;
+/* GHASH basis slot: NPOW x 128 vectors P * x^e, then H^1 .. H^128 (the sparse kernel's per-lane final powers: H^(q+1),
+ * q < 64; a two-wave single record of up to 128 GHASH elements multiplies element i by H^(N - i)) */
+constexpr int LANE_POWS = 128;
 /* HYBRID (measurement switch): this many waves per batch-kernel workgroup (the last ones) run their
  * full-block stretch as bit-sliced AES on the VALU (bs8_aes.h), the others with the LDS T-tables.  Parity-green, but
  * no faster on MI355X (c2: +0-1 % at 4 of 12 waves, -5 % at 8, -20 % at 12), so off. */
@@ -48,7 +49,7 @@ constexpr int LANE_POWS = 64;
 /* with HYBRID, the slot also holds the bit-sliced round keys 1..rounds (bs8::slice_key: 32 words per round) */
 constexpr int BS_KEY_OFF = NPOW * 128 + LANE_POWS; /* uint4 offset in the slot */
 constexpr int BS_KEY_VECS = HYBRID ? 14 * 32 / 4 : 0;
-constexpr int BASIS_VECS = BS_KEY_OFF + BS_KEY_VECS; /* uint4 per key slot (15 KiB; 16.75 KiB with HYBRID, 21 KiB with SPLIT_TASKS) */
+constexpr int BASIS_VECS = BS_KEY_OFF + BS_KEY_VECS; /* uint4 per key slot (16 KiB; 17.75 KiB with HYBRID, 22 KiB with SPLIT_TASKS) */
 constexpr int MAX_LANES = 32;    /* lanes per record (G) of the batch kernel: 1, 2, 4, 8, 16, 32 */
 constexpr int SPARSE_LANES = 64; /* "lanes" value of the wave-per-record kernel (sparse_kernel.hip) */
 /* the planner picks that kernel when a batch's key runs hold fewer records than this on average */
@@ -133,7 +134,7 @@ struct KernelArgs {
  * plugin's single-record calls from a mailbox in fine-grained pinned host memory instead of one kernel launch per call.
  * The host writes the request, then (release) seq; the wave serves it, stores the call's completion word (as a launched
  * call's kernel does), then `served`. */
-enum : uint32_t { WREQ_OPEN = 1, WREQ_AES256 = 2, WREQ_ECB = 4, WREQ_INLINE = 8 };
+enum : uint32_t { WREQ_OPEN = 1, WREQ_AES256 = 2, WREQ_INLINE = 8 };
 /* WREQ_INLINE: the record sits in the mailbox's data area (AAD padded to 16 bytes, then the input: element i of the GHASH
  * input at data + 16 i), read in the same PCIe round trip as the request.  Records that do not fit stay in the caller's
  * pinned staging. */
@@ -151,8 +152,7 @@ struct WorkerReq {
     uint32_t *done;           /* the call's completion word */
     uint32_t done_seq;
     uint32_t flags;           /* WREQ_* */
-    uint32_t blk[4];          /* WREQ_ECB: the input block (the output goes to `out`) */
-    uint32_t pad[10];
+    uint32_t pad[14];
 };
 static_assert(sizeof(WorkerReq) == 192, "WorkerReq: 192 bytes");
 struct WorkerSlot {

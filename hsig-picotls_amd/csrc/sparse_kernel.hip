@@ -488,6 +488,103 @@ __device__ __forceinline__ void sparse_record(uint8_t *lds, int lane, uint32_t l
     }
 }
 
+/* Two waves on one record of 65 .. 128 GHASH elements (a QUIC packet; the plugin's single-record launch and the worker).
+ * One wave alone is bound by its own LDS issue rate (a single wave gets a fraction of the LDS's rate, MI355X_MICROARCH.md
+ * §LDS), and sparse_record gives it two elements per lane plus an H^64 table and a Horner step.  Here element i = 64 w + l
+ * goes to lane l of wave w: one counter-mode AES block per lane, its GHASH input times H^(N - i) (keysetup's power list;
+ * the windowed multiply's table is built from the power before the AES), an XOR butterfly per wave, and wave 1 adds
+ * wave 0's sum from LDS after a workgroup barrier and writes the tag.  Wave 0 makes its output stores visible at system
+ * scope before the barrier, so the completion word wave 1 stores after the tag covers them.  Every wave of the workgroup
+ * calls this (the barrier); waves >= 2 only take part in the barrier.  pre = the lane's element (16 bytes, read early). */
+constexpr int MW_MIN_N = 65, MW_MAX_N = 2 * 64;
+
+template <int ROUNDS, bool OPEN, bool ALIGNED>
+__device__ __forceinline__ void mw_record(uint8_t *lds, int wave, int lane, uint32_t lb_aes, uint32_t ctab, uint32_t xslot,
+                                          const ptls_hip_record_t &rec, const uint8_t *in, const uint8_t *__restrict__ aad,
+                                          uint8_t *out, uint64_t *__restrict__ result, const KeySlot *__restrict__ slots,
+                                          const uint32_t *__restrict__ basis, const ptls_hip_supp_t *__restrict__ supp,
+                                          const KeySlot *__restrict__ hp_slots, uint32_t hp_nslots, uint8_t *mask, V4 pre)
+{
+    const uint32_t key = __builtin_amdgcn_readfirstlane(rec.key);
+    const KeySlot *__restrict__ slot = slots + key;
+    const uint32_t *__restrict__ rk = slot->rk;
+    const uint4 *__restrict__ bs = reinterpret_cast<const uint4 *>(basis) + (size_t)key * BASIS_VECS;
+    const int L = (int)__builtin_amdgcn_readfirstlane(rec.len);
+    const int A = (int)__builtin_amdgcn_readfirstlane(rec.aad_len);
+    const int na = (A + 15) >> 4, nc = (L + 15) >> 4;
+    const int N = na + nc + 1;
+    const bool tflag = !OPEN && (rec.flags & 1u) != 0 && L > 0;
+    const uint32_t ttype = (rec.flags >> 8) & 0xffu;
+    const uint8_t *in_p = in + rec.in_off;
+    uint8_t *out_p = out + rec.out_off;
+    const uint8_t *aad_p = aad + rec.aad_off;
+    const int i = 64 * wave + lane;
+    V4 z = V4{0, 0, 0, 0}, ek0 = V4{0, 0, 0, 0};
+    if (wave < 2) {
+        const uint4 hp = bs[NPOW * 128 + (i < N ? N - i - 1 : 0)]; /* H^(N - i) */
+        const uint32_t n0 = __builtin_amdgcn_readfirstlane(slot->iv[0]),
+                       n1 = __builtin_amdgcn_readfirstlane(slot->iv[1] ^ bswap32((uint32_t)(rec.seq >> 32))),
+                       n2 = __builtin_amdgcn_readfirstlane(slot->iv[2] ^ bswap32((uint32_t)rec.seq));
+        CtrConst cc = ctr_const(lds, lb_aes, rk, n0, n1, n2);
+        cc.k10 = __builtin_amdgcn_readfirstlane(cc.k10);
+        cc.k11 = __builtin_amdgcn_readfirstlane(cc.k11);
+        cc.k20 = __builtin_amdgcn_readfirstlane(cc.k20);
+        cc.k21 = __builtin_amdgcn_readfirstlane(cc.k21);
+        cc.k22 = __builtin_amdgcn_readfirstlane(cc.k22);
+        cc.k23 = __builtin_amdgcn_readfirstlane(cc.k23);
+        cc.r03 = __builtin_amdgcn_readfirstlane(cc.r03);
+        const Win4<16> w4 = gf_win4_build<16>(lds, ctab, lane, V4{hp.x, hp.y, hp.z, hp.w});
+        const Elem e = elem_of(i < N ? i : N, N, na, nc, L, N);
+        V4 inb = V4{0, 0, 0, 0};
+        if (e.is_c) {
+            const bool tb = tflag && e.c == nc - 1; /* the block holding the content-type byte */
+            inb = mask_block(pre, e.nbytes - (tb ? 1 : 0));
+            if (tb)
+                inb = put_byte(inb, e.nbytes - 1, ttype);
+        } else if (e.is_aad) {
+            inb = mask_block(pre, min(16, A - 16 * e.i));
+        }
+        uint32_t cw[1] = {e.is_c ? bswap32((uint32_t)e.c + 2u) : 0x01000000u}; /* E_K(J0) on the length-block lane */
+        V4 ks[1] = {V4{n0, n1, n2, cw[0]}};
+        const V4 nohash[1] = {};
+        V4 ydummy = V4{0, 0, 0, 0};
+        ctr_ghash_skewed<ROUNDS, 1, false>(lds, lb_aes, rk, cc, cw, ks, ydummy, nohash, GhNibble{ctab});
+        const V4 x = finish_elem<OPEN, ALIGNED, true>(e, inb, ks[0], aad_p, A, L, out_p, ek0); /* 0 past the record */
+        z = wave_xor(gf_win4_mul<16>(lds, w4, x));
+        if (wave == 0) {
+            if (lane == 0)
+                lds128_store(lds, xslot, z);
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, ""); /* this wave's output stores, before wave 1's completion word */
+        }
+    }
+    __syncthreads();
+    if (wave == 1) {
+        const V4 y = v4xor(z, lds128(lds, xslot));
+        if (i == N - 1) {
+            const V4 tag = v4xor(y, ek0);
+            if (OPEN) {
+                const V4 rt = load_block<false>(in_p + L, 16);
+                const bool ok = rt.w0 == tag.w0 && rt.w1 == tag.w1 && rt.w2 == tag.w2 && rt.w3 == tag.w3;
+                result[0] = ok ? (uint64_t)L : ~(uint64_t)0;
+            } else {
+                store_full(out_p + L, tag);
+            }
+        }
+        if (!OPEN && supp != nullptr) { /* header protection after the tag (the sample may cover it), as sparse_record */
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+            if (lane == 0) {
+                const ptls_hip_supp_t sp = supp[0];
+                if ((sp.flags & PTLS_HIP_SUPP_ENABLE) && sp.hp_key < hp_nslots) {
+                    const V4 sample = load_full(out + sp.sample_off);
+                    const V4 mk = aes_encrypt<ROUNDS>(lds, lb_aes, hp_slots[sp.hp_key].rk, sample);
+                    store_full(mask + sp.mask_off, mk);
+                }
+            }
+        }
+    }
+}
+
 /* BYVAL: the plugin's single-record launch (the record by value in the kernel arguments, recs_ord == nullptr); its own
  * instantiation, so the batch one carries none of its prefetch registers.  It runs 256 threads (one wave per SIMD, the
  * whole register file: no spills) since only wave 0 works on the record; the others help build the AES tables. */
@@ -501,8 +598,10 @@ __global__ void __launch_bounds__(WG)
                          const KeySlot *__restrict__ hp_slots, uint32_t hp_nslots, uint8_t *mask, ptls_hip_record_t one,
                          uint32_t *done, uint32_t done_seq, uint64_t *__restrict__ clk)
 {
-    __shared__ __attribute__((aligned(16))) uint8_t lds[SP_TAB + (WG / 64) * 8192];
-    static_assert(SP_TAB + (WG / 64) * 8192 <= 163840, "AES tables + per-wave GHASH tables must fit the CU's 160 KiB");
+    /* BYVAL: 16 KiB more for wave 1's windowed table of a two-wave record (mw_record) */
+    constexpr uint32_t LDS_SIZE = SP_TAB + (WG / 64) * 8192 + (BYVAL ? 16384 : 0);
+    __shared__ __attribute__((aligned(16))) uint8_t lds[LDS_SIZE];
+    static_assert(LDS_SIZE <= 163840, "AES tables + per-wave GHASH tables must fit the CU's 160 KiB");
     const int lane = threadIdx.x & 63;
     const uint32_t lb_aes = (uint32_t)(lane & 31) * 4u; /* table base 0: byte 2 of the address is 0 */
     const uint32_t tab = __builtin_amdgcn_readfirstlane(SP_TAB + (uint32_t)(threadIdx.x >> 6) * 8192u); /* wave-uniform */
@@ -552,8 +651,28 @@ __global__ void __launch_bounds__(WG)
         else if (threadIdx.x >= 64)
             build_aes_tables<WG - 64>(lds, 0, t0, (int)threadIdx.x - 64);
     }
+    /* a two-wave record (mw_record): wave 1's element lane + 64 was prefetched by wave 0 (pre[1]); it goes through LDS
+     * (wave 3's table area, unused by a single record) */
+    const int n_one = BYVAL ? (((int)one.aad_len + 15) >> 4) + (((int)one.len + 15) >> 4) + 1 : 0;
+    const bool mw = BYVAL && STAMP_PHASES == 0 && n_one >= MW_MIN_N && n_one <= MW_MAX_N;
+    const uint32_t XCH = SP_TAB + 3u * 8192u;
+    if (mw && threadIdx.x < 64)
+        lds128_store(lds, XCH + (uint32_t)lane * 16u, pre[1]);
     __syncthreads();
     asm volatile("" ::"v"(touch.w0), "v"(touch.w1), "v"(touch.w2), "v"(touch.w3)); /* keep the touch loads */
+    if (mw) {
+        const int wave = (int)(threadIdx.x >> 6);
+        const V4 mine = wave == 0 ? pre[0] : wave == 1 ? lds128(lds, XCH + (uint32_t)lane * 16u) : V4{0, 0, 0, 0};
+        const uint32_t ctab_w = wave == 0 ? SP_TAB + 8192u : SP_TAB + (uint32_t)(WG / 64) * 8192u;
+        mw_record<ROUNDS, OPEN, ALIGNED>(lds, wave, lane, lb_aes, ctab_w, SP_TAB, one, in, aad, out, result, slots, basis, supp,
+                                         hp_slots, hp_nslots, mask, mine);
+        if (done != nullptr && wave == 1) { /* the tag's wave: wave 0 released its stores before the barrier */
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+            if (lane == 0)
+                __hip_atomic_store(done, done_seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+        return;
+    }
     phase_stamp(clk, stamps, lane, 1);
     uint32_t nrecs = 1;
     if (!by_value) {
@@ -602,8 +721,8 @@ __global__ void __launch_bounds__(WG)
 
 /* The plugin worker: one wave stays resident and serves the mailbox (internal.h WorkerSlot, fine-grained pinned host
  * memory): it polls seq over PCIe, reads the request, runs the record through sparse_record (the single-record path of a
- * launched call: prefetched first elements, the wave's H^64 table, the early lane-combination table) or one ECB block,
- * stores the call's completion word after all its output (system scope) and then `served`.  The AES tables are built
+ * launched call: prefetched first elements, the wave's H^64 table, the early lane-combination table; records of 65..128
+ * GHASH elements on both waves, mw_record), stores the call's completion word after all its output (system scope) and then `served`.  The AES tables are built
  * once for the worker's life instead of once per call, and no launch sits between the caller and the kernel.
  *   - Polling keeps WORKER_POLLS loads of {seq, quit} in flight (a PCIe read takes ~2 us): a new request is seen about one
  *     read latency after it is written, not up to two.
@@ -641,47 +760,63 @@ __device__ __forceinline__ uint64_t poll_word(const WorkerSlot *ms)
     return __hip_atomic_load(reinterpret_cast<const uint64_t *>(&ms->seq), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-__global__ void __launch_bounds__(64)
+constexpr int WORKER_WG = 128; /* two waves: wave 0 polls; both serve a two-wave record (mw_record) */
+
+__global__ void __launch_bounds__(WORKER_WG)
     plugin_worker_kernel(WorkerSlot *mb, uint32_t epoch, const uint32_t *__restrict__ t0, uint64_t idle_ticks, uint64_t life_ticks)
 {
-    __shared__ __attribute__((aligned(16))) uint8_t lds[SP_TAB + 8192 + 16384];
-    const int lane = threadIdx.x & 63;
+    /* AES tables | wave 0's H^64 table | wave 0's lane-combination table | wave 1's | the poll's verdict */
+    constexpr uint32_t CTAB0 = SP_TAB + 8192, CTAB1 = CTAB0 + 16384, CTL = CTAB1 + 16384;
+    __shared__ __attribute__((aligned(16))) uint8_t lds[CTL + 16];
+    const int lane = threadIdx.x & 63, wave = (int)(threadIdx.x >> 6);
     const uint32_t lb_aes = (uint32_t)(lane & 31) * 4u;
     const uint32_t tab = SP_TAB;
-    build_aes_tables<64>(lds, 0, t0);
+    build_aes_tables<WORKER_WG>(lds, 0, t0);
     __syncthreads();
     WorkerSlot *ms = mb;
     const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
     uint64_t t_last = t_start;
     uint32_t last = __builtin_amdgcn_readfirstlane(__hip_atomic_load(&ms->served, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
-    if (lane == 0)
+    if (threadIdx.x == 0)
         __hip_atomic_store(&ms->started, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     PhaseAcc pa{};
     uint64_t ring[WORKER_POLLS];
+    if (wave == 0) {
 #pragma unroll
-    for (int k = 0; k < WORKER_POLLS; ++k) {
-        ring[k] = poll_word(ms);
-        __builtin_amdgcn_s_sleep(8);
-    }
-    bool leave = false;
-    while (!leave) {
-        uint32_t seq = last;
-#pragma unroll
-        for (int k = 0; k < WORKER_POLLS; ++k) { /* the oldest read in flight (vmcnt retires in order), then a new one */
-            const uint64_t v = ring[k];
-            const uint32_t s = __builtin_amdgcn_readfirstlane((uint32_t)v), quit = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
-            /* a read issued before the last request was served may still return the one before it: only a later
-             * request number counts (the host numbers them consecutively) */
-            if (seq == last && (int32_t)(s - last) > 0)
-                seq = s;
-            const uint64_t now = __builtin_amdgcn_s_memrealtime();
-            if (seq == last && (quit != 0 || now - t_last > idle_ticks || now - t_start > life_ticks))
-                leave = true;
+        for (int k = 0; k < WORKER_POLLS; ++k) {
             ring[k] = poll_word(ms);
-            __builtin_amdgcn_s_sleep(2);
+            __builtin_amdgcn_s_sleep(8);
         }
-        if (leave || seq == last)
-            continue;
+    }
+    for (;;) {
+        if (wave == 0) { /* poll until a request or a reason to leave; the verdict goes to wave 1 through LDS */
+            uint32_t seq = last;
+            bool leave = false;
+            while (!leave && seq == last) {
+#pragma unroll
+                for (int k = 0; k < WORKER_POLLS; ++k) { /* the oldest read in flight (vmcnt retires in order), then a new one */
+                    const uint64_t v = ring[k];
+                    const uint32_t sv = __builtin_amdgcn_readfirstlane((uint32_t)v),
+                                   quit = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+                    /* a read issued before the last request was served may still return the one before it: only a later
+                     * request number counts (the host numbers them consecutively) */
+                    if (seq == last && (int32_t)(sv - last) > 0)
+                        seq = sv;
+                    const uint64_t now = __builtin_amdgcn_s_memrealtime();
+                    if (seq == last && (quit != 0 || now - t_last > idle_ticks || now - t_start > life_ticks))
+                        leave = true;
+                    ring[k] = poll_word(ms);
+                    __builtin_amdgcn_s_sleep(2);
+                }
+            }
+            if (lane == 0)
+                *reinterpret_cast<uint2 *>(lds + CTL) = make_uint2(seq, leave ? 1u : 0u);
+        }
+        __syncthreads();
+        const uint2 verdict = *reinterpret_cast<const uint2 *>(lds + CTL);
+        const uint32_t seq = __builtin_amdgcn_readfirstlane(verdict.x);
+        if (__builtin_amdgcn_readfirstlane(verdict.y) != 0)
+            break;
         /* the request (and the record, inline or in the caller's pinned staging) was written before seq.  Ordering the
          * loads is not enough: the vector L1 keeps the previous request's lines at the same addresses (measured: a
          * workgroup-scope acquire served request 2 with request 1's completion pointer), so the acquire is at system
@@ -693,14 +828,14 @@ __global__ void __launch_bounds__(64)
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
         if (WORKER_STAMPS)
             st[1] = worker_stamp();
-        if (lane == 0)
+        if (threadIdx.x == 0)
             __hip_atomic_store(&ms->seen, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         const WorkerReq &rq = ms->req;
-        /* an inline record's first two elements per lane, loaded with the request (unused otherwise) */
+        /* an inline record's element 64 w + l for lane l of wave w, and wave 0's element l + 64, loaded with the request
+         * (unused otherwise) */
         V4 pin[2];
-#pragma unroll
-        for (int m = 0; m < 2; ++m)
-            pin[m] = load_full(ms->data + 16 * (size_t)(lane + 64 * m));
+        pin[0] = load_full(ms->data + 16 * (size_t)(lane + 64 * wave));
+        pin[1] = wave == 0 ? load_full(ms->data + 16 * (size_t)(lane + 64)) : V4{0, 0, 0, 0};
         const ptls_hip_record_t rec = rq.rec;
         const uint32_t flags = __builtin_amdgcn_readfirstlane(rq.flags);
         const uint8_t *in = as_global(rq.in), *aad = as_global(rq.aad);
@@ -708,88 +843,105 @@ __global__ void __launch_bounds__(64)
         const KeySlot *slots = as_global(rq.slots);
         uint32_t *done = as_global(rq.done);
         const uint32_t done_seq = __builtin_amdgcn_readfirstlane(rq.done_seq);
+        const ptls_hip_supp_t *supp = rq.supp != nullptr ? as_global(rq.supp) : nullptr;
+        const KeySlot *hp_slots = rq.hp_slots != nullptr ? as_global(rq.hp_slots) : nullptr;
+        uint8_t *mask = rq.mask != nullptr ? as_global(rq.mask) : nullptr;
+        uint64_t *result = as_global(rq.result);
+        const uint32_t *basis = as_global(rq.basis);
+        const bool open = (flags & WREQ_OPEN) != 0, a256 = (flags & WREQ_AES256) != 0;
+        const int na1 = ((int)rec.aad_len + 15) >> 4, nc1 = ((int)rec.len + 15) >> 4;
+        const int n1 = na1 + nc1 + 1;
+        const bool mw = n1 >= MW_MIN_N && n1 <= MW_MAX_N;
         if (WORKER_STAMPS)
             st[2] = worker_stamp();
         /* WORKER_STAMPS builds (with STAMP_PHASES): the record's phase stamps (shader cycles) go to the end of the data area,
          * clk[1] = the request loaded, clk[9] = the record done */
         uint64_t *wclk = WORKER_STAMPS ? reinterpret_cast<uint64_t *>(ms->data + WORKER_DATA - 128) : nullptr;
-        if (WORKER_STAMPS) {
+        if (WORKER_STAMPS && wave == 0) {
             const uint64_t t = __builtin_amdgcn_s_memtime();
             if (lane == 0)
                 wclk[1] = t;
         }
-        if (flags & WREQ_ECB) {
-            const V4 blk = V4{rq.blk[0], rq.blk[1], rq.blk[2], rq.blk[3]};
-            const V4 m = (flags & WREQ_AES256) ? aes_encrypt<14>(lds, lb_aes, slots->rk, blk) : aes_encrypt<10>(lds, lb_aes, slots->rk, blk);
-            if (lane == 0)
-                store_full(out, m);
-        } else {
-            /* the record's first two elements per lane, as the launched single-record kernel reads them */
-            V4 pre[2] = {V4{0, 0, 0, 0}, V4{0, 0, 0, 0}};
-            if (flags & WREQ_INLINE) {
-                pre[0] = pin[0];
-                pre[1] = pin[1];
-            } else {
-                const int na1 = ((int)rec.aad_len + 15) >> 4, nc1 = ((int)rec.len + 15) >> 4;
-#pragma unroll
-                for (int m = 0; m < 2; ++m) {
-                    const int i = lane + 64 * m;
-                    if (i < na1)
-                        pre[m] = load_full(aad + rec.aad_off + 16 * (size_t)i);
-                    else if (i < na1 + nc1)
-                        pre[m] = load_full(in + rec.in_off + 16 * (size_t)(i - na1));
-                }
-            }
-            const ptls_hip_supp_t *supp = rq.supp != nullptr ? as_global(rq.supp) : nullptr;
-            const KeySlot *hp_slots = rq.hp_slots != nullptr ? as_global(rq.hp_slots) : nullptr;
-            uint8_t *mask = rq.mask != nullptr ? as_global(rq.mask) : nullptr;
-            uint64_t *result = as_global(rq.result);
-            const uint32_t *basis = as_global(rq.basis);
-            const bool open = (flags & WREQ_OPEN) != 0, a256 = (flags & WREQ_AES256) != 0;
-            const uint32_t ctab = SP_TAB + 8192u;
+        /* an element read from the caller's staging (records that do not fit inline) */
+        auto elem_block = [&](int i) __attribute__((always_inline)) {
+            V4 v = V4{0, 0, 0, 0};
+            if (i < na1)
+                v = load_full(aad + rec.aad_off + 16 * (size_t)i);
+            else if (i < na1 + nc1)
+                v = load_full(in + rec.in_off + 16 * (size_t)(i - na1));
+            return v;
+        };
+        if (mw) {
+            const V4 mine = (flags & WREQ_INLINE) ? pin[0] : elem_block(lane + 64 * wave);
+            const uint32_t ctab_w = wave == 0 ? CTAB0 : CTAB1;
             if (open && a256)
-                sparse_record<14, true, true, true>(lds, lane, lb_aes, tab, rec, 0, in, aad, out, result, slots, basis, supp,
-                                                    hp_slots, 1, mask, true, pre, wclk, WORKER_STAMPS, false, pa, ctab);
+                mw_record<14, true, true>(lds, wave, lane, lb_aes, ctab_w, tab, rec, in, aad, out, result, slots, basis, supp, hp_slots, 1, mask, mine);
             else if (open)
-                sparse_record<10, true, true, true>(lds, lane, lb_aes, tab, rec, 0, in, aad, out, result, slots, basis, supp,
-                                                    hp_slots, 1, mask, true, pre, wclk, WORKER_STAMPS, false, pa, ctab);
+                mw_record<10, true, true>(lds, wave, lane, lb_aes, ctab_w, tab, rec, in, aad, out, result, slots, basis, supp, hp_slots, 1, mask, mine);
             else if (a256)
-                sparse_record<14, false, true, true>(lds, lane, lb_aes, tab, rec, 0, in, aad, out, result, slots, basis, supp,
-                                                     hp_slots, 1, mask, true, pre, wclk, WORKER_STAMPS, false, pa, ctab);
+                mw_record<14, false, true>(lds, wave, lane, lb_aes, ctab_w, tab, rec, in, aad, out, result, slots, basis, supp, hp_slots, 1, mask, mine);
             else
-                sparse_record<10, false, true, true>(lds, lane, lb_aes, tab, rec, 0, in, aad, out, result, slots, basis, supp,
-                                                     hp_slots, 1, mask, true, pre, wclk, WORKER_STAMPS, false, pa, ctab);
+                mw_record<10, false, true>(lds, wave, lane, lb_aes, ctab_w, tab, rec, in, aad, out, result, slots, basis, supp, hp_slots, 1, mask, mine);
+        } else if (wave == 0) {
+            {
+                /* the record's first two elements per lane, as the launched single-record kernel reads them */
+                V4 pre[2];
+                if (flags & WREQ_INLINE) {
+                    pre[0] = pin[0];
+                    pre[1] = pin[1];
+                } else {
+                    pre[0] = elem_block(lane);
+                    pre[1] = elem_block(lane + 64);
+                }
+                const uint32_t ctab = CTAB0;
+                if (open && a256)
+                    sparse_record<14, true, true, true>(lds, lane, lb_aes, tab, rec, 0, in, aad, out, result, slots, basis, supp,
+                                                        hp_slots, 1, mask, true, pre, wclk, WORKER_STAMPS, false, pa, ctab);
+                else if (open)
+                    sparse_record<10, true, true, true>(lds, lane, lb_aes, tab, rec, 0, in, aad, out, result, slots, basis, supp,
+                                                        hp_slots, 1, mask, true, pre, wclk, WORKER_STAMPS, false, pa, ctab);
+                else if (a256)
+                    sparse_record<14, false, true, true>(lds, lane, lb_aes, tab, rec, 0, in, aad, out, result, slots, basis, supp,
+                                                         hp_slots, 1, mask, true, pre, wclk, WORKER_STAMPS, false, pa, ctab);
+                else
+                    sparse_record<10, false, true, true>(lds, lane, lb_aes, tab, rec, 0, in, aad, out, result, slots, basis, supp,
+                                                         hp_slots, 1, mask, true, pre, wclk, WORKER_STAMPS, false, pa, ctab);
+            }
         }
-        if (WORKER_STAMPS) {
-            st[3] = worker_stamp();
-            const uint64_t t = __builtin_amdgcn_s_memtime();
-            if (lane == 0)
-                wclk[9] = t;
-        }
-        /* every store of the call reaches system scope before its completion word; then the slot is free again */
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-        if (WORKER_STAMPS) {
-            st[4] = worker_stamp();
-            if (lane < 5)
-                __hip_atomic_store(&ms->stamps[lane], lane == 0 ? st[0] : lane == 1 ? st[1] : lane == 2 ? st[2] : lane == 3 ? st[3] : st[4],
-                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        /* the wave holding the tag (wave 1 of a two-wave record; wave 0 otherwise): every store of the call reaches system
+         * scope before its completion word (wave 0 of a two-wave record released its own before mw_record's barrier) */
+        if (wave == (mw ? 1 : 0)) {
+            if (WORKER_STAMPS) {
+                st[3] = worker_stamp();
+                const uint64_t t = __builtin_amdgcn_s_memtime();
+                if (lane == 0)
+                    wclk[9] = t;
+            }
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+            if (WORKER_STAMPS) {
+                st[4] = worker_stamp();
+                if (lane < 5)
+                    __hip_atomic_store(&ms->stamps[lane], lane == 0 ? st[0] : lane == 1 ? st[1] : lane == 2 ? st[2] : lane == 3 ? st[3] : st[4],
+                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+            }
+            if (lane == 0) {
+                __hip_atomic_store(done, done_seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                __hip_atomic_store(&ms->served, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+            }
         }
-        if (lane == 0) {
-            __hip_atomic_store(done, done_seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            __hip_atomic_store(&ms->served, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-        }
+        __syncthreads(); /* both waves are done with the request (its LDS tables, the verdict slot) */
         last = seq;
         t_last = __builtin_amdgcn_s_memrealtime();
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-    if (lane == 0)
+    if (threadIdx.x == 0)
         __hip_atomic_store(&ms->exited, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 int launch_plugin_worker(WorkerSlot *mb, uint32_t epoch, const uint32_t *t0, uint64_t idle_ticks, uint64_t life_ticks, void *stream)
 {
-    hipLaunchKernelGGL(plugin_worker_kernel, dim3(1), dim3(64), 0, static_cast<hipStream_t>(stream), mb, epoch, t0, idle_ticks,
+    hipLaunchKernelGGL(plugin_worker_kernel, dim3(1), dim3(WORKER_WG), 0, static_cast<hipStream_t>(stream), mb, epoch, t0, idle_ticks,
                        life_ticks);
     return (int)hipGetLastError();
 }

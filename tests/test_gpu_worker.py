@@ -1,11 +1,11 @@
-"""The plugin worker (engine.cpp worker_call, sparse_kernel.hip plugin_worker_kernel): a resident one-wave kernel that
+"""The plugin worker (engine.cpp worker_call, sparse_kernel.hip plugin_worker_kernel): a resident two-wave kernel that
 serves plugin calls from a pinned mailbox instead of one launch per call.  Its lifecycle is exercised through the
 reference's own picotls lifecycle code (tests/plugin_driver.py) and every output is compared with lib/fusion.c
 (oracle/_ref): calls separated by gaps longer than the worker's idle timeout (it leaves, the next call relaunches it),
 IV changes (ptls_aead_xor_iv: the worker leaves before the key slot's IV is rewritten), contexts created and freed
-between calls (a freed key slot's address comes back with other keys), header-protection ECB blocks interleaved with
-AEAD calls on one worker, and two threads sharing it.  Each case runs in its own process, with the worker on and off
-(PTLS_HIP_PLUGIN_WORKER=0: one launch per call)."""
+between calls (a freed key slot's address comes back with other keys), header-protection ECB blocks (one launch each) and
+fused header protection interleaved with AEAD calls on the worker, and two threads sharing it.  Each case runs in its
+own process, with the worker on (the default) and off (PTLS_HIP_PLUGIN_WORKER=0: one launch per call)."""
 import os
 import subprocess
 import sys
