@@ -126,8 +126,10 @@ def make_workload(cfg, rank, world=1, scaling="weak", n_full=None):
         seq = (idx // K).astype(np.uint64)
     lens = record_lengths(cfg, idx)
     aad_len = 5 if cfg["aad"] == "tls" else 13
-    # records at 16-byte aligned offsets; PTLS_BENCH_ALIGN (environment, for traffic A/B) overrides the alignment
-    align = int(os.environ.get("PTLS_BENCH_ALIGN", "16"))
+    # records at 128-byte (L2 line) aligned offsets: no line holds the end of one record and the start of the next, which
+    # different waves would write at different times (c3 at 16-byte alignment: 1.21x the algorithmic HBM bytes, at 128:
+    # 1.05x, seal 5.15 -> 4.97 ms; profiles/r03_traffic_c3_align*.json).  PTLS_BENCH_ALIGN (environment) overrides it.
+    align = int(os.environ.get("PTLS_BENCH_ALIGN", "128"))
     recs, in_total, out_total, _ = ptls_hip.layout_records(lens, np.full(n, aad_len), keyslot, seq, align=align)
     recs["aad_off"] = np.arange(n, dtype=np.uint64) * np.uint64(16)
     return idx, recs, in_total, out_total, lens
@@ -425,7 +427,7 @@ def host_e2e(args, cfg, eng, ks, recs, lens, d_pt, d_aad, aad_len):
     h_res = torch.zeros(n, dtype=torch.int64).pin_memory()
     sub_o = sub.copy()
     sub_o["in_off"], sub_o["out_off"] = sub["out_off"], sub["in_off"]
-    # compare record bytes only (gaps between 16-byte aligned records are never written)
+    # compare record bytes only (gaps between aligned records are never written)
     edge = np.zeros(in_hi - in_lo + 1, dtype=np.int32)
     np.add.at(edge, sub["in_off"].astype(np.int64), 1)
     np.add.at(edge, (sub["in_off"] + sub["len"]).astype(np.int64), -1)

@@ -1,5 +1,5 @@
 #!/bin/bash
-# round 3, call 14: ECB back on its own launch; worker + size sweep; plugin latency; c3 HBM traffic with records at 16- and
+# round 3, call 14 (second run, the call-13 build: the first run of this call on a build with constant-space key pointers and worker ECB requests faulted in the lifecycle test, reverted); worker + size sweep; plugin latency; c3 HBM traffic with records at 16- and
 # 128-byte aligned offsets (PTLS_BENCH_ALIGN), each pass under its own limit (tools/profile_round.sh)
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}" || exit 1
 export HSA_ENABLE_IPC_MODE_LEGACY=0 TMPDIR=/tmp
@@ -16,3 +16,5 @@ for A in 16 128; do
   PTLS_BENCH_ALIGN=$A bash tools/profile_round.sh a$A c3 > "$O/traffic_a$A.log" 2>&1 || { echo "profile a$A rc=$?"; tail "$O/traffic_a$A.log"; exit 1; }
   grep -E "traffic_over|fetch_bytes_per|write_bytes_per|bench_seal" "$O/traffic_a$A.log"
 done
+timeout -k 10 200 python tools/worker_stamps.py > "$O/wstamps.log" 2>&1 || { echo "wstamps rc=$?"; tail "$O/wstamps.log"; exit 1; }
+grep -v amdgpu.ids "$O/wstamps.log"
