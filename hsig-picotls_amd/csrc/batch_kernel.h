@@ -66,6 +66,9 @@ __host__ __device__ constexpr uint32_t lds_bytes(int log2g)
 #ifndef DYN_DEAL
 #define DYN_DEAL 1 /* waves draw tasks from a workgroup counter in LDS instead of a fixed per-chunk deal: c2 +3 %, c3 +5 %, c4 +5 % */
 #endif
+#ifndef G32_WIN
+#define G32_WIN 1 /* G = 32 lane combination: 1 = shared per-key window tables (gf_win4_mul), 0 = gf_mul_valu */
+#endif
 #ifndef VALU_TREE
 #define VALU_TREE 0 /* 1: combine a record's G partial sums by one VALU multiply per lane (H^(q+1) from the key slot's
                        power table) and an XOR butterfly instead of the log2(G)-level LDS nibble-table tree.
@@ -912,7 +915,7 @@ __device__ __forceinline__ void build_aes_tables(uint8_t *lds, uint32_t base, co
  * stores whose 8-lane groups hold 8 different positions p, i.e. 8 different bank quads (conflict-free).
  * (Per entry from up to 8 basis loads with lanes 256 B apart cost a key switch 8x the loads and 8-way store
  * conflicts.)  The other threads build the tree tables meanwhile. */
-__device__ void build_ghash_tables(uint8_t *lds, const uint32_t *__restrict__ basis, int log2g, bool tree = true)
+__device__ void build_ghash_tables(uint8_t *lds, const uint32_t *__restrict__ basis, int log2g, bool tree = true, bool win = false)
 {
     const uint32_t *bm = basis + log2g * 128 * 4;
     const int tid = (int)threadIdx.x;
@@ -953,6 +956,23 @@ __device__ void build_ghash_tables(uint8_t *lds, const uint32_t *__restrict__ ba
             }
         }
         lds128_store(lds, LDS_GTREE + d * LDS_TREE_STRIDE + p * 256 + v * 16, acc);
+    }
+    /* win (G = 32, no tree): the lane combination's shared window tables in the tree area, [q][slot (n + q) mod 16] =
+     * n * H^(q + 1) for q < 32, n < 16, in gf_win4_mul's big-endian words (gf_win4_build's entries, shared by every lane of
+     * the workgroup whose record position is q) */
+    for (int e = tid - t0; win && e >= 0 && e < 32 * 16; e += nt) {
+        const int q = e >> 4, n = e & 15;
+        const uint32_t *hp = basis + (NPOW * 128 + q) * 4; /* H^(q + 1) */
+        uint32_t m[4] = {bswap32(hp[0]), bswap32(hp[1]), bswap32(hp[2]), bswap32(hp[3])}, acc[4] = {0, 0, 0, 0};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) { /* n3 -> y, n2 -> y x, n1 -> y x^2, n0 -> y x^3 */
+            if ((n >> (3 - k)) & 1)
+#pragma unroll
+                for (int w = 0; w < 4; ++w)
+                    acc[w] ^= m[w];
+            mulx_be(m);
+        }
+        lds128_store(lds, LDS_GTREE + (uint32_t)q * 256u + (uint32_t)((n + q) & 15) * 16u, V4{acc[0], acc[1], acc[2], acc[3]});
     }
 }
 
@@ -1223,6 +1243,9 @@ __global__ void __launch_bounds__(WGT)
     static_assert(G >= 1 && G <= 32 && (G & (G - 1)) == 0, "lanes per record: 1, 2, 4, 8, 16 or 32");
     /* DYN_DEAL: the task counter sits after the tables; SPLIT (G >= 16): then the split-record slots */
     constexpr bool DYN = DYN_DEAL != 0 && SPLIT_PROBE != 1; /* the counter is reset at key switches, which SPLIT_PROBE 1 skips */
+    /* G = 32: the lane combination by 4-bit windows over a per-key table of H^1..H^32 in the (unused) tree area instead of
+     * gf_mul_valu's 1 408 VALU per lane (G32_WIN = 0: the VALU multiply) */
+    constexpr bool WINCOMB = G >= 32 && VALU_TREE == 0 && G32_WIN != 0;
     constexpr bool SPLIT = SPLIT_TASKS != 0 && G >= 16 && DYN && SPLIT_PROBE == 0 && HYBRID == 0 && KEYSWITCH_PROBE == 0;
     constexpr uint32_t LDS_SPLIT = lds_bytes(LOG2G) + 16;                 /* partials: [slot][part] 16 B each */
     constexpr uint32_t LDS_SPLIT_CTR = LDS_SPLIT + SPLIT_SLOTS * 32;      /* arrival counters: [slot] */
@@ -1256,7 +1279,7 @@ __global__ void __launch_bounds__(WGT)
         } else if (SPLIT_PROBE != 1 && ch.key != cur_key) {
             __syncthreads();
             if (KEYSWITCH_PROBE != 1 || cur_key == 0xffffffffu)
-                build_ghash_tables(lds, basis + (size_t)ch.key * (BASIS_VECS * 4), LOG2G, !(VALU_TREE != 0 || G >= 32));
+                build_ghash_tables(lds, basis + (size_t)ch.key * (BASIS_VECS * 4), LOG2G, !(VALU_TREE != 0 || G >= 32), WINCOMB);
             if (DYN && threadIdx.x == 0)
                 *task_ctr = 0;
             if (SPLIT)
@@ -1565,8 +1588,15 @@ __global__ void __launch_bounds__(WGT)
             if constexpr (VCOMB) {
                 s = V4{0, 0, 0, 0};
                 if (SPLIT_PROBE != 1) {
-                    const uint4 hp = reinterpret_cast<const uint4 *>(basis)[(size_t)ch.key * BASIS_VECS + NPOW * 128 + q]; /* H^(q+1) */
-                    s = gf_mul_valu(y, V4{hp.x, hp.y, hp.z, hp.w});
+                    if constexpr (WINCOMB) { /* the key's shared window table of H^(q+1) (build_ghash_tables) */
+                        Win4<16> wt;
+                        wt.base = LDS_GTREE + (uint32_t)q * 256u;
+                        wt.rot = (uint32_t)q & 15u;
+                        s = gf_win4_mul<16, 4>(lds, wt, y);
+                    } else {
+                        const uint4 hp = reinterpret_cast<const uint4 *>(basis)[(size_t)ch.key * BASIS_VECS + NPOW * 128 + q]; /* H^(q+1) */
+                        s = gf_mul_valu(y, V4{hp.x, hp.y, hp.z, hp.w});
+                    }
 #pragma unroll
                     for (int o = G / 2; o > 0; o >>= 1) {
                         s.w0 ^= __shfl_xor(s.w0, o, 64);
