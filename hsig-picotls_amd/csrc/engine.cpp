@@ -436,12 +436,14 @@ static int choose_lanes(const ptls_hip_record_t *recs, size_t n)
     if (per_run < SPARSE_MAX_PER_RUN)
         return SPARSE_LANES;
     /* long records, short key runs: more lanes per record give a key run more wave tasks for the workgroup's 12
-     * waves.  Measured on configs[3]'s shape (AES-256, 64 B - 16 KiB, 64K keys; tools/time_cfg.py),
-     * seal GiB/s at 16 / 32 lanes (sparse kernel): 8 records per key 126 / 258 (503), 16: 260 / 499 (516),
-     * 24: 394 / 681 (525), 32: 518 / 715, 48: 717 / 734, 64: 786 / 776. */
-    if (g == 8 && mean >= 256 && per_run < 56)
+     * waves, as long as the run fits one chunk (2 * 16 * 64 / G records): a run spilling into a second chunk costs up to
+     * 25 %.  Measured on configs[3]'s lengths (AES-256, 64 B - 16 KiB, 4M records; tools/time_cfg.py), seal
+     * GiB/s at 8 / 16 / 32 lanes, round 3 (the G = 32 window combination): 64 records per key 532 / 769 / 803, 96: 748 /
+     * 813 / 620, 128: 810 / 827 / 804, 192: 838 / 644 / 806 (tools/calls_r03/r03_call17.sh); round 2 at 16 / 32 lanes
+     * (sparse kernel): 8 per key 126 / 258 (503), 16: 260 / 499 (516), 24: 394 / 681 (525), 32: 518 / 715, 48: 717 / 734. */
+    if (g == 8 && mean >= 256 && per_run <= 64)
         return 32;
-    if (g == 8 && mean >= 256 && per_run < (double)(WG_ALT / 64) * (64 / 8))
+    if (g == 8 && mean >= 256 && per_run <= 128)
         return 16;
     return g;
 }
