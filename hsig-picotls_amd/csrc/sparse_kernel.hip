@@ -129,6 +129,7 @@ __device__ __forceinline__ V4 mulx_raw(V4 v)
 
 __device__ __forceinline__ void load_wave_basis(const uint4 *__restrict__ bp, int lane, V4 (&b)[4])
 {
+    asm volatile("" : "+v"(lane)); /* the lane's basis offset computed here, not hoisted out of the record loop (scratch) */
     const int p = lane >> 1, w = p >> 3, j = p & 7;
     /* the lane's four vectors are P x^(e0), P x^(e0 - 1), P x^(e0 - 2), P x^(e0 - 3) for one e0 (bits 4j .. 4j + 3 of
      * word w lie in one byte): SPARSE_DERIVE loads the last and store_wave_table derives the others */
@@ -182,15 +183,32 @@ __device__ __forceinline__ void store_wave_table(uint8_t *lds, uint32_t tab, V4 
 #define SPARSE_WIN_LB 4 /* the batch instantiations' lookups in flight per group (8: 32 VGPRs, spills at 168) */
 #endif
 
+/* the wave's maximum (every lane), from an opaque lane index like wave_xor below: batch_kernel.h's wave_max lets the
+ * compiler hoist its six partner addresses out of the record loop (scratch in the sparse kernel's batch instantiations) */
+__device__ __forceinline__ int wave_max_sp(int v)
+{
+    int ln = (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+    asm volatile("" : "+v"(ln));
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1)
+        v = max(v, __builtin_amdgcn_ds_bpermute((ln ^ o) << 2, v));
+    return v;
+}
+
 /* XOR butterfly over the wave: every lane ends with the sum of the 64 lanes' values */
 __device__ __forceinline__ V4 wave_xor(V4 z)
 {
+    /* the partner lanes' addresses from an opaque lane index: hoisted out of the record loop, the five (lane ^ o) * 4 stay
+     * live across the kernel and pushed the batch instantiations into scratch (reloaded from HBM per record) */
+    int ln = (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+    asm volatile("" : "+v"(ln));
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
-        z.w0 ^= __shfl_xor(z.w0, o, 64);
-        z.w1 ^= __shfl_xor(z.w1, o, 64);
-        z.w2 ^= __shfl_xor(z.w2, o, 64);
-        z.w3 ^= __shfl_xor(z.w3, o, 64);
+        const int a = (ln ^ o) << 2;
+        z.w0 ^= (uint32_t)__builtin_amdgcn_ds_bpermute(a, (int)z.w0);
+        z.w1 ^= (uint32_t)__builtin_amdgcn_ds_bpermute(a, (int)z.w1);
+        z.w2 ^= (uint32_t)__builtin_amdgcn_ds_bpermute(a, (int)z.w2);
+        z.w3 ^= (uint32_t)__builtin_amdgcn_ds_bpermute(a, (int)z.w3);
     }
     return z;
 }
@@ -223,6 +241,11 @@ __device__ __forceinline__ void sparse_record(uint8_t *lds, int lane, uint32_t l
 {
     constexpr bool by_value = BYVAL;
     (void)by_value, (void)clk, (void)stamps, (void)bstamps, (void)pa;
+    /* everything derived from the lane index is computed per record: hoisted out of the kernel's record loop, such values
+     * (partner lanes, table slots, negative lane offsets) stayed live across the whole kernel and went to scratch, which
+     * the streaming records then evicted to HBM (c4s: 84 B per lane, +4.9 KB of HBM traffic per record) */
+    lane = (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)); /* recomputed, not carried across records */
+    asm volatile("" : "+v"(lane));
     const uint32_t key = __builtin_amdgcn_readfirstlane(rec.key);
     const KeySlot *__restrict__ slot = slots + key;
     const uint32_t *__restrict__ rk = slot->rk;
@@ -311,7 +334,7 @@ __device__ __forceinline__ void sparse_record(uint8_t *lds, int lane, uint32_t l
             ks[b] = V4{n0, n1, n2, cw[b]};
             big |= (e[b].is_c && e[b].c >= 65534) ? 1 : 0;
         }
-        if (wave_max(big)) {
+        if (wave_max_sp(big)) {
             aes_encrypt_n<ROUNDS, NE>(lds, lb_aes, rk, ks);
         } else if (!SPARSE_GEN_SKEW) {
             aes_ctr_n<ROUNDS, NE>(lds, lb_aes, rk, cc, cw, ks);
@@ -350,13 +373,13 @@ __device__ __forceinline__ void sparse_record(uint8_t *lds, int lane, uint32_t l
      * record, tools/sparse_stamps.py) is gone. */
     const int ml = lane < na ? (na - lane + 63) >> 6 : 0;                          /* the lane's first data element */
     const int mhl = lastc + na - lane >= 0 ? ((lastc + na - lane) >> 6) + 1 : 0;  /* its elements m < mhl: full blocks */
-    const int npure = SPARSE_PURE ? -wave_max(-max(mhl - ml, 0)) / KP : 0;
+    const int npure = SPARSE_PURE ? -wave_max_sp(-max(mhl - ml, 0)) / KP : 0;
     const int iters_l = lane < N ? ((N - 1 - lane) >> 6) + 1 : 0;                /* the lane's elements */
     const int pm1 = ml + npure * KP;                                              /* the lane's first after the stretch */
     if (!npure) { /* head and tail are one range: elements share one round trip to the record's memory (the plugin) */
         generic_range(std::integral_constant<bool, BYVAL>{}, 0, iters);
     } else { /* the lane's AAD elements: GHASH only */
-        const int naad = wave_max(ml);
+        const int naad = wave_max_sp(ml);
         for (int j = 0; j < naad; ++j) {
             if (j < ml) {
                 const int i = lane + 64 * j;
@@ -440,7 +463,7 @@ __device__ __forceinline__ void sparse_record(uint8_t *lds, int lane, uint32_t l
     phase_stamp(clk, stamps, lane, 5);
     phase_acc(pa, bstamps, 5);
     if (npure) { /* the rest of each lane's elements from its own position (partial, length and leftover blocks) */
-        const int rest = wave_max(max(iters_l - pm1, 0));
+        const int rest = wave_max_sp(max(iters_l - pm1, 0));
         int j = 0;
         for (; j + 1 < rest; j += 2)
             generic(std::integral_constant<int, 2>{}, std::false_type{}, pm1 + j, iters_l);
