@@ -54,7 +54,8 @@ constexpr int MAX_LANES = 32;    /* lanes per record (G) of the batch kernel: 1,
 constexpr int SPARSE_LANES = 64; /* "lanes" value of the wave-per-record kernel (sparse_kernel.hip) */
 /* the planner picks that kernel when a batch's key runs hold fewer records than this on average */
 #ifndef SPARSE_MAX_PER_RUN
-#define SPARSE_MAX_PER_RUN 16 /* measured tie with 32 lanes per record at 16 AES-256 records of 64 B-16 KiB per key */
+#define SPARSE_MAX_PER_RUN 20 /* configs[3]'s lengths, seal GiB/s, sparse kernel / 32 lanes (round 3): 16 records per key 533 / 498,
+                                 24 per key 533 / 680 (tools/calls_r03/r03_call24.sh) */
 #endif
 /* one workgroup per CU (LDS-limited); 768 threads (3 waves per SIMD, 168 VGPRs) by default, 512 selectable
  * per batch (engine.cpp:plan_wg).  WG_MAX bounds the chunk size the planner cuts key runs into. */
