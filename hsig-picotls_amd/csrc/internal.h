@@ -34,9 +34,9 @@
 
 namespace ptls_hip {
 
-constexpr int NPOW = SPLIT_TASKS ? 10 : 7; /* H^1 .. H^16 (batch kernel main and tree tables), H^32 (batch kernel main table
-                                              at G = 32), H^64 (sparse kernel); SPLIT_TASKS: H^128 .. H^512 (the shift of a
-                                              split record's first part, batch_kernel.h) */
+constexpr int NPOW = SPLIT_TASKS ? 10 : 8; /* H^1 .. H^16 (batch kernel main and tree tables), H^32 (batch kernel main table
+                                              at G = 32), H^64 (sparse kernel), H^128 (a single record on two waves, stride
+                                              128); SPLIT_TASKS: H^128 .. H^512 (the shift of a split record's first part) */
 /* GHASH basis slot: NPOW x 128 vectors P * x^e, then H^1 .. H^128 (the sparse kernel's per-lane final powers: H^(q+1),
  * q < 64; a two-wave single record of up to 128 GHASH elements multiplies element i by H^(N - i)) */
 constexpr int LANE_POWS = 128;
@@ -49,7 +49,7 @@ constexpr int LANE_POWS = 128;
 /* with HYBRID, the slot also holds the bit-sliced round keys 1..rounds (bs8::slice_key: 32 words per round) */
 constexpr int BS_KEY_OFF = NPOW * 128 + LANE_POWS; /* uint4 offset in the slot */
 constexpr int BS_KEY_VECS = HYBRID ? 14 * 32 / 4 : 0;
-constexpr int BASIS_VECS = BS_KEY_OFF + BS_KEY_VECS; /* uint4 per key slot (16 KiB; 17.75 KiB with HYBRID, 22 KiB with SPLIT_TASKS) */
+constexpr int BASIS_VECS = BS_KEY_OFF + BS_KEY_VECS; /* uint4 per key slot (18 KiB; 19.75 KiB with HYBRID, 22 KiB with SPLIT_TASKS) */
 constexpr int MAX_LANES = 32;    /* lanes per record (G) of the batch kernel: 1, 2, 4, 8, 16, 32 */
 constexpr int SPARSE_LANES = 64; /* "lanes" value of the wave-per-record kernel (sparse_kernel.hip) */
 /* the planner picks that kernel when a batch's key runs hold fewer records than this on average */

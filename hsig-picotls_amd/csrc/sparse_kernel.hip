@@ -230,15 +230,22 @@ __device__ __forceinline__ V4 ghash_combine(uint8_t *lds, uint32_t tab, int lane
  * constants, its per-wave H^64 table, the elements (generic head / branch-free stretch / generic tail), the lane
  * combination, the tag, header protection.  pre / prefetch: a single record's first two elements per lane, read before
  * (BYVAL: the plugin's launch and the worker). */
-template <int ROUNDS, bool OPEN, bool ALIGNED, bool BYVAL>
+template <int ROUNDS, bool OPEN, bool ALIGNED, bool BYVAL, int S = 64>
 __device__ __forceinline__ void sparse_record(uint8_t *lds, int lane, uint32_t lb_aes, uint32_t tab, const ptls_hip_record_t &rec,
                                               uint32_t rec_i, const uint8_t *in, const uint8_t *__restrict__ aad, uint8_t *out,
                                               uint64_t *__restrict__ result, const KeySlot *__restrict__ slots,
                                               const uint32_t *__restrict__ basis, const ptls_hip_supp_t *__restrict__ supp,
                                               const KeySlot *__restrict__ hp_slots, uint32_t hp_nslots, uint8_t *mask, bool prefetch,
                                               const V4 (&pre)[2], uint64_t *__restrict__ clk, bool stamps, bool bstamps, PhaseAcc &pa,
-                                              uint32_t ctab)
+                                              uint32_t ctab, int vw = 0, uint32_t xslot = 0)
 {
+    /* S = 64: one wave per record (lane l: elements l + 64 m, Horner with H^64).  S = 128 (a single long record on two
+     * waves, vw = this wave's index 0 / 1): the two waves act as one 128-lane wave, virtual lane vl = 64 vw + l takes
+     * elements vl + 128 m with Horner by H^128 (basis plane 7) and multiplies its sum by H^(q+1), q = (N - 1 - vl) mod 128
+     * (keysetup's list); wave 0's sum joins wave 1's through LDS (xslot) after a workgroup barrier, and the wave holding
+     * the length block (q = 0) writes the tag.  Every element index below goes through vl and S. */
+    static_assert(S == 64 || S == 128, "stride: one or two waves");
+    constexpr int LOG2S = S == 64 ? 6 : 7;
     constexpr bool by_value = BYVAL;
     (void)by_value, (void)clk, (void)stamps, (void)bstamps, (void)pa;
     /* everything derived from the lane index is computed per record: hoisted out of the kernel's record loop, such values
@@ -246,6 +253,7 @@ __device__ __forceinline__ void sparse_record(uint8_t *lds, int lane, uint32_t l
      * the streaming records then evicted to HBM (c4s: 84 B per lane, +4.9 KB of HBM traffic per record) */
     lane = (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)); /* recomputed, not carried across records */
     asm volatile("" : "+v"(lane));
+    const int vl = 64 * vw + lane; /* the virtual lane (S = 64: the lane) */
     const uint32_t key = __builtin_amdgcn_readfirstlane(rec.key);
     const KeySlot *__restrict__ slot = slots + key;
     const uint32_t *__restrict__ rk = slot->rk;
@@ -262,13 +270,13 @@ __device__ __forceinline__ void sparse_record(uint8_t *lds, int lane, uint32_t l
     const uint32_t n0 = __builtin_amdgcn_readfirstlane(slot->iv[0]),
                    n1 = __builtin_amdgcn_readfirstlane(slot->iv[1] ^ bswap32((uint32_t)(rec.seq >> 32))),
                    n2 = __builtin_amdgcn_readfirstlane(slot->iv[2] ^ bswap32((uint32_t)rec.seq));
-    const int iters = (N + 63) >> 6;
-    const bool horner = SPARSE_ABLATE != 3 && iters > 1; /* N <= 64: one element per lane, no Horner step */
+    const int iters = (N + S - 1) >> LOG2S;
+    const bool horner = SPARSE_ABLATE != 3 && iters > 1; /* N <= S: one element per lane, no Horner step */
     V4 b[4];
     /* a single record (the plugin's launch): the H^64 basis loads go out before the counter-mode constants, so their
      * memory latency overlaps that LDS chain (in batches other waves hide it; there the early loads cost c4s open
      * 2.5 %, measured) */
-    const int q = (N - 1 - lane) & 63;
+    const int q = (N - 1 - vl) & (S - 1);
     /* a single record builds its lane-combination table (the 16 multiples of H^(q+1)) early, in an LDS area of its own
      * (ctab), so that only the lookups remain after its last element */
     constexpr bool early_win = BYVAL && SPARSE_WIN;
@@ -276,7 +284,7 @@ __device__ __forceinline__ void sparse_record(uint8_t *lds, int lane, uint32_t l
     if (early_win)
         hpe = bs[NPOW * 128 + q]; /* H^(q+1) */
     if (horner && by_value)
-        load_wave_basis(bs + 6 * 128, lane, b); /* H^64 */
+        load_wave_basis(bs + LOG2S * 128, lane, b); /* H^S */
     /* the record (and so its counter-mode constants) is the wave's alone: keep them in SGPRs */
     CtrConst cc = ctr_const(lds, lb_aes, rk, n0, n1, n2);
     cc.k10 = __builtin_amdgcn_readfirstlane(cc.k10);
@@ -295,7 +303,7 @@ __device__ __forceinline__ void sparse_record(uint8_t *lds, int lane, uint32_t l
     wave_lds_sync(); /* the previous record's Horner reads of the table are done */
     if (horner) { /* (loading the basis during the previous record's VALU combine measured no faster: other waves hide it) */
         if (!by_value)
-            load_wave_basis(bs + 6 * 128, lane, b); /* H^64 */
+            load_wave_basis(bs + LOG2S * 128, lane, b); /* H^S */
         store_wave_table(lds, tab, b, lane);
     }
     wave_lds_sync();
@@ -314,7 +322,7 @@ __device__ __forceinline__ void sparse_record(uint8_t *lds, int lane, uint32_t l
         int big = 0;
 #pragma unroll
         for (int b = 0; b < NE; ++b) {
-            e[b] = elem_of(m + b < mend ? lane + (m + b) * 64 : N, N, na, nc, L, N);
+            e[b] = elem_of(m + b < mend ? vl + (m + b) * S : N, N, na, nc, L, N);
             inb[b] = V4{0, 0, 0, 0};
             /* the lane's first two elements of a single record were read at the start (pre) */
             const bool have_pre = USE_PRE && prefetch && m + b < 2;
@@ -371,10 +379,10 @@ __device__ __forceinline__ void sparse_record(uint8_t *lds, int lane, uint32_t l
      * others) and ends where its blocks stop being full: the stretch is the shortest lane's, the AAD elements before
      * it are hashed only, and the record's generic head (one full AES per lane for one AAD block, 17 % of a c4s
      * record, tools/sparse_stamps.py) is gone. */
-    const int ml = lane < na ? (na - lane + 63) >> 6 : 0;                          /* the lane's first data element */
-    const int mhl = lastc + na - lane >= 0 ? ((lastc + na - lane) >> 6) + 1 : 0;  /* its elements m < mhl: full blocks */
+    const int ml = vl < na ? (na - vl + S - 1) >> LOG2S : 0;                      /* the lane's first data element */
+    const int mhl = lastc + na - vl >= 0 ? ((lastc + na - vl) >> LOG2S) + 1 : 0;  /* its elements m < mhl: full blocks */
     const int npure = SPARSE_PURE ? -wave_max_sp(-max(mhl - ml, 0)) / KP : 0;
-    const int iters_l = lane < N ? ((N - 1 - lane) >> 6) + 1 : 0;                /* the lane's elements */
+    const int iters_l = vl < N ? ((N - 1 - vl) >> LOG2S) + 1 : 0;                /* the lane's elements */
     const int pm1 = ml + npure * KP;                                              /* the lane's first after the stretch */
     if (!npure) { /* head and tail are one range: elements share one round trip to the record's memory (the plugin) */
         generic_range(std::integral_constant<bool, BYVAL>{}, 0, iters);
@@ -382,7 +390,7 @@ __device__ __forceinline__ void sparse_record(uint8_t *lds, int lane, uint32_t l
         const int naad = wave_max_sp(ml);
         for (int j = 0; j < naad; ++j) {
             if (j < ml) {
-                const int i = lane + 64 * j;
+                const int i = vl + S * j;
                 const int nb = min(16, A - 16 * i);
                 const V4 x = (BYVAL && prefetch && j < 2) ? mask_block(j == 0 ? pre[0] : pre[1], nb)
                                                           : load_block<ALIGNED>(aad_p + 16 * i, nb);
@@ -393,7 +401,7 @@ __device__ __forceinline__ void sparse_record(uint8_t *lds, int lane, uint32_t l
     phase_stamp(clk, stamps, lane, 4);
     phase_acc(pa, bstamps, 4);
     if (npure) {
-        const int c0 = 64 * ml + lane - na; /* the lane's first data block of the stretch */
+        const int c0 = S * ml + vl - na; /* the lane's first data block of the stretch */
         const uint8_t *src = in_p + 16 * (size_t)c0;
         uint8_t *dst = out_p + 16 * (size_t)c0;
         V4 pend[KP], bufA[KP], bufB[KP];
@@ -402,19 +410,19 @@ __device__ __forceinline__ void sparse_record(uint8_t *lds, int lane, uint32_t l
          * iteration into one buffer (8 VGPRs fewer: the seal instantiations stay within 168 without scratch). */
 #pragma unroll
         for (int b = 0; b < KP; ++b)
-            bufA[b] = load_full(src + 1024 * b);
+            bufA[b] = load_full(src + 16 * S * b);
         auto pure_iter = [&](int it, bool hash_pending, V4(&d)[KP], V4(&dn)[KP]) __attribute__((always_inline)) {
-            const size_t o = (size_t)it * KP * 1024;
-            const size_t on = (size_t)min(it + 1, npure - 1) * KP * 1024;
+            const size_t o = (size_t)it * KP * 16 * S;
+            const size_t on = (size_t)min(it + 1, npure - 1) * KP * 16 * S;
             V4 k[KP];
             uint32_t cw[KP];
 #pragma unroll
             for (int b = 0; b < KP; ++b) {
                 if (OPEN)
-                    dn[b] = load_full(src + on + 1024 * b);
+                    dn[b] = load_full(src + on + 16 * S * b);
                 else if (it != 0)
-                    d[b] = load_full(src + o + 1024 * b);
-                cw[b] = bswap32((uint32_t)(c0 + 2 + (it * KP + b) * 64));
+                    d[b] = load_full(src + o + 16 * S * b);
+                cw[b] = bswap32((uint32_t)(c0 + 2 + (it * KP + b) * S));
                 k[b] = V4{n0, n1, n2, cw[b]};
             }
             __builtin_amdgcn_sched_barrier(0); /* keep the loads at the top of the iteration */
@@ -423,13 +431,13 @@ __device__ __forceinline__ void sparse_record(uint8_t *lds, int lane, uint32_t l
 #pragma unroll
                 for (int b = 0; b < KP; ++b) {
                     pend[b] = v4xor(d[b], k[b]);
-                    store_full(dst + o + 1024 * b, pend[b]);
+                    store_full(dst + o + 16 * S * b, pend[b]);
                 }
             } else if (OPEN) {
                 ctr_ghash_skewed<ROUNDS, KP, true>(lds, lb_aes, rk, cc, cw, k, y, d, GhNibble{tab});
 #pragma unroll
                 for (int b = 0; b < KP; ++b)
-                    store_full(dst + o + 1024 * b, v4xor(d[b], k[b]));
+                    store_full(dst + o + 16 * S * b, v4xor(d[b], k[b]));
             } else {
                 if (hash_pending)
                     ctr_ghash_skewed<ROUNDS, KP, true>(lds, lb_aes, rk, cc, cw, k, y, pend, GhNibble{tab});
@@ -438,7 +446,7 @@ __device__ __forceinline__ void sparse_record(uint8_t *lds, int lane, uint32_t l
 #pragma unroll
                 for (int b = 0; b < KP; ++b) {
                     pend[b] = v4xor(d[b], k[b]);
-                    store_full(dst + o + 1024 * b, pend[b]);
+                    store_full(dst + o + 16 * S * b, pend[b]);
                 }
             }
         };
@@ -481,6 +489,19 @@ __device__ __forceinline__ void sparse_record(uint8_t *lds, int lane, uint32_t l
         else
             y = ghash_combine(lds, tab, lane, bs, q, y);
     }
+    /* S = 128: the wave without the length block hands its sum over (and makes its output stores visible at system scope
+     * first: the tag wave's caller stores the completion word); both waves pass the barrier */
+    const int tagw = ((N - 1) & (S - 1)) >> 6;
+    if (S > 64) {
+        if (vw != tagw) {
+            if (lane == 0)
+                lds128_store(lds, xslot, y);
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+        }
+        __syncthreads();
+        if (vw == tagw)
+            y = v4xor(y, lds128(lds, xslot));
+    }
     phase_stamp(clk, stamps, lane, 7);
     phase_acc(pa, bstamps, 7);
     if (q == 0) {
@@ -495,7 +516,7 @@ __device__ __forceinline__ void sparse_record(uint8_t *lds, int lane, uint32_t l
     }
     phase_stamp(clk, stamps, lane, 8);
     phase_acc(pa, bstamps, 8);
-    if (!OPEN && supp != nullptr) {
+    if (!OPEN && supp != nullptr && vw == tagw) {
         /* QUIC header protection after the record (lib/fusion.c:636-650), as in aesgcm_batch_kernel: the
          * sample may cover the tag written by another lane of this wave */
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
@@ -621,8 +642,10 @@ __global__ void __launch_bounds__(WG)
                          const KeySlot *__restrict__ hp_slots, uint32_t hp_nslots, uint8_t *mask, ptls_hip_record_t one,
                          uint32_t *done, uint32_t done_seq, uint64_t *__restrict__ clk)
 {
-    /* BYVAL: 16 KiB more for wave 1's windowed table of a two-wave record (mw_record) */
-    constexpr uint32_t LDS_SIZE = SP_TAB + (WG / 64) * 8192 + (BYVAL ? 16384 : 0);
+    /* BYVAL: 16 KiB more for wave 1's windowed table of a two-wave record (mw_record, or a long record at stride 128),
+     * then 2 KiB for wave 1's prefetched elements of a long record and 64 B for the waves' hand-over */
+    constexpr uint32_t XCH2 = SP_TAB + (WG / 64) * 8192 + 16384, XSLOT = XCH2 + 2048;
+    constexpr uint32_t LDS_SIZE = SP_TAB + (WG / 64) * 8192 + (BYVAL ? 16384 + 2048 + 64 : 0);
     __shared__ __attribute__((aligned(16))) uint8_t lds[LDS_SIZE];
     static_assert(LDS_SIZE <= 163840, "AES tables + per-wave GHASH tables must fit the CU's 160 KiB");
     const int lane = threadIdx.x & 63;
@@ -648,18 +671,28 @@ __global__ void __launch_bounds__(WG)
      * AAD block or the data block, whole 16 bytes: the plugin's own pinned staging holds them) and touches its key slot
      * and its lane's final power before the AES tables are built, so those PCIe / HBM latencies run under the build
      * instead of after it (tools/plugin_stamps.py).  pre[m] = element lane + 64 m. */
-    V4 pre[2] = {V4{0, 0, 0, 0}, V4{0, 0, 0, 0}};
+    V4 pre[2] = {V4{0, 0, 0, 0}, V4{0, 0, 0, 0}}, pre_hi[2] = {V4{0, 0, 0, 0}, V4{0, 0, 0, 0}};
     V4 touch = V4{0, 0, 0, 0};
     const bool prefetch = BV_PREFETCH && by_value && blockIdx.x == 0 && threadIdx.x < 64;
+    /* a single record longer than MW_MAX_N GHASH elements runs on waves 0 and 1 at stride 128 (sparse_record S = 128):
+     * wave 0 reads elements lane + 64 m, m < 4; it keeps m = 0, 2 and hands m = 1, 3 to wave 1 through LDS (XCH2) */
+    const int n_one = BYVAL ? (((int)one.aad_len + 15) >> 4) + (((int)one.len + 15) >> 4) + 1 : 0;
+    const bool longrec = BYVAL && STAMP_PHASES == 0 && WG >= 128 && n_one > MW_MAX_N;
     if (prefetch) {
         const int na1 = ((int)one.aad_len + 15) >> 4, nc1 = ((int)one.len + 15) >> 4;
-#pragma unroll
-        for (int m = 0; m < 2; ++m) {
-            const int i = lane + 64 * m;
+        auto elem16 = [&](int i) __attribute__((always_inline)) {
+            V4 v = V4{0, 0, 0, 0};
             if (i < na1)
-                pre[m] = load_full(aad + one.aad_off + 16 * (size_t)i);
+                v = load_full(aad + one.aad_off + 16 * (size_t)i);
             else if (i < na1 + nc1)
-                pre[m] = load_full(in + one.in_off + 16 * (size_t)(i - na1));
+                v = load_full(in + one.in_off + 16 * (size_t)(i - na1));
+            return v;
+        };
+        pre[0] = elem16(lane);
+        pre[1] = elem16(lane + 64);
+        if (longrec) {
+            pre_hi[0] = elem16(lane + 128);
+            pre_hi[1] = elem16(lane + 192);
         }
         const uint4 *bsk = reinterpret_cast<const uint4 *>(basis) + (size_t)one.key * BASIS_VECS;
         const uint4 kv = reinterpret_cast<const uint4 *>(slots + one.key)[lane & 15];       /* round keys, IV: 256 B */
@@ -676,11 +709,14 @@ __global__ void __launch_bounds__(WG)
     }
     /* a two-wave record (mw_record): wave 1's element lane + 64 was prefetched by wave 0 (pre[1]); it goes through LDS
      * (wave 3's table area, unused by a single record) */
-    const int n_one = BYVAL ? (((int)one.aad_len + 15) >> 4) + (((int)one.len + 15) >> 4) + 1 : 0;
     const bool mw = BYVAL && STAMP_PHASES == 0 && n_one >= MW_MIN_N && n_one <= MW_MAX_N;
     const uint32_t XCH = SP_TAB + 3u * 8192u;
     if (mw && threadIdx.x < 64)
         lds128_store(lds, XCH + (uint32_t)lane * 16u, pre[1]);
+    if (longrec && threadIdx.x < 64) {
+        lds128_store(lds, XCH2 + (uint32_t)lane * 16u, pre[1]);
+        lds128_store(lds, XCH2 + 1024u + (uint32_t)lane * 16u, pre_hi[1]);
+    }
     __syncthreads();
     asm volatile("" ::"v"(touch.w0), "v"(touch.w1), "v"(touch.w2), "v"(touch.w3)); /* keep the touch loads */
     if (mw) {
@@ -693,6 +729,34 @@ __global__ void __launch_bounds__(WG)
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
             if (lane == 0)
                 __hip_atomic_store(done, done_seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+        return;
+    }
+    if (longrec) { /* waves 0 and 1 as one 128-lane wave (sparse_record S = 128); waves 2, 3 only take its barrier */
+        const int wave = (int)(threadIdx.x >> 6);
+        if (wave < 2) {
+            V4 p2[2];
+            if (wave == 0) {
+                p2[0] = pre[0];
+                p2[1] = pre_hi[0];
+            } else {
+                p2[0] = lds128(lds, XCH2 + (uint32_t)lane * 16u);
+                p2[1] = lds128(lds, XCH2 + 1024u + (uint32_t)lane * 16u);
+            }
+            /* wave 0: its H^128 table in area 0, its combination table in areas 2-3; wave 1: area 1 and the extra 16 KiB */
+            const uint32_t tab_w = SP_TAB + (uint32_t)wave * 8192u;
+            const uint32_t ctab_w = wave == 0 ? SP_TAB + 2u * 8192u : SP_TAB + (uint32_t)(WG / 64) * 8192u;
+            sparse_record<ROUNDS, OPEN, ALIGNED, BYVAL, 128>(lds, lane, lb_aes, tab_w, one, 0, in, aad, out, result, slots, basis,
+                                                            supp, hp_slots, hp_nslots, mask, true, p2, clk, false, false, pa,
+                                                            ctab_w, wave, XSLOT);
+            const int tagw = ((n_one - 1) & 127) >> 6;
+            if (done != nullptr && wave == tagw) { /* the other wave released its stores before sparse_record's barrier */
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+                if (lane == 0)
+                    __hip_atomic_store(done, done_seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            }
+        } else {
+            __syncthreads(); /* sparse_record's hand-over barrier */
         }
         return;
     }
@@ -788,9 +852,10 @@ constexpr int WORKER_WG = 128; /* two waves: wave 0 polls; both serve a two-wave
 __global__ void __launch_bounds__(WORKER_WG)
     plugin_worker_kernel(WorkerSlot *mb, uint32_t epoch, const uint32_t *__restrict__ t0, uint64_t idle_ticks, uint64_t life_ticks)
 {
-    /* AES tables | wave 0's H^64 table | wave 0's lane-combination table | wave 1's | the poll's verdict */
-    constexpr uint32_t CTAB0 = SP_TAB + 8192, CTAB1 = CTAB0 + 16384, CTL = CTAB1 + 16384;
-    __shared__ __attribute__((aligned(16))) uint8_t lds[CTL + 16];
+    /* AES tables | wave 0's Horner table | wave 1's | wave 0's lane-combination table | wave 1's | the poll's verdict | the
+     * long record's hand-over */
+    constexpr uint32_t TAB1 = SP_TAB + 8192, CTAB0 = TAB1 + 8192, CTAB1 = CTAB0 + 16384, CTL = CTAB1 + 16384, XSLOT = CTL + 16;
+    __shared__ __attribute__((aligned(16))) uint8_t lds[XSLOT + 16];
     const int lane = threadIdx.x & 63, wave = (int)(threadIdx.x >> 6);
     const uint32_t lb_aes = (uint32_t)(lane & 31) * 4u;
     const uint32_t tab = SP_TAB;
@@ -856,9 +921,10 @@ __global__ void __launch_bounds__(WORKER_WG)
         const WorkerReq &rq = ms->req;
         /* an inline record's element 64 w + l for lane l of wave w, and wave 0's element l + 64, loaded with the request
          * (unused otherwise) */
-        V4 pin[2];
-        pin[0] = load_full(ms->data + 16 * (size_t)(lane + 64 * wave));
-        pin[1] = wave == 0 ? load_full(ms->data + 16 * (size_t)(lane + 64)) : V4{0, 0, 0, 0};
+        V4 pin[3]; /* elements 64 w + l, + 64, + 128 */
+#pragma unroll
+        for (int m = 0; m < 3; ++m)
+            pin[m] = load_full(ms->data + 16 * (size_t)(lane + 64 * wave + 64 * m));
         const ptls_hip_record_t rec = rq.rec;
         const uint32_t flags = __builtin_amdgcn_readfirstlane(rq.flags);
         const uint8_t *in = as_global(rq.in), *aad = as_global(rq.aad);
@@ -875,6 +941,7 @@ __global__ void __launch_bounds__(WORKER_WG)
         const int na1 = ((int)rec.aad_len + 15) >> 4, nc1 = ((int)rec.len + 15) >> 4;
         const int n1 = na1 + nc1 + 1;
         const bool mw = n1 >= MW_MIN_N && n1 <= MW_MAX_N;
+        const bool longrec = n1 > MW_MAX_N; /* both waves at stride 128 (sparse_record S = 128) */
         if (WORKER_STAMPS)
             st[2] = worker_stamp();
         /* WORKER_STAMPS builds (with STAMP_PHASES): the record's phase stamps (shader cycles) go to the end of the data area,
@@ -894,7 +961,29 @@ __global__ void __launch_bounds__(WORKER_WG)
                 v = load_full(in + rec.in_off + 16 * (size_t)(i - na1));
             return v;
         };
-        if (mw) {
+        if (longrec) {
+            V4 p2[2];
+            if (flags & WREQ_INLINE) {
+                p2[0] = pin[0];
+                p2[1] = pin[2];
+            } else {
+                p2[0] = elem_block(lane + 64 * wave);
+                p2[1] = elem_block(lane + 64 * wave + 128);
+            }
+            const uint32_t tab_w = wave == 0 ? tab : TAB1, ctab_w = wave == 0 ? CTAB0 : CTAB1;
+            if (open && a256)
+                sparse_record<14, true, true, true, 128>(lds, lane, lb_aes, tab_w, rec, 0, in, aad, out, result, slots, basis, supp,
+                                                         hp_slots, 1, mask, true, p2, nullptr, false, false, pa, ctab_w, wave, XSLOT);
+            else if (open)
+                sparse_record<10, true, true, true, 128>(lds, lane, lb_aes, tab_w, rec, 0, in, aad, out, result, slots, basis, supp,
+                                                         hp_slots, 1, mask, true, p2, nullptr, false, false, pa, ctab_w, wave, XSLOT);
+            else if (a256)
+                sparse_record<14, false, true, true, 128>(lds, lane, lb_aes, tab_w, rec, 0, in, aad, out, result, slots, basis, supp,
+                                                          hp_slots, 1, mask, true, p2, nullptr, false, false, pa, ctab_w, wave, XSLOT);
+            else
+                sparse_record<10, false, true, true, 128>(lds, lane, lb_aes, tab_w, rec, 0, in, aad, out, result, slots, basis, supp,
+                                                          hp_slots, 1, mask, true, p2, nullptr, false, false, pa, ctab_w, wave, XSLOT);
+        } else if (mw) {
             const V4 mine = (flags & WREQ_INLINE) ? pin[0] : elem_block(lane + 64 * wave);
             const uint32_t ctab_w = wave == 0 ? CTAB0 : CTAB1;
             if (open && a256)
@@ -933,7 +1022,7 @@ __global__ void __launch_bounds__(WORKER_WG)
         }
         /* the wave holding the tag (wave 1 of a two-wave record; wave 0 otherwise): every store of the call reaches system
          * scope before its completion word (wave 0 of a two-wave record released its own before mw_record's barrier) */
-        if (wave == (mw ? 1 : 0)) {
+        if (wave == (mw ? 1 : longrec ? ((n1 - 1) & 127) >> 6 : 0)) {
             if (WORKER_STAMPS) {
                 st[3] = worker_stamp();
                 const uint64_t t = __builtin_amdgcn_s_memtime();
