@@ -623,11 +623,12 @@ def main():
     clk_o = torch.zeros(4 * open_b.grid, dtype=torch.int64, device="cuda")
     seal_b.set_clock(clk_s)
     open_b.set_clock(clk_o)
-    ktimes, kclk = [], []
+    ktimes, kclk, kdet = [], [], []
     for _ in range(max(2, min(args.steps, 5))):
         step(ktimes)
         kclk.append((ptls_hip.clock_of(clk_s.cpu().numpy().view(np.uint64), seal_b.grid),
                      ptls_hip.clock_of(clk_o.cpu().numpy().view(np.uint64), open_b.grid)))
+        kdet.append(ptls_hip.clock_detail(clk_s.cpu().numpy().view(np.uint64), seal_b.grid))
     seal_b.set_clock(None)
     open_b.set_clock(None)
     seal_ms = float(np.median([a for a, _ in ktimes]))
@@ -676,6 +677,12 @@ def main():
                          "seal_ghz_min_max_over_workgroups": [round(min(c[0][1] for c in kclk), 3),
                                                               round(max(c[0][2] for c in kclk), 3)],
                          "seal_span_ms_100mhz": round(float(np.median([c[0][3] for c in kclk])), 3),
+                         # how the seal launches ended across workgroups: (last end - median end) / span, median of the
+                         # stamped launches, and the median launch's per-XCD clock and end time
+                         "seal_finish_spread": round(float(np.median([d["finish_spread"] for d in kdet])), 4),
+                         "seal_finish_spread_first_to_last": round(float(np.median([d["finish_spread_min_to_max"]
+                                                                                   for d in kdet])), 4),
+                         "seal_per_xcd": sorted(kdet, key=lambda d: d["span_ms"])[len(kdet) // 2]["per_xcd"],
                          "seal_mcycles_per_launch": round(seal_ghz * seal_ms, 2),
                          "cycles_note": "clock x kernel time = the launch's length in shader cycles: the work measure that does "
                                         "not move with the box's clock (MI355X_MICROARCH.md DVFS)",

@@ -89,6 +89,13 @@ __host__ __device__ constexpr uint32_t lds_bytes(int log2g)
 #define DEAL_MUTANT 0 /* TEST-ONLY broken builds (tools/build_mutants.sh, tests/test_gpu_dealing.py): 1 = the task a wave
                          drew past one chunk is dropped at the next chunk of the key run, 2 = cbase is not advanced */
 #endif
+#ifndef CHUNK_QUEUE
+#define CHUNK_QUEUE 1 /* workgroups take their chunks after the first from a device-wide queue (one returning atomic add per
+                         chunk) instead of the static grid stride blockIdx.x + k * gridDim.x */
+#endif
+/* the chunk sequence a workgroup's waves walk: a ring in LDS of {sequence number, chunk} entries */
+constexpr int QRING = 32;
+constexpr uint32_t Q_END = 0xffffffffu;
 
 struct V4 {
     uint32_t w0, w1, w2, w3;
@@ -1103,9 +1110,11 @@ __device__ __forceinline__ void clock_stamp(uint64_t *__restrict__ clk, int slot
     if (clk != nullptr && threadIdx.x == 0) {
         const uint64_t t = __builtin_amdgcn_s_memtime();
         const uint64_t r = __builtin_amdgcn_s_memrealtime();
+        /* the XCD this workgroup runs on (HW_REG_XCC_ID bits 3:0) rides in the top byte of the start's 100 MHz stamp */
+        const uint64_t xcc = slot == 0 ? (uint64_t)(__builtin_amdgcn_s_getreg((3 << 11) | 20) & 15u) << 56 : 0;
         __builtin_amdgcn_s_waitcnt(0xC07F); /* lgkmcnt(0): the counters are back before any LDS wait is counted */
         clk[4 * blockIdx.x + 2 * slot] = t;
-        clk[4 * blockIdx.x + 2 * slot + 1] = r;
+        clk[4 * blockIdx.x + 2 * slot + 1] = r | xcc;
     }
 }
 
@@ -1237,7 +1246,7 @@ __global__ void __launch_bounds__(WGT)
                         const uint8_t *in, const uint8_t *__restrict__ aad, uint8_t *out, uint64_t *__restrict__ result,
                         const KeySlot *__restrict__ slots, const uint32_t *__restrict__ basis, const uint32_t *__restrict__ t0,
                         const ptls_hip_supp_t *__restrict__ supp, const KeySlot *__restrict__ hp_slots, uint32_t hp_nslots,
-                        uint8_t *mask, uint64_t *__restrict__ clk)
+                        uint8_t *mask, uint64_t *__restrict__ clk, uint32_t *queue)
 {
     constexpr int LOG2G = G == 1 ? 0 : G == 2 ? 1 : G == 4 ? 2 : G == 8 ? 3 : G == 16 ? 4 : 5;
     static_assert(G >= 1 && G <= 32 && (G & (G - 1)) == 0, "lanes per record: 1, 2, 4, 8, 16 or 32");
@@ -1249,14 +1258,80 @@ __global__ void __launch_bounds__(WGT)
     constexpr bool SPLIT = SPLIT_TASKS != 0 && G >= 16 && DYN && SPLIT_PROBE == 0 && HYBRID == 0 && KEYSWITCH_PROBE == 0;
     constexpr uint32_t LDS_SPLIT = lds_bytes(LOG2G) + 16;                 /* partials: [slot][part] 16 B each */
     constexpr uint32_t LDS_SPLIT_CTR = LDS_SPLIT + SPLIT_SLOTS * 32;      /* arrival counters: [slot] */
-    constexpr uint32_t LDS_TOTAL = SPLIT ? LDS_SPLIT_CTR + SPLIT_SLOTS * 4 : lds_bytes(LOG2G) + (DYN ? 16 : 0);
-    static_assert(LDS_TOTAL <= 163840, "tables + task counter + split slots must fit the CU's 160 KiB");
+    constexpr uint32_t LDS_QBASE = ((SPLIT ? LDS_SPLIT_CTR + SPLIT_SLOTS * 4 : lds_bytes(LOG2G) + (DYN ? 16 : 0)) + 7u) & ~7u;
+    /* QUEUE: a workgroup takes its chunks from a device-wide counter (queue[0]), one at a time, each claimed by the first
+     * of its waves that needs it; the waves walk the same chunk sequence, so the claimed chunk is left in an LDS ring for
+     * the others.  A workgroup that starts late (a CU still held by another kernel) or runs at a lower clock (the CUs of
+     * one XCD do not all hold the same clock under load) simply takes fewer chunks.  queue[1] counts the workgroups that
+     * have drawn past the end; the last one resets both words for the next launch that gets this slot (engine.cpp
+     * queue_slot). */
+    constexpr bool QUEUE = CHUNK_QUEUE != 0 && DYN && KEYSWITCH_PROBE == 0 && SPLIT_PROBE == 0;
+    constexpr int NW = WGT / 64;
+    constexpr uint32_t LDS_QRING = LDS_QBASE;              /* uint64 [QRING]: position << 32 | chunk */
+    constexpr uint32_t LDS_QCLAIM = LDS_QRING + QRING * 8; /* positions claimed so far */
+    constexpr uint32_t LDS_QSEQ = LDS_QCLAIM + 4;          /* uint32 [NW]: positions each wave has entered */
+    constexpr uint32_t LDS_TOTAL = QUEUE ? LDS_QSEQ + NW * 4 : LDS_QBASE;
+    static_assert(LDS_TOTAL <= 163840, "tables + task counter + split slots + chunk ring must fit the CU's 160 KiB");
     __shared__ __attribute__((aligned(16))) uint8_t lds[LDS_TOTAL];
     uint32_t *const task_ctr = reinterpret_cast<uint32_t *>(lds + lds_bytes(LOG2G));
     constexpr int R = 64 / G; /* records per wave task */
 
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
+    const bool use_q = QUEUE && queue != nullptr;
+    if (use_q) {
+        for (int k = (int)threadIdx.x; k < QRING; k += WGT)
+            reinterpret_cast<uint64_t *>(lds + LDS_QRING)[k] = ~0ull;
+        if (threadIdx.x < NW)
+            reinterpret_cast<uint32_t *>(lds + LDS_QSEQ)[threadIdx.x] = 0;
+        if (threadIdx.x == 0)
+            *reinterpret_cast<uint32_t *>(lds + LDS_QCLAIM) = 0;
+        __syncthreads();
+    }
+    /* the chunk at the wave's next position k of the workgroup's sequence (wave-uniform; lane 0 works, the wave waits), or
+     * Q_END.  The wave's position lives in LDS (LDS_QSEQ), not in a register held across the record loop. */
+    auto next_chunk = [&]() -> uint32_t {
+        uint32_t c = 0;
+        if (lane == 0) {
+            uint32_t *const entered = reinterpret_cast<uint32_t *>(lds + LDS_QSEQ);
+            const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x) >> 6;
+            const uint32_t k = __hip_atomic_load(entered + wv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            /* published before the entry is read: a wave that has entered e positions still reads entry e - 1 */
+            __hip_atomic_store(entered + wv, k + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            uint64_t *const ent = reinterpret_cast<uint64_t *>(lds + LDS_QRING) + (k % QRING);
+            if (__hip_atomic_fetch_max(reinterpret_cast<uint32_t *>(lds + LDS_QCLAIM), k + 1, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_WORKGROUP) < k + 1) {
+                /* this wave claims position k.  Its ring entry last held position k - QRING, which a wave still reads while
+                 * it has entered at most k - QRING + 1 positions: wait for every wave to be past that (such a wave is
+                 * working on a task of an earlier chunk, and walks on without waiting for this entry) */
+                if (k >= (uint32_t)QRING)
+                    for (;;) {
+                        uint32_t lo = 0xffffffffu;
+                        for (int w = 0; w < NW; ++w)
+                            lo = min(lo, __hip_atomic_load(entered + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+                        if (lo > k + 1 - (uint32_t)QRING)
+                            break;
+                        __builtin_amdgcn_s_sleep(2);
+                    }
+                c = __hip_atomic_fetch_add(queue, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (c >= nchunks) {
+                    c = Q_END;
+                    if (__hip_atomic_fetch_add(queue + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1) {
+                        /* every workgroup has drawn past the end: no more adds to either word in this launch */
+                        __hip_atomic_store(queue, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        __hip_atomic_store(queue + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    }
+                }
+                __hip_atomic_store(ent, (uint64_t)k << 32 | c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            } else {
+                uint64_t v;
+                while (((v = __hip_atomic_load(ent, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) >> 32) != k)
+                    __builtin_amdgcn_s_sleep(2);
+                c = (uint32_t)v;
+            }
+        }
+        return __builtin_amdgcn_readfirstlane(c);
+    };
     const uint32_t lb_aes = (uint32_t)(lane & 31) * 4u | LDS_AES;
     const GhLane gl = gh_lane_init(lane);
     const int r = lane & (G - 1);
@@ -1270,7 +1345,7 @@ __global__ void __launch_bounds__(WGT)
     uint32_t g = 0, cbase = 0, sbase = 0;
     bool have_g = false;
 
-    for (uint32_t ci = blockIdx.x; ci < nchunks; ci += gridDim.x) {
+    for (uint32_t ci = use_q ? next_chunk() : blockIdx.x; ci < nchunks; ci = use_q ? next_chunk() : ci + gridDim.x) {
         const Chunk ch = chunks[ci];
         if ((KEYSWITCH_PROBE == 2 || KEYSWITCH_PROBE == 3) && cur_key != 0xffffffffu && ch.key != cur_key) {
             /* timing bound only: later key switches neither wait nor rebuild; with DYN (3) the workgroup's task counter
@@ -1305,7 +1380,6 @@ __global__ void __launch_bounds__(WGT)
          * (issue arbitration favours the older wave), so a fixed deal leaves the slowest wave on the critical
          * path.  Otherwise: snake order over the chunk's tasks, the waves that drew the longest tasks in one
          * pass draw the shortest ones in the next. */
-        constexpr int NW = WGT / 64;
         for (int pass = 0;; ++pass) {
             int t;
             if (DYN) {
@@ -1719,10 +1793,12 @@ static hipError_t launch_one(unsigned grid, hipStream_t s, const KernelArgs &a, 
 {
     if (aligned)
         hipLaunchKernelGGL((aesgcm_batch_kernel<G, R, O, true, W>), dim3(grid), dim3(W), 0, s, a.recs_ord, a.order, a.chunks,
-                           a.nchunks, a.in, a.aad, a.out, a.result, a.slots, a.basis, a.t0, a.supp, a.hp_slots, a.hp_nslots, a.mask, a.clk);
+                           a.nchunks, a.in, a.aad, a.out, a.result, a.slots, a.basis, a.t0, a.supp, a.hp_slots, a.hp_nslots, a.mask, a.clk,
+                           a.queue);
     else
         hipLaunchKernelGGL((aesgcm_batch_kernel<G, R, O, false, W>), dim3(grid), dim3(W), 0, s, a.recs_ord, a.order, a.chunks,
-                           a.nchunks, a.in, a.aad, a.out, a.result, a.slots, a.basis, a.t0, a.supp, a.hp_slots, a.hp_nslots, a.mask, a.clk);
+                           a.nchunks, a.in, a.aad, a.out, a.result, a.slots, a.basis, a.t0, a.supp, a.hp_slots, a.hp_nslots, a.mask, a.clk,
+                           a.queue);
     return hipGetLastError();
 }
 

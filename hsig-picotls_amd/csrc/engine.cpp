@@ -15,6 +15,7 @@
 #include <hip/hip_runtime_api.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
@@ -102,7 +103,17 @@ struct st_ptls_hip_engine_t {
     int device;
     int ncu;
     uint32_t *d_t0;
+    uint32_t *d_queue;                /* QUEUE_SLOTS x {next chunk, workgroups done}: the batch kernel's chunk queues */
+    std::atomic<uint32_t> queue_next; /* the slot the next batch launch takes */
 };
+
+/* the chunk-queue words of one batch-kernel launch (batch_kernel.h QUEUE): zero when handed out, and the launch leaves
+ * them zero (its last workgroup resets them), so slots are reused round robin without a memset; QUEUE_SLOTS launches
+ * would have to be in flight at once for two to share one */
+static uint32_t *queue_slot(ptls_hip_engine_t *e)
+{
+    return e->d_queue + 2 * (size_t)(e->queue_next.fetch_add(1, std::memory_order_relaxed) % QUEUE_SLOTS);
+}
 
 struct st_ptls_hip_keyset_t {
     ptls_hip_engine_t *eng;
@@ -201,8 +212,14 @@ extern "C" ptls_hip_engine_t *ptls_hip_engine_new(int device)
     e->ncu = prop.multiProcessorCount;
     uint32_t t0[256];
     make_t0(t0);
-    if (hipMalloc(&e->d_t0, sizeof(t0)) != hipSuccess || hipMemcpy(e->d_t0, t0, sizeof(t0), hipMemcpyHostToDevice) != hipSuccess) {
-        fail(PTLS_HIP_ENOMEM, "cannot allocate the AES table on device %d", device);
+    e->d_queue = nullptr;
+    e->queue_next = 0;
+    if (hipMalloc(&e->d_t0, sizeof(t0)) != hipSuccess || hipMemcpy(e->d_t0, t0, sizeof(t0), hipMemcpyHostToDevice) != hipSuccess ||
+        hipMalloc(&e->d_queue, 2 * sizeof(uint32_t) * QUEUE_SLOTS) != hipSuccess ||
+        hipMemset(e->d_queue, 0, 2 * sizeof(uint32_t) * QUEUE_SLOTS) != hipSuccess) {
+        fail(PTLS_HIP_ENOMEM, "cannot allocate the AES table / chunk queues on device %d", device);
+        (void)hipFree(e->d_t0);
+        (void)hipFree(e->d_queue);
         delete e;
         return nullptr;
     }
@@ -221,6 +238,7 @@ extern "C" void ptls_hip_engine_free(ptls_hip_engine_t *e)
         return;
     DeviceGuard g(e->device);
     (void)hipFree(e->d_t0);
+    (void)hipFree(e->d_queue);
     delete e;
 }
 
@@ -531,6 +549,48 @@ static void plan_splits(const ptls_hip_record_t *recs, const std::vector<uint32_
     }
 }
 
+/* Guided chunk sizes at the end of long key runs (batch_kernel.h QUEUE hands chunks out in plan order).  A workgroup's
+ * last chunk ends the launch for it, so the chunks dealt last should be small: a chunk that starts when `rem` wave tasks
+ * remain in the batch gets at most rem / (2 ncu) tasks (at least one), like guided self-scheduling.  Only chunks of key
+ * runs longer than one full chunk are cut (configs[1], [2], [4]): a short run's pieces would each rebuild the key's GHASH
+ * tables on another workgroup, and such batches already balance over many runs.  The records of a chunk stay in their
+ * length-sorted order, so each piece is a contiguous, sorted range. */
+static void guided_tail(std::vector<Chunk> &ch, uint32_t per_task, unsigned ncu)
+{
+    static const bool on = [] { /* PTLS_HIP_GUIDED=0 (environment): full-size chunks to the end (A/B measurements) */
+        const char *e = getenv("PTLS_HIP_GUIDED");
+        return e == nullptr || atoi(e) != 0;
+    }();
+    if (!on)
+        return;
+    size_t total = 0;
+    for (const Chunk &c : ch)
+        total += (c.count + per_task - 1) / per_task;
+    std::vector<Chunk> out;
+    out.reserve(ch.size() + 4 * (size_t)ncu);
+    size_t done = 0;
+    for (size_t k = 0; k < ch.size(); ++k) {
+        Chunk c = ch[k];
+        const bool long_run = (k > 0 && ch[k - 1].key == c.key) || (k + 1 < ch.size() && ch[k + 1].key == c.key);
+        size_t tasks = (c.count + per_task - 1) / per_task;
+        while (long_run && tasks > 1) {
+            const size_t want = std::max<size_t>(1, (total - done) / (2 * (size_t)ncu));
+            if (want >= tasks)
+                break;
+            Chunk piece = c;
+            piece.count = (uint32_t)(want * per_task);
+            out.push_back(piece);
+            c.first += piece.count;
+            c.count -= piece.count;
+            done += want;
+            tasks -= want;
+        }
+        done += tasks;
+        out.push_back(c);
+    }
+    ch.swap(out);
+}
+
 /* chunk = run of records with one key slot, sized to keep all waves of a workgroup busy for a few tasks
  * (at most 32 wave tasks), but small enough that a batch of fewer tasks still spreads over every CU (the
  * grid is one workgroup per chunk up to the CU count).  Inside a chunk the records are ordered by
@@ -602,6 +662,7 @@ static void build_chunks(const ptls_hip_record_t *recs, size_t n, int lanes, uns
         all_aligned = all_aligned && (c.flags & 1u);
         ch.push_back(c);
     }
+    guided_tail(ch, per_task, ncu ? ncu : 1);
     if (SPLIT_TASKS && lanes >= 16)
         plan_splits(recs, order, ch, lanes);
 }
@@ -797,6 +858,7 @@ static int run_batch(ptls_hip_batch_t *b, ptls_hip_keyset_t *ks, const void *in,
     if (b->d_clk != nullptr && b->clk_bytes < (size_t)grid * 32)
         return fail(PTLS_HIP_EINVAL, "seal/open: the clock-stamp buffer is smaller than 32 bytes x %u workgroups", grid);
     a.clk = b->d_clk;
+    a.queue = queue_slot(b->eng);
     const int rounds = ks->key_size == 16 ? 10 : 14;
     int e = launch_batch(b->lanes, rounds, open, b->wg, grid, stream, a, aligned);
     if (e != 0)
@@ -1343,6 +1405,7 @@ static int pipeline_run_mapped(ptls_hip_pipeline_t *p, ptls_hip_keyset_t *ks, co
         const bool base_aligned =
             ((reinterpret_cast<uintptr_t>(a.in) | reinterpret_cast<uintptr_t>(a.aad) | reinterpret_cast<uintptr_t>(a.out)) & 15) == 0;
         const unsigned grid = plan_grid(cnt, ch.size(), lanes, (unsigned)p->eng->ncu);
+        a.queue = queue_slot(p->eng);
         const int e = launch_batch(lanes, rounds, open, plan_wg(ch, lanes), grid, s.stream, a, aligned && base_aligned);
         if (e != 0)
             return fail(PTLS_HIP_ELAUNCH, "pipeline: kernel launch failed: %s", hipGetErrorString((hipError_t)e));
@@ -1578,6 +1641,7 @@ static int pipeline_run_copy(ptls_hip_pipeline_t *p, ptls_hip_keyset_t *ks, cons
             a.mask = s.d_mask;
         }
         const unsigned grid = plan_grid(cnt, ch.size(), lanes, (unsigned)p->eng->ncu);
+        a.queue = queue_slot(p->eng);
         const int e = launch_batch(lanes, rounds, open, plan_wg(ch, lanes), grid, s.stream, a, aligned);
         if (e != 0)
             return fail(PTLS_HIP_ELAUNCH, "pipeline: kernel launch failed: %s", hipGetErrorString((hipError_t)e));

@@ -129,7 +129,12 @@ struct KernelArgs {
     uint32_t done_seq;
     /* optional diagnostic clock stamps, 4 x uint64 per workgroup (ptls_hip_batch_set_clock); nullptr = none */
     uint64_t *clk;
+    /* batch kernel: this launch's chunk-queue words {next chunk - grid, workgroups done}, zero at launch and left zero by
+     * the kernel (engine.cpp queue_slot); nullptr = the static grid stride */
+    uint32_t *queue;
 };
+/* chunk-queue slots per engine: launches take them round robin, so two launches in flight never share one */
+constexpr uint32_t QUEUE_SLOTS = 4096;
 
 /* The plugin worker (sparse_kernel.hip plugin_worker_kernel, engine.cpp): a resident one-wave kernel that serves the
  * plugin's single-record calls from a mailbox in fine-grained pinned host memory instead of one kernel launch per call.

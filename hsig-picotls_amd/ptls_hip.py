@@ -361,12 +361,38 @@ def clock_of(stamps, grid):
     """the clock one launch ran at, from its stamps (Batch.set_clock; array of >= 4 * grid uint64): per workgroup
     delta(shader cycles) / delta(100 MHz ticks) x 100 MHz.  Returns (median GHz over workgroups, min, max, the launch's
     span in ms from the first start to the last end on the 100 MHz counter)"""
-    a = np.asarray(stamps, dtype=np.uint64).reshape(-1, 4)[:grid].astype(np.float64)
+    d = clock_detail(stamps, grid)
+    return d["ghz_median"], d["ghz_min"], d["ghz_max"], d["span_ms"]
+
+
+def clock_detail(stamps, grid):
+    """clock_of plus how the launch ended across workgroups: every workgroup's start and end on the
+    100 MHz counter and its XCD (HW_REG_XCC_ID, in the top byte of the start stamp).
+      finish_spread = (last end - median end) / span: the share of the launch that only its slowest workgroups ran;
+      per_xcd = median GHz and median end (ms after the first start) of the workgroups of each XCD"""
+    u = np.asarray(stamps, dtype=np.uint64).reshape(-1, 4)[:grid]
+    xcc = (u[:, 1] >> np.uint64(56)).astype(np.int64)
+    a = u.astype(np.float64)
+    a[:, 1] = (u[:, 1] & np.uint64((1 << 56) - 1)).astype(np.float64)
     dt, dr = a[:, 2] - a[:, 0], a[:, 3] - a[:, 1]
     ok = dr > 0
-    ghz = dt[ok] / dr[ok] * 0.1
-    span_ms = (a[:, 3].max() - a[:, 1].min()) / 1e5
-    return float(np.median(ghz)), float(ghz.min()), float(ghz.max()), float(span_ms)
+    ghz = np.where(ok, dt / np.where(ok, dr, 1) * 0.1, np.nan)
+    t0 = a[:, 1].min()
+    ends = (a[:, 3] - t0) / 1e5  # ms after the first start
+    starts = (a[:, 1] - t0) / 1e5
+    span_ms = float(ends.max())
+    med_end = float(np.median(ends))
+    per_xcd = {}
+    for x in sorted(set(xcc.tolist())):
+        m = xcc == x
+        per_xcd[int(x)] = {"workgroups": int(m.sum()), "ghz_median": round(float(np.nanmedian(ghz[m])), 3),
+                           "end_ms_median": round(float(np.median(ends[m])), 4), "end_ms_max": round(float(ends[m].max()), 4)}
+    g = ghz[ok]
+    return {"ghz_median": float(np.median(g)), "ghz_min": float(g.min()), "ghz_max": float(g.max()), "span_ms": span_ms,
+            "end_ms_median": med_end, "end_ms_min": float(ends.min()), "start_ms_max": float(starts.max()),
+            "finish_spread": (span_ms - med_end) / span_ms if span_ms > 0 else 0.0,
+            "finish_spread_min_to_max": (span_ms - float(ends.min())) / span_ms if span_ms > 0 else 0.0,
+            "per_xcd": per_xcd}
 
 
 def is_supported():

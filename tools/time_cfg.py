@@ -80,8 +80,11 @@ for lib in args.libs:
         torch.cuda.synchronize()
         sc = ptls_hip.clock_of(cs.cpu().numpy().view(np.uint64), sb.grid)
         oc = ptls_hip.clock_of(co.cpu().numpy().view(np.uint64), ob.grid)
+        sd = ptls_hip.clock_detail(cs.cpu().numpy().view(np.uint64), sb.grid)
+        xc = " ".join(f"x{x}:{v['ghz_median']:.2f}/{v['end_ms_median']:.2f}/{v['end_ms_max']:.2f}" for x, v in sd["per_xcd"].items())
         clk = (f"  clock seal {sc[0]:.3f} GHz (wg {sc[1]:.3f}-{sc[2]:.3f}, span {sc[3]:.3f} ms, event {ev[0].elapsed_time(ev[1]):.3f} ms)"
-               f" open {oc[0]:.3f} GHz")
+               f" open {oc[0]:.3f} GHz  finish spread {sd['finish_spread']:.4f} (first end {sd['end_ms_min']:.3f}, median "
+               f"{sd['end_ms_median']:.3f}, last start {sd['start_ms_max']:.3f} ms)  xcd ghz/end med/end max: {xc}")
         sb.set_clock(None); ob.set_clock(None)
     print(f"{os.path.basename(os.path.dirname(os.path.dirname(lib))) or '.'}/{os.path.basename(lib)} {args.config} lanes={sb.lanes} "
           f"wg={sb.workgroup}: seal {s:.3f} ms ({gib / s * 1e3:.1f} GiB/s)  open {o:.3f} ms ({gib / o * 1e3:.1f} GiB/s){clk}",
