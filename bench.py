@@ -180,6 +180,47 @@ def cpu_share():
     return aff[:n], len(aff), quota
 
 
+def gpu_local_cpus(dev, cpus):
+    """order `cpus` for a CPU baseline that stands beside GPU `dev`: physical cores (one hardware thread per core) of the
+    GPU's NUMA node first, then the other physical cores, then SMT siblings.  Returns (ordered cpus, NUMA node or None,
+    the node's cpus).  The node comes from the GPU's PCI device in sysfs (hipDeviceGetPCIBusId)."""
+    import ctypes
+    node, node_cpus = None, set()
+    try:
+        hip = ctypes.CDLL("libamdhip64.so")
+        buf = ctypes.create_string_buffer(64)
+        if hip.hipDeviceGetPCIBusId(buf, 64, dev) == 0:
+            with open(f"/sys/bus/pci/devices/{buf.value.decode().lower()}/numa_node") as f:
+                node = int(f.read())
+            if node >= 0:
+                with open(f"/sys/devices/system/node/node{node}/cpulist") as f:
+                    node_cpus = set(_cpulist(f.read()))
+            else:
+                node = None
+    except (OSError, ValueError):
+        node = None
+
+    def primary(c):  # the first hardware thread of its core
+        try:
+            with open(f"/sys/devices/system/cpu/cpu{c}/topology/thread_siblings_list") as f:
+                return min(_cpulist(f.read())) == c
+        except (OSError, ValueError):
+            return True
+    rank = {c: (0 if c in node_cpus else 1) + (0 if primary(c) else 2) for c in cpus}
+    return sorted(cpus, key=lambda c: (rank[c], c)), node, sorted(node_cpus)
+
+
+def _cpulist(text):
+    out = []
+    for part in text.strip().split(","):
+        if "-" in part:
+            a, b = part.split("-")
+            out.extend(range(int(a), int(b) + 1))
+        elif part:
+            out.append(int(part))
+    return out
+
+
 def _steady(run_rep, min_reps=5, min_s=3.0, max_s=20.0, tol=0.10):
     """repeat run_rep() (-> GiB/s of one rep) until the last min_reps agree within tol of their median, or max_s;
     "noisy" says the spread bar was not met (a shared host: the GPU box grants a CPU share of a larger machine)"""
@@ -194,12 +235,17 @@ def _steady(run_rep, min_reps=5, min_s=3.0, max_s=20.0, tol=0.10):
                         spread=round(spread, 4), reps=len(rates), reps_used=len(last), noisy=bool(spread > tol))
 
 
-def cpu_baseline(cfg_name, cfg):
-    """lib/fusion.c (oracle/_ref, built unmodified from the reference) on this host's cores: distinct record
-    buffers of the config's shape (about 1 GiB, larger than the CPU caches, like the GPU's HBM-resident batch),
-    the config's AAD form, one ptls_aead_context_t per pinned thread.  Each rep = one seal
-    pass + one open pass over the sample (repeated inside the rep to last >= 0.3 s); reps repeat until five
-    agree within 10 %.  Reported: median of those five, min / max, for 1 thread and for every CPU available."""
+def cpu_baseline(cfg_name, cfg, dev=0):
+    """The reference's CPU engines (oracle/_ref, built unmodified from lib/fusion.c) on this host's cores: distinct record
+    buffers of the config's shape (about 1 GiB, larger than the CPU caches, like the GPU's HBM-resident batch), the
+    config's AAD form, one ptls_aead_context_t per pinned thread.  Two engines, the same bytes:
+      fusion        ptls_fusion_aes{128,256}gcm (lib/fusion.c:400-844, 128-bit AES-NI / PCLMUL)
+      non_temporal  ptls_non_temporal_aes{128,256}gcm (lib/fusion.c:1258-2179: 256-bit VAES / VPCLMULQDQ encrypt when the
+                    CPU has them, ptls_fusion_can_aesni256; what ptls_send uses with fusion)
+    `value` is the faster of the two.  Threads go to physical cores of the GPU's NUMA node first (gpu_local_cpus), as many as
+    the host's CPU share grants.  Each rep = one seal pass + one open pass over the sample (repeated inside the rep to last
+    >= 0.3 s); reps repeat until five agree within 10 %.  Reported: median of those five, min / max, for 1 thread and for
+    every CPU available."""
     import ctypes
     from oracle_lib import Ref, ORACLE_SO
     L = cfg["L"] or 8224
@@ -219,28 +265,38 @@ def cpu_baseline(cfg_name, cfg):
     idx = np.arange(nrec, dtype=np.uint64)
     aad = build_aad(cfg, idx, np.full(nrec, L, dtype=np.uint64)).reshape(nrec, 16)[:, :aad_len].copy()
     key, iv = (b"\x11" * cfg["key_len"]), b"\x22" * 12
-    cpus, n_aff, quota = cpu_share()
+    share, n_aff, quota = cpu_share()
+    try:
+        aff = sorted(os.sched_getaffinity(0))
+    except AttributeError:
+        aff = share
+    ordered, node, node_cpus = gpu_local_cpus(dev, aff)
+    cpus = ordered[:len(share)]
     threads = len(cpus)
     ref = Ref()
+    ref.lib.ref_bench_algo.restype = ctypes.c_double
+    ref.lib.ref_bench_algo.argtypes = [ctypes.c_int] + list(ref.lib.ref_bench.argtypes)
     ct = np.zeros_like(data)
     pt = np.zeros_like(data)
 
-    def run(do_open, src, dst, nthreads, passes, aad_arr, alen):
+    def run(nt, do_open, src, dst, nthreads, passes, aad_arr, alen):
         arr = (ctypes.c_int * nthreads)(*cpus[:nthreads])
-        return ref.lib.ref_bench(cfg["key_len"] * 8, do_open, key, iv, src.ctypes.data, dst.ctypes.data, nrec, L, stride,
-                                 aad_arr.ctypes.data, alen, nthreads, arr, passes)
+        return ref.lib.ref_bench_algo(nt, cfg["key_len"] * 8, do_open, key, iv, src.ctypes.data, dst.ctypes.data, nrec, L, stride,
+                                      aad_arr.ctypes.data, alen, nthreads, arr, passes)
 
-    def measure(nthreads, aad_arr, alen):
-        run(0, data, ct, nthreads, 1, aad_arr, alen)  # warm-up, and valid ciphertext for open
-        t1 = run(0, data, ct, nthreads, 1, aad_arr, alen) + run(1, ct, pt, nthreads, 1, aad_arr, alen)
+    def measure(nt, nthreads, aad_arr, alen):
+        run(nt, 0, data, ct, nthreads, 1, aad_arr, alen)  # warm-up, and valid ciphertext for open
+        t1 = run(nt, 0, data, ct, nthreads, 1, aad_arr, alen) + run(nt, 1, ct, pt, nthreads, 1, aad_arr, alen)
         passes = max(1, int(np.ceil(0.3 / max(t1, 1e-6))))
-        st = _steady(lambda: 2 * passes * nrec * L / (run(0, data, ct, nthreads, passes, aad_arr, alen) +
-                                                      run(1, ct, pt, nthreads, passes, aad_arr, alen)) / GIB)
+        st = _steady(lambda: 2 * passes * nrec * L / (run(nt, 0, data, ct, nthreads, passes, aad_arr, alen) +
+                                                      run(nt, 1, ct, pt, nthreads, passes, aad_arr, alen)) / GIB)
         assert np.array_equal(pt[:, :L], data[:, :L]), "reference round trip failed"
         st["passes_per_rep"] = passes
         return st
 
-    out = {n: measure(n, aad, aad_len) for n in sorted({1, threads})}
+    engines = {"fusion": 0, "non_temporal": 1}
+    out = {name: {n: measure(nt, n, aad, aad_len) for n in sorted({1, threads})} for name, nt in engines.items()}
+    best_name = max(out, key=lambda k: out[k][threads]["median"])
     # BASELINE configs[0]'s shape: 4K x 16 KiB with t/ptlsbench.c's 32-byte AAD uint64_t h[4], h[0] = seq (:129-141)
     h = np.zeros((nrec, 4), dtype="<u8")
     h[:, 0] = np.arange(1, nrec + 1, dtype=np.uint64)
@@ -249,7 +305,7 @@ def cpu_baseline(cfg_name, cfg):
     if L == 16384:
         saved = nrec
         nrec = 4096
-        conf1 = {n: measure(n, h8, 32) for n in sorted({1, threads})}
+        conf1 = {n: measure(engines[best_name], n, h8, 32) for n in sorted({1, threads})}
         nrec = saved
     cpu_model = ""
     try:
@@ -257,20 +313,27 @@ def cpu_baseline(cfg_name, cfg):
             cpu_model = next((ln.split(":", 1)[1].strip() for ln in f if ln.startswith("model name")), "")
     except OSError:
         pass
-    best = out[threads]
-    res = dict(value=best["median"], unit="GiB/s seal+open", cores=threads, kind="reference",
+    best = out[best_name][threads]
+    on_node = sum(1 for c in cpus if c in set(node_cpus))
+    res = dict(value=best["median"], unit="GiB/s seal+open", cores=threads, kind="reference", engine=best_name,
                min=best["min"], max=best["max"], spread=best["spread"], reps=best["reps"], noisy=best["noisy"],
                spread_target=0.10,
-               single_core=out[1]["median"], single_core_min=out[1]["min"], single_core_spread=out[1]["spread"],
+               single_core=out[best_name][1]["median"], single_core_min=out[best_name][1]["min"],
+               single_core_spread=out[best_name][1]["spread"],
+               engines={name: dict(all_cores=o[threads]["median"], all_cores_spread=o[threads]["spread"],
+                                   single_core=o[1]["median"]) for name, o in out.items()},
+               cpus_used=cpus, gpu_numa_node=node, cpus_on_gpu_node=on_node,
                cpus_in_affinity=n_aff, cgroup_cpu_quota=quota,
                fusion_can_aesni256=bool(ref.lib.ref_fusion_can_aesni256()), cpu=cpu_model,
                sample=f"{nrec} x {L} B distinct records ({nrec * L / GIB:.2f} GiB, {cfg_name} shape, {aad_len} B AAD), "
-                      f"lib/fusion.c via ptls_aead_encrypt/decrypt, one context per pinned thread; median of 5 reps "
-                      f"within {best['spread'] * 100:.1f} %, {threads} threads"
+                      f"lib/fusion.c's {best_name} engine (the faster of ptls_fusion_aes*gcm and ptls_non_temporal_aes*gcm) "
+                      f"via ptls_aead_encrypt/decrypt, one context per thread pinned to a physical core "
+                      f"({on_node} of {threads} on the GPU's NUMA node {node}); median of 5 reps within "
+                      f"{best['spread'] * 100:.1f} %, {threads} threads"
                       + (f" (the host's cgroup grants {quota:g} CPUs of the {n_aff} in the affinity mask)" if quota else ""))
     if conf1 is not None:
         res["config1_ptlsbench_aad"] = dict(
-            sample="BASELINE configs[0]: 4096 x 16384 B, 32-B AAD h[4] with h[0] = seq (t/ptlsbench.c:129-141)",
+            sample=f"BASELINE configs[0]: 4096 x 16384 B, 32-B AAD h[4] with h[0] = seq (t/ptlsbench.c:129-141), {best_name}",
             single_core=conf1[1]["median"], all_cores=conf1[threads]["median"], all_cores_spread=conf1[threads]["spread"],
             cores=threads, unit="GiB/s seal+open")
     return res
@@ -733,7 +796,7 @@ def main():
     if rank == 0 and world == 1 and not args.no_plugin:
         result["plugin_ptlsbench"] = plugin_ptlsbench()
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        result["cpu_baseline"] = cpu_baseline(args.config, cfg)
+        result["cpu_baseline"] = cpu_baseline(args.config, cfg, dev)
     if rank == 0:
         print(json.dumps(result), flush=True)
     for o in (ks, eng):

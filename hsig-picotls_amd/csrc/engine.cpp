@@ -121,7 +121,31 @@ struct st_ptls_hip_keyset_t {
     KeySlot *d_slots;
     uint32_t *d_basis;
     std::vector<uint8_t> ivs; /* host mirror of every slot's static IV (do_get_iv) */
+    int64_t pool_id = -1;     /* >= 0: a plugin context's slot from the plugin pool (pool_keyset), not its own allocation */
+    /* the streams launches on this keyset went to, each with an event recorded after its last such launch: keyset_free
+     * waits for exactly that work */
+    std::mutex use_mu;
+    std::vector<std::pair<hipStream_t, hipEvent_t>> uses;
 };
+
+/* after a launch on `stream` that reads ks */
+static void keyset_note_use(ptls_hip_keyset_t *ks, void *stream)
+{
+    if (ks == nullptr || ks->pool_id >= 0)
+        return;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    std::lock_guard<std::mutex> lk(ks->use_mu);
+    for (auto &u : ks->uses)
+        if (u.first == s) {
+            (void)hipEventRecord(u.second, s);
+            return;
+        }
+    hipEvent_t ev = nullptr;
+    if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) == hipSuccess && hipEventRecord(ev, s) == hipSuccess)
+        ks->uses.emplace_back(s, ev);
+    else /* no event: keyset_free falls back to waiting for the device */
+        ks->uses.emplace_back(s, nullptr);
+}
 
 struct st_ptls_hip_batch_t {
     ptls_hip_engine_t *eng;
@@ -257,7 +281,6 @@ extern "C" int ptls_hip_engine_cu_count(ptls_hip_engine_t *e)
 /* ---------------------------------------------------------------------------------------------- */
 
 static const size_t BASIS_WORDS_PER_SLOT = (size_t)BASIS_VECS * 4;
-static void worker_quiesce(void); /* the plugin worker leaves before key material changes (below, plugin section) */
 
 extern "C" ptls_hip_keyset_t *ptls_hip_keyset_new(ptls_hip_engine_t *eng, size_t key_size, size_t nslots)
 {
@@ -282,15 +305,40 @@ extern "C" ptls_hip_keyset_t *ptls_hip_keyset_new(ptls_hip_engine_t *eng, size_t
     return ks;
 }
 
+static void pool_release(ptls_hip_keyset_t *ks); /* plugin section */
+
 extern "C" void ptls_hip_keyset_free(ptls_hip_keyset_t *ks)
 {
     if (ks == nullptr)
         return;
     DeviceGuard g(ks->eng->device);
+    if (ks->pool_id >= 0) { /* a plugin context's pooled slot: zeroed and retired, nothing waits */
+        pool_release(ks);
+        std::fill(ks->ivs.begin(), ks->ivs.end(), 0);
+        delete ks;
+        return;
+    }
+    /* the launches that read this keyset (keyset_note_use), not the whole device: a resident plugin worker or another
+     * thread's batches are not waited for */
+    bool device_wide = false;
+    for (auto &u : ks->uses) {
+        if (u.second == nullptr) {
+            device_wide = true;
+            continue;
+        }
+        (void)hipEventSynchronize(u.second);
+        (void)hipEventDestroy(u.second);
+    }
+    ks->uses.clear();
+    if (device_wide)
+        (void)hipDeviceSynchronize();
     /* zeroize key material before release (ptls_clear_memory in aesgcm_dispose_crypto, lib/fusion.c:1102-1107, :1042-1048) */
-    (void)hipMemset(ks->d_slots, 0, ks->nslots * sizeof(KeySlot));
-    (void)hipMemset(ks->d_basis, 0, ks->nslots * BASIS_WORDS_PER_SLOT * 4);
-    (void)hipDeviceSynchronize();
+    hipStream_t s = nullptr;
+    (void)hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
+    (void)hipMemsetAsync(ks->d_slots, 0, ks->nslots * sizeof(KeySlot), s);
+    (void)hipMemsetAsync(ks->d_basis, 0, ks->nslots * BASIS_WORDS_PER_SLOT * 4, s);
+    (void)hipStreamSynchronize(s);
+    (void)hipStreamDestroy(s);
     (void)hipFree(ks->d_slots);
     (void)hipFree(ks->d_basis);
     std::fill(ks->ivs.begin(), ks->ivs.end(), 0);
@@ -309,7 +357,6 @@ extern "C" int ptls_hip_keyset_set(ptls_hip_keyset_t *ks, size_t first, size_t c
         return fail(PTLS_HIP_EINVAL, "keyset_set: bad arguments");
     if (count == 0)
         return 0;
-    worker_quiesce();
     std::vector<uint8_t> zero_ivs;
     if (ivs == nullptr) { /* header-protection / ECB-only keys carry no IV */
         zero_ivs.assign(count * 12, 0);
@@ -351,7 +398,6 @@ static int keyset_from_secrets(ptls_hip_keyset_t *ks, size_t first, size_t count
         return fail(PTLS_HIP_EINVAL, "keyset_%s_secrets: bad arguments", update ? "update" : "set");
     if (count == 0)
         return 0;
-    worker_quiesce();
     DeviceGuard g(ks->eng->device);
     hipStream_t s = static_cast<hipStream_t>(stream);
     const size_t sbytes = count * hash_size, kbytes = count * ks->key_size, ibytes = count * 12;
@@ -407,7 +453,6 @@ extern "C" int ptls_hip_keyset_set_iv(ptls_hip_keyset_t *ks, size_t slot, const 
 {
     if (ks == nullptr || slot >= ks->nslots)
         return fail(PTLS_HIP_EINVAL, "keyset_set_iv: bad slot");
-    worker_quiesce();
     DeviceGuard g(ks->eng->device);
     std::memcpy(&ks->ivs[slot * 12], iv, 12);
     hipStream_t s = static_cast<hipStream_t>(stream);
@@ -863,6 +908,8 @@ static int run_batch(ptls_hip_batch_t *b, ptls_hip_keyset_t *ks, const void *in,
     int e = launch_batch(b->lanes, rounds, open, b->wg, grid, stream, a, aligned);
     if (e != 0)
         return fail(PTLS_HIP_ELAUNCH, "kernel launch failed: %s", hipGetErrorString((hipError_t)e));
+    keyset_note_use(ks, stream);
+    keyset_note_use(hp_ks, stream);
     return 0;
 }
 
@@ -896,6 +943,7 @@ extern "C" int ptls_hip_aesecb_batch(ptls_hip_engine_t *eng, ptls_hip_keyset_t *
                                 stream);
     if (e != 0)
         return fail(PTLS_HIP_ELAUNCH, "aesecb_batch: kernel launch failed: %s", hipGetErrorString((hipError_t)e));
+    keyset_note_use(hp_ks, stream);
     return 0;
 }
 
@@ -1273,20 +1321,16 @@ static void *mapped_span(const void *h, uint64_t need, bool *partial)
     void *d = mapped_ptr(h);
     if (d == nullptr || need <= 1)
         return d;
-    const uintptr_t hp = reinterpret_cast<uintptr_t>(h), dp = reinterpret_cast<uintptr_t>(d);
+    const uintptr_t dp = reinterpret_cast<uintptr_t>(d);
+    /* the allocation's range, queried and compared in the device address space: a span inside it is
+     * mapped; otherwise the mapping of the span's last byte decides (one registration covering both ends) */
     uintptr_t start = 0;
     size_t size = 0;
     if (hipPointerGetAttribute(&start, HIP_POINTER_ATTRIBUTE_RANGE_START_ADDR, reinterpret_cast<hipDeviceptr_t>(d)) == hipSuccess &&
         hipPointerGetAttribute(&size, HIP_POINTER_ATTRIBUTE_RANGE_SIZE, reinterpret_cast<hipDeviceptr_t>(d)) == hipSuccess &&
-        size != 0) {
-        const bool in_range = (start <= dp && dp + need <= start + size) || (start <= hp && hp + need <= start + size);
-        if (!in_range) {
-            *partial = true;
-            return nullptr;
-        }
-    } else {
-        (void)hipGetLastError();
-    }
+        size != 0 && start <= dp && dp + need <= start + size)
+        return d;
+    (void)hipGetLastError();
     void *d_last = mapped_ptr(static_cast<const uint8_t *>(h) + (need - 1));
     if (d_last == nullptr || reinterpret_cast<uintptr_t>(d_last) != dp + (need - 1)) {
         *partial = true;
@@ -1463,7 +1507,7 @@ static int pipeline_run(ptls_hip_pipeline_t *p, ptls_hip_keyset_t *ks, const ptl
         if (recs[i].key >= ks->nslots)
             return fail(PTLS_HIP_EINVAL, "pipeline: record %zu names key slot %u, the keyset has %zu", i, recs[i].key, ks->nslots);
     DeviceGuard g(p->eng->device);
-    if (n != 0) {
+    if (n != 0 && p->transport != PTLS_HIP_TRANSPORT_COPY) { /* the copy engines take any host buffer */
         /* the bytes the kernels would touch in each buffer: [base, base + need) */
         uint64_t need_in = 0, need_out = 0, need_aad = 0, need_mask = 0;
         for (size_t i = 0; i < n; ++i) {
@@ -1898,19 +1942,19 @@ static ptls_hip_engine_t *plugin_engine(void)
     return g_plugin_engine;
 }
 
-/* per-context state: one key slot plus pinned, device-mapped staging for one record.  A call copies the record in
- * on the CPU, launches, and copies the output out: the kernel reads and writes the staging over PCIe itself (no
- * copy-engine transfers, one launch + one stream synchronisation per call). */
+/* per-context state: one pooled key slot.  A call through the worker carries the record, the context's IV and the
+ * output in a mailbox (pinned, device-mapped: the kernel reads and writes it over PCIe itself, no copy engine); the
+ * context's own pinned staging exists only for records that do not fit a mailbox and for launched calls
+ * (PTLS_HIP_PLUGIN_WORKER=0), and is allocated on first use. */
 struct hip_aead_state {
     ptls_hip_engine_t *eng;
     ptls_hip_keyset_t *ks;
-    hipStream_t stream;
-    uint8_t *h_io, *d_io; /* pinned [in: cap][out: cap + 16][aad: aad_cap] and its device address */
+    uint8_t *h_io, *d_io; /* pinned [in: cap][out: cap + 16][aad: aad_cap] and its device address (lazy) */
     size_t cap, aad_cap;
-    uint8_t *h_stage, *d_stage; /* pinned 256 B: record, chunk, order, result, supp, mask (ST_*) and its device address */
+    uint8_t *h_stage, *d_stage; /* pooled 256-B pinned piece: result, supp, mask, completion word (ST_*) (lazy) */
     uint8_t iv[12];
-    bool iv_dirty;
-    uint32_t done_seq; /* completion word sequence of the last call (ST_DONE) */
+    bool iv_dirty;     /* launched calls: the slot's IV must be uploaded before the next launch */
+    uint32_t done_seq; /* completion word sequence of the last launched call (ST_DONE) */
 };
 
 struct hip_aead_context {
@@ -1962,21 +2006,35 @@ static void plugin_wait(hipStream_t stream, const uint8_t *word_p, uint32_t seq)
 static unsigned staging_flags(void);
 
 /* ---- the plugin worker (sparse_kernel.hip plugin_worker_kernel) ------------------------------------------------- *
- * A plugin call launches nothing while the worker is resident: it writes its request into the worker's mailbox (pinned,
- * fine-grained), then waits on its completion word as a launched call does.  Calls are serialized on the worker (one
- * request at a time; the mutex is held for the whole call).  The worker leaves after WORKER_IDLE_US without a request
- * or after WORKER_LIFE_US, and a call that finds it gone relaunches it (the launch a call without the worker pays each
- * time).  On by default; PTLS_HIP_PLUGIN_WORKER=0 (environment) makes every call launch its own kernel instead. */
+ * A plugin call launches nothing while the worker is resident: it writes its request into a mailbox (pinned,
+ * fine-grained), then waits on its completion word as a launched call does.  The worker is ONE dispatch of `n`
+ * workgroups, workgroup j serving mailbox j; a calling thread has a home mailbox (threads are spread over them round
+ * robin) and takes any free one when its home is busy, so calls from different threads run side by side on different
+ * CUs (lib/fusion.c contexts share no state either, :1135-1166).  The workgroups leave together after WORKER_IDLE_US
+ * without a request on any of them, after WORKER_LIFE_US in any case (the dispatch must not hold its hardware queue), or
+ * when asked; a call that finds its workgroup gone waits for the whole dispatch to drain and launches the next one.
+ * On by default; PTLS_HIP_PLUGIN_WORKER=0 (environment) makes every call launch its own kernel instead;
+ * PTLS_HIP_PLUGIN_WORKERS=n sets the number of mailboxes / workgroups (default 8, 1..64). */
 static const uint64_t WORKER_IDLE_US = 200, WORKER_LIFE_US = 2000;
+static const unsigned WORKER_MAX = 64;
+
+struct Mailbox {
+    std::mutex mu;         /* held for a whole call */
+    uint32_t seq = 0;      /* the last request number written */
+    uint32_t done_seq = 0; /* the last completion-word value asked for */
+};
 
 struct PluginWorker {
-    std::mutex mu;
+    std::mutex launch_mu; /* launching / draining the dispatch */
     ptls_hip_engine_t *eng = nullptr;
     hipStream_t stream = nullptr;
+    unsigned n = 0;
     WorkerSlot *h_mb = nullptr, *d_mb = nullptr;
-    uint32_t epoch = 0; /* of the last worker launched; h_mb->exited == epoch: it has left */
-    uint32_t seq = 0;
-    bool launched = false;
+    uint64_t *d_activity = nullptr;   /* the last time any workgroup served a request (100 MHz ticks) */
+    std::atomic<uint32_t> epoch{0};   /* of the last dispatch launched; h_mb[j].exited == epoch: workgroup j has left */
+    std::atomic<bool> launched{false};
+    std::atomic<unsigned> next_home{0};
+    Mailbox mbox[WORKER_MAX];
 };
 static PluginWorker g_worker;
 
@@ -1989,87 +2047,149 @@ static bool worker_enabled(void)
     return on;
 }
 
+static unsigned worker_count(void)
+{
+    static const unsigned n = [] {
+        const char *e = getenv("PTLS_HIP_PLUGIN_WORKERS");
+        const int v = e != nullptr ? atoi(e) : 8;
+        return (unsigned)std::max(1, std::min(v, (int)WORKER_MAX));
+    }();
+    return n;
+}
+
 static uint32_t load_acquire(const uint32_t *p)
 {
     return __atomic_load_n(p, __ATOMIC_ACQUIRE);
 }
 
-/* at process exit (atexit: before the HIP runtime's own teardown): ask a resident worker to leave and wait for it, with
- * host memory only, so no kernel is running when the process ends */
-static void worker_atexit(void)
+static void cpu_relax(void)
 {
-    PluginWorker &w = g_worker;
-    if (w.h_mb == nullptr || !w.launched)
-        return;
-    __atomic_store_n(&w.h_mb->quit, 1u, __ATOMIC_RELEASE);
-    const auto t0 = std::chrono::steady_clock::now();
-    while (load_acquire(&w.h_mb->exited) != w.epoch && std::chrono::steady_clock::now() - t0 < std::chrono::milliseconds(50))
-        std::this_thread::yield();
+#if defined(__x86_64__) || defined(__i386__)
+    __builtin_ia32_pause();
+#else
+    std::this_thread::yield();
+#endif
 }
 
-/* under w.mu: the worker's mailbox (fine-grained pinned host memory) and stream on the plugin engine's device */
-static WorkerSlot *worker_mailbox(PluginWorker &w)
+/* every workgroup of dispatch `epoch` has left (or none was launched) */
+static bool worker_drained(const PluginWorker &w, uint32_t epoch)
 {
-    if (w.h_mb == nullptr) {
-        void *d = nullptr;
-        WorkerSlot *h = nullptr;
-        if (hipStreamCreateWithFlags(&w.stream, hipStreamNonBlocking) != hipSuccess ||
-            hipHostMalloc(reinterpret_cast<void **>(&h), sizeof(WorkerSlot), hipHostMallocCoherent) != hipSuccess ||
-            hipHostGetDevicePointer(&d, h, 0) != hipSuccess) {
-            g_err = "plugin worker mailbox";
-            plugin_die("worker_mailbox");
-        }
-        std::memset(h, 0, sizeof(WorkerSlot));
-        w.h_mb = h;
-        w.d_mb = static_cast<WorkerSlot *>(d);
-        atexit(worker_atexit);
-    }
-    return w.h_mb;
-}
-
-/* under w.mu: a resident worker */
-static bool worker_launch(PluginWorker &w)
-{
-    worker_mailbox(w);
-    /* a worker that has not left yet keeps serving: a second one on the same mailbox would serve its requests twice */
-    if (w.launched && load_acquire(&w.h_mb->exited) != w.epoch)
-        return true;
-    ++w.epoch;
-    const int e = launch_plugin_worker(w.d_mb, w.epoch, w.eng->d_t0, WORKER_IDLE_US * 100, WORKER_LIFE_US * 100, w.stream);
-    if (e != 0) {
-        g_err = hipGetErrorString((hipError_t)e);
-        return false;
-    }
-    w.launched = true;
+    if (!w.launched.load(std::memory_order_acquire) || w.epoch.load(std::memory_order_acquire) != epoch)
+        return true; /* a later dispatch exists: this one was drained before it was launched (worker_ensure) */
+    for (unsigned j = 0; j < w.n; ++j)
+        if (load_acquire(&w.h_mb[j].exited) != epoch)
+            return false;
     return true;
 }
 
-/* Before key material changes (a keyset's keys, IVs or secrets): a resident worker leaves, so the next call's fresh
- * dispatch reads the new slot contents (a dispatch starts with its caches invalidated; a running wave's scalar cache
- * could still hold a slot's old round keys or IV, and a freed slot's address may come back for a new context). */
-static void worker_quiesce(void)
+/* at process exit (atexit: before the HIP runtime's own teardown): ask the resident workgroups to leave and wait for them,
+ * with host memory only, so no kernel is running when the process ends */
+static void worker_atexit(void)
 {
     PluginWorker &w = g_worker;
-    std::lock_guard<std::mutex> lk(w.mu);
-    if (w.h_mb == nullptr || !w.launched || load_acquire(&w.h_mb->exited) == w.epoch)
+    if (w.h_mb == nullptr || !w.launched.load())
         return;
-    __atomic_store_n(&w.h_mb->quit, 1u, __ATOMIC_RELEASE);
+    for (unsigned j = 0; j < w.n; ++j)
+        __atomic_store_n(&w.h_mb[j].quit, 1u, __ATOMIC_RELEASE);
     const auto t0 = std::chrono::steady_clock::now();
-    while (load_acquire(&w.h_mb->exited) != w.epoch) {
-        if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(2)) {
-            g_err = "the plugin worker did not leave";
-            plugin_die("worker_quiesce");
-        }
+    while (!worker_drained(w, w.epoch.load()) && std::chrono::steady_clock::now() - t0 < std::chrono::milliseconds(50))
         std::this_thread::yield();
+}
+
+/* under launch_mu: the mailboxes (fine-grained pinned host memory), the activity word and the stream, on the plugin
+ * engine's device */
+static void worker_init(PluginWorker &w, ptls_hip_engine_t *eng)
+{
+    if (w.h_mb != nullptr)
+        return;
+    DeviceGuard g(eng->device);
+    const unsigned n = worker_count();
+    void *d = nullptr;
+    WorkerSlot *h = nullptr;
+    if (hipStreamCreateWithFlags(&w.stream, hipStreamNonBlocking) != hipSuccess ||
+        hipHostMalloc(reinterpret_cast<void **>(&h), n * sizeof(WorkerSlot), hipHostMallocCoherent) != hipSuccess ||
+        hipHostGetDevicePointer(&d, h, 0) != hipSuccess || hipMalloc(&w.d_activity, sizeof(uint64_t)) != hipSuccess ||
+        hipMemset(w.d_activity, 0, sizeof(uint64_t)) != hipSuccess) {
+        g_err = "plugin worker mailboxes";
+        plugin_die("worker_init");
     }
-    __atomic_store_n(&w.h_mb->quit, 0u, __ATOMIC_RELEASE);
+    std::memset(h, 0, n * sizeof(WorkerSlot));
+    w.eng = eng;
+    w.n = n;
+    w.d_mb = static_cast<WorkerSlot *>(d);
+    w.h_mb = h; /* published last: readers test h_mb first */
+    atexit(worker_atexit);
+}
+
+/* With mailbox j's lock held: a dispatch whose workgroup j has not left.  A dispatch in which it has left is drained first
+ * (every workgroup asked to quit; one with a request pending serves it before it leaves), so two dispatches never serve
+ * one mailbox, and a request written before the next launch is served by it (a workgroup starts from `served`). */
+static void worker_ensure(PluginWorker &w, unsigned j)
+{
+    if (w.launched.load(std::memory_order_acquire) && load_acquire(&w.h_mb[j].exited) != w.epoch.load(std::memory_order_acquire))
+        return;
+    std::lock_guard<std::mutex> lk(w.launch_mu);
+    DeviceGuard g(w.eng->device);
+    const uint32_t ep = w.epoch.load();
+    if (w.launched.load() && load_acquire(&w.h_mb[j].exited) == ep) {
+        if (!worker_drained(w, ep)) {
+            for (unsigned k = 0; k < w.n; ++k)
+                __atomic_store_n(&w.h_mb[k].quit, 1u, __ATOMIC_RELEASE);
+            const auto t0 = std::chrono::steady_clock::now();
+            while (!worker_drained(w, ep)) {
+                if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(2)) {
+                    /* a workgroup that never started (the CUs were held by other kernels): the dispatch ends once it has
+                     * run; a device fault is reported here */
+                    plugin_check(hipStreamSynchronize(w.stream), "plugin worker drain");
+                    if (!worker_drained(w, ep)) {
+                        g_err = "the plugin worker dispatch completed with a workgroup that did not report its exit";
+                        plugin_die("worker_ensure");
+                    }
+                    break;
+                }
+                std::this_thread::yield();
+            }
+            for (unsigned k = 0; k < w.n; ++k)
+                __atomic_store_n(&w.h_mb[k].quit, 0u, __ATOMIC_RELEASE);
+        }
+        w.launched.store(false, std::memory_order_release);
+    }
+    if (!w.launched.load()) {
+        const uint32_t next = ep + 1;
+        const int e = launch_plugin_worker(w.d_mb, w.n, next, w.eng->d_t0, WORKER_IDLE_US * 100, WORKER_LIFE_US * 100, w.d_activity,
+                                           w.stream);
+        if (e != 0) {
+            g_err = hipGetErrorString((hipError_t)e);
+            plugin_die("plugin worker launch");
+        }
+        w.epoch.store(next, std::memory_order_release);
+        w.launched.store(true, std::memory_order_release);
+    }
+}
+
+/* a mailbox for this call, locked: the thread's home mailbox, or the first free one, or (all busy) the home one */
+static unsigned worker_acquire(PluginWorker &w)
+{
+    static thread_local int home = -1;
+    if (home < 0)
+        home = (int)(w.next_home.fetch_add(1) % w.n);
+    if (w.mbox[home].mu.try_lock())
+        return (unsigned)home;
+    for (unsigned k = 1; k < w.n; ++k) {
+        const unsigned j = ((unsigned)home + k) % w.n;
+        if (w.mbox[j].mu.try_lock())
+            return j;
+    }
+    w.mbox[home].mu.lock();
+    return (unsigned)home;
 }
 
 #ifndef WORKER_STAMPS
 #define WORKER_STAMPS 0 /* diagnostic build only (Makefile `diag`) */
 #endif
 #if WORKER_STAMPS
-/* diagnostic build: the worker's phase stamps of the last request and the host's wall-clock microseconds of that call */
+/* diagnostic build: the worker's phase stamps of the last request on mailbox 0 and the host's wall-clock microseconds of
+ * that call */
 static double g_worker_call_us = 0;
 extern "C" int ptls_hip_diag_worker_stamps(uint64_t *out, double *call_us)
 {
@@ -2086,18 +2206,19 @@ extern "C" int ptls_hip_diag_worker_stamps(uint64_t *out, double *call_us)
 }
 #endif
 
-/* one request through the worker; returns once the call's completion word shows done_seq (the same protocol as a
- * launched call, plugin_wait).  A worker that left without serving the request is relaunched (its successor serves it:
- * seq != served); without any progress for 2 s the process aborts like a launched call's device fault would. */
-static void worker_call(const WorkerReq &req, const uint8_t *word_p)
+/* one request through mailbox j (its lock held); returns once the call's completion word shows done_seq (the same
+ * protocol as a launched call, plugin_wait).  A workgroup that left without serving the request is replaced (the next
+ * dispatch serves it: seq != served).  A dispatch that has not started after 2 s (every CU held by other kernels) is
+ * waited for with a stream synchronize, which also reports a device fault. */
+static void worker_call(unsigned j, const WorkerReq &req, const uint8_t *word_p)
 {
     PluginWorker &w = g_worker;
-    DeviceGuard g(w.eng->device);
-    if (!worker_launch(w))
-        plugin_die("plugin worker launch");
-    w.h_mb->req = req;
+    Mailbox &m = w.mbox[j];
+    WorkerSlot *mb = &w.h_mb[j];
+    worker_ensure(w, j);
+    mb->req = req;
     const auto tc = std::chrono::steady_clock::now();
-    __atomic_store_n(&w.h_mb->seq, ++w.seq, __ATOMIC_RELEASE);
+    __atomic_store_n(&mb->seq, ++m.seq, __ATOMIC_RELEASE);
     const uint32_t *word = reinterpret_cast<const uint32_t *>(word_p);
     auto t0 = std::chrono::steady_clock::now();
     for (uint32_t spin = 1;; ++spin) {
@@ -2108,38 +2229,226 @@ static void worker_call(const WorkerReq &req, const uint8_t *word_p)
             (void)tc;
             return;
         }
-#if defined(__x86_64__) || defined(__i386__)
-        __builtin_ia32_pause();
-#else
-        std::this_thread::yield();
-#endif
-        if ((spin & 1023) == 0) {
-            if (load_acquire(&w.h_mb->exited) == w.epoch && load_acquire(&w.h_mb->served) != w.seq) {
-                if (!worker_launch(w)) /* it left (idle / lifetime) just before the request: its successor serves it */
-                    plugin_die("plugin worker relaunch");
+        cpu_relax();
+        if ((spin & 1023) != 0)
+            continue;
+        if (load_acquire(&mb->exited) == w.epoch.load(std::memory_order_acquire) && load_acquire(&mb->served) != m.seq) {
+            worker_ensure(w, j); /* it left (idle / lifetime / drained) just before the request: the next dispatch serves it */
+            t0 = std::chrono::steady_clock::now();
+        } else if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(2)) {
+            DeviceGuard g(w.eng->device);
+            plugin_check(hipStreamSynchronize(w.stream), "plugin worker");
+            if (load_acquire(word) == req.done_seq)
+                return;
+            if (load_acquire(&mb->served) != m.seq) { /* the dispatch ended without it: the next one serves it */
+                worker_ensure(w, j);
                 t0 = std::chrono::steady_clock::now();
-            } else if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(2)) {
-                plugin_check(hipStreamSynchronize(w.stream), "plugin worker");
-                static char msg[256];
-                snprintf(msg, sizeof(msg),
-                         "the plugin worker stopped serving (request %u, served %u, seen %u, epoch %u, started %u, exited %u, "
-                         "word %u of %u)",
-                         w.seq, load_acquire(&w.h_mb->served), load_acquire(&w.h_mb->seen), w.epoch,
-                         load_acquire(&w.h_mb->started), load_acquire(&w.h_mb->exited), load_acquire(word), req.done_seq);
-                g_err = msg;
-                plugin_die("worker_call");
+                continue;
             }
+            static char msg[256];
+            snprintf(msg, sizeof(msg),
+                     "the plugin worker served request %u without its completion word (mailbox %u, seen %u, epoch %u, started %u, "
+                     "exited %u, word %u of %u)",
+                     m.seq, j, load_acquire(&mb->seen), w.epoch.load(), load_acquire(&mb->started), load_acquire(&mb->exited),
+                     load_acquire(word), req.done_seq);
+            g_err = msg;
+            plugin_die("worker_call");
         }
     }
 }
+
+/* ---- pooled plugin resources --------------------------------------------------------------------------------------- *
+ * A picotls application creates and frees AEAD contexts per connection (lib/picotls.c:6458-6479: a malloc and a key
+ * expansion for fusion, lib/fusion.c:984-1010).  Device memory, pinned host memory and streams are expensive to create
+ * and to free (hipFree / hipHostFree synchronize), so the plugin keeps them in pools:
+ *   - key slots: blocks of POOL_BLOCK KeySlot + GHASH basis, each with pinned staging for the raw keys the key-setup kernel
+ *     reads in place.  A freed slot is zeroed on the device (async) and retired; it is handed out again only after that
+ *     zeroing has completed AND every worker dispatch that could have read it has left, so the resident worker never
+ *     sees a slot it has cached change under it (its key loads are vector loads after a system-scope acquire, and each
+ *     dispatch starts with its caches invalidated).
+ *   - streams for key setup and launched calls: taken for one operation, then returned.
+ *   - 256-byte pieces of pinned staging (completion words, ECB blocks, launched calls' results). */
+static const uint32_t POOL_BLOCK = 64;
+
+struct SlotPool {
+    std::mutex mu;
+    struct Block {
+        KeySlot *d_slots;
+        uint32_t *d_basis;
+        uint8_t *h_keys, *d_keys; /* pinned: [POOL_BLOCK][64] = key (32) | iv (12) */
+    };
+    std::vector<Block> blocks[2]; /* [AES-128, AES-256] */
+    std::vector<uint32_t> free_ids[2];
+    struct Retired {
+        uint32_t id;
+        uint32_t epoch; /* worker dispatch resident when it was freed (0: none) */
+        hipEvent_t zeroed;
+    };
+    std::vector<Retired> retired[2];
+    std::vector<hipStream_t> streams;
+    std::vector<hipEvent_t> events;
+    std::vector<uint8_t *> pieces; /* free 256-B pinned pieces */
+};
+static SlotPool g_pool;
+
+static hipStream_t pool_stream(void)
+{
+    {
+        std::lock_guard<std::mutex> lk(g_pool.mu);
+        if (!g_pool.streams.empty()) {
+            hipStream_t s = g_pool.streams.back();
+            g_pool.streams.pop_back();
+            return s;
+        }
+    }
+    hipStream_t s = nullptr;
+    plugin_check(hipStreamCreateWithFlags(&s, hipStreamNonBlocking), "hipStreamCreate(pool)");
+    return s;
+}
+
+static void pool_stream_put(hipStream_t s)
+{
+    std::lock_guard<std::mutex> lk(g_pool.mu);
+    g_pool.streams.push_back(s);
+}
+
+/* a 256-B piece of pinned, device-mapped staging (zeroed) */
+static uint8_t *pool_piece(void)
+{
+    std::lock_guard<std::mutex> lk(g_pool.mu);
+    if (g_pool.pieces.empty()) {
+        uint8_t *h = nullptr;
+        plugin_check(hipHostMalloc(reinterpret_cast<void **>(&h), 64 * 256, staging_flags()), "hipHostMalloc(pieces)");
+        std::memset(h, 0, 64 * 256);
+        for (int k = 63; k >= 0; --k)
+            g_pool.pieces.push_back(h + 256 * k);
+    }
+    uint8_t *p = g_pool.pieces.back();
+    g_pool.pieces.pop_back();
+    return p;
+}
+
+static void pool_piece_put(uint8_t *p)
+{
+    std::memset(p, 0, 256);
+    std::lock_guard<std::mutex> lk(g_pool.mu);
+    g_pool.pieces.push_back(p);
+}
+
+/* under g_pool.mu: a slot id of key size class c (0: AES-128, 1: AES-256), recycling retired slots that are safe to reuse */
+static uint32_t pool_take_locked(ptls_hip_engine_t *eng, int c)
+{
+    auto &ret = g_pool.retired[c];
+    for (size_t k = 0; k < ret.size();) {
+        if (hipEventQuery(ret[k].zeroed) == hipSuccess && (ret[k].epoch == 0 || worker_drained(g_worker, ret[k].epoch))) {
+            g_pool.free_ids[c].push_back(ret[k].id);
+            g_pool.events.push_back(ret[k].zeroed);
+            ret[k] = ret.back();
+            ret.pop_back();
+        } else {
+            ++k;
+        }
+    }
+    if (g_pool.free_ids[c].empty()) {
+        SlotPool::Block b{};
+        void *dk = nullptr;
+        if (hipMalloc(&b.d_slots, POOL_BLOCK * sizeof(KeySlot)) != hipSuccess ||
+            hipMalloc(&b.d_basis, POOL_BLOCK * BASIS_WORDS_PER_SLOT * 4) != hipSuccess ||
+            hipHostMalloc(reinterpret_cast<void **>(&b.h_keys), POOL_BLOCK * 64, staging_flags()) != hipSuccess ||
+            hipHostGetDevicePointer(&dk, b.h_keys, 0) != hipSuccess) {
+            g_err = "cannot allocate plugin key slots";
+            return UINT32_MAX;
+        }
+        (void)eng;
+        b.d_keys = static_cast<uint8_t *>(dk);
+        std::memset(b.h_keys, 0, POOL_BLOCK * 64);
+        const uint32_t base = (uint32_t)g_pool.blocks[c].size() * POOL_BLOCK;
+        g_pool.blocks[c].push_back(b);
+        for (uint32_t k = POOL_BLOCK; k-- > 0;)
+            g_pool.free_ids[c].push_back(base + k);
+    }
+    const uint32_t id = g_pool.free_ids[c].back();
+    g_pool.free_ids[c].pop_back();
+    return id;
+}
+
+/* a one-slot keyset on a pooled slot, keyed (key setup on the device from the slot's pinned key staging) */
+static ptls_hip_keyset_t *pool_keyset(ptls_hip_engine_t *eng, size_t key_size, const void *key, const void *iv)
+{
+    const int c = key_size == 32 ? 1 : 0;
+    uint32_t id;
+    SlotPool::Block b;
+    {
+        std::lock_guard<std::mutex> lk(g_pool.mu);
+        id = pool_take_locked(eng, c);
+        if (id == UINT32_MAX)
+            return nullptr;
+        b = g_pool.blocks[c][id / POOL_BLOCK];
+    }
+    const uint32_t k = id % POOL_BLOCK;
+    auto *ks = new st_ptls_hip_keyset_t();
+    ks->eng = eng;
+    ks->key_size = key_size;
+    ks->nslots = 1;
+    ks->d_slots = b.d_slots + k;
+    ks->d_basis = b.d_basis + (size_t)k * BASIS_WORDS_PER_SLOT;
+    ks->pool_id = (int64_t)id;
+    ks->ivs.assign(12, 0);
+    uint8_t *hk = b.h_keys + 64 * k;
+    std::memcpy(hk, key, key_size);
+    if (iv != nullptr)
+        std::memcpy(hk + 32, iv, 12);
+    hipStream_t s = pool_stream();
+    const int e = launch_keysetup(b.d_slots, b.d_basis, b.d_keys + 64 * k, b.d_keys + 64 * k + 32, k, 1, (int)key_size, eng->d_t0, s);
+    const hipError_t se = e == 0 ? hipStreamSynchronize(s) : (hipError_t)e;
+    pool_stream_put(s);
+    std::memset(hk, 0, 64); /* the raw key does not stay in host memory */
+    if (se != hipSuccess) {
+        g_err = hipGetErrorString(se);
+        ptls_hip_keyset_free(ks);
+        return nullptr;
+    }
+    if (iv != nullptr)
+        std::memcpy(ks->ivs.data(), iv, 12);
+    return ks;
+}
+
+/* ptls_hip_keyset_free of a pooled keyset: zero the slot (async) and retire it; nothing waits */
+static void pool_release(ptls_hip_keyset_t *ks)
+{
+    const int c = ks->key_size == 32 ? 1 : 0;
+    const uint32_t id = (uint32_t)ks->pool_id;
+    DeviceGuard g(ks->eng->device);
+    hipStream_t s = pool_stream();
+    hipEvent_t ev = nullptr;
+    {
+        std::lock_guard<std::mutex> lk(g_pool.mu);
+        if (!g_pool.events.empty()) {
+            ev = g_pool.events.back();
+            g_pool.events.pop_back();
+        }
+    }
+    if (ev == nullptr)
+        plugin_check(hipEventCreateWithFlags(&ev, hipEventDisableTiming), "hipEventCreate(pool)");
+    /* zeroize key material before release (ptls_clear_memory in aesgcm_dispose_crypto, lib/fusion.c:1102-1107) */
+    plugin_check(hipMemsetAsync(ks->d_slots, 0, sizeof(KeySlot), s), "hipMemsetAsync(slot)");
+    plugin_check(hipMemsetAsync(ks->d_basis, 0, BASIS_WORDS_PER_SLOT * 4, s), "hipMemsetAsync(basis)");
+    plugin_check(hipEventRecord(ev, s), "hipEventRecord(pool)");
+    pool_stream_put(s);
+    const PluginWorker &w = g_worker;
+    const uint32_t ep = w.h_mb != nullptr && w.launched.load() ? w.epoch.load() : 0;
+    std::lock_guard<std::mutex> lk(g_pool.mu);
+    g_pool.retired[c].push_back(SlotPool::Retired{id, ep, ev});
+}
+
+static uint8_t *mapped_or_die(uint8_t *h);
 
 /* ---- CTR cipher for header protection (replaces lib/fusion.c:1050-1100) ---------------------------- */
 
 struct hip_ctr_state {
     ptls_hip_engine_t *eng;
-    ptls_hip_keyset_t *ks;
-    hipStream_t stream;
-    uint8_t *h_stage; /* pinned [ptls_hip_supp_t @0][input block @32][mask @48] */
+    ptls_hip_keyset_t *ks; /* pooled slot */
+    uint8_t *h_stage; /* pooled 256-B pinned piece: [output block @48][completion word @64] */
     uint8_t *d_stage; /* its device address: the kernel reads and writes it in place */
     uint8_t bits[16];
     bool ready;
@@ -2170,14 +2479,16 @@ static void ecb_block(hip_ctr_state *st, const void *src, uint8_t dst[16])
     /* one launch per block even with the plugin worker resident: measured faster than a worker request (9.5 against
      * 11.2 us per block): the kernel's block travels in its arguments, while a request adds a PCIe read of the mailbox */
     /* the block goes in the kernel arguments; the result comes back through the pinned staging (@48) */
+    hipStream_t stream = pool_stream();
     const int e = launch_aesecb_one(st->ks->key_size == 16 ? 10 : 14, static_cast<const uint8_t *>(src), st->ks->d_slots,
                                     st->eng->d_t0, st->d_stage + 48, reinterpret_cast<uint32_t *>(st->d_stage + ECB_DONE),
-                                    ++st->done_seq, st->stream);
+                                    ++st->done_seq, stream);
     if (e != 0) {
         g_err = hipGetErrorString((hipError_t)e);
         plugin_die("ecb launch");
     }
-    plugin_wait(st->stream, st->h_stage + ECB_DONE, st->done_seq);
+    plugin_wait(stream, st->h_stage + ECB_DONE, st->done_seq);
+    pool_stream_put(stream);
     std::memcpy(dst, st->h_stage + 48, 16);
     std::memset(st->h_stage + 48, 0, 16);
 }
@@ -2212,39 +2523,22 @@ static hip_ctr_state *ecb_state_new(const void *key, size_t key_size)
     DeviceGuard g(eng->device);
     auto *st = new hip_ctr_state();
     st->eng = eng;
-    if (hipStreamCreateWithFlags(&st->stream, hipStreamNonBlocking) != hipSuccess) {
+    st->ks = pool_keyset(eng, key_size, key, nullptr);
+    if (st->ks == nullptr) {
         delete st;
         return nullptr;
     }
-    st->ks = ptls_hip_keyset_new(eng, key_size, 1);
-    void *d_stage = nullptr;
-    const bool ok = st->ks != nullptr && hipHostMalloc(&st->h_stage, 128, staging_flags()) == hipSuccess &&
-                    hipHostGetDevicePointer(&d_stage, st->h_stage, 0) == hipSuccess &&
-                    ptls_hip_keyset_set(st->ks, 0, 1, key, nullptr, st->stream) == 0;
-    st->d_stage = static_cast<uint8_t *>(d_stage);
-    if (!ok) {
-        if (st->ks != nullptr)
-            ptls_hip_keyset_free(st->ks);
-        (void)hipHostFree(st->h_stage);
-        (void)hipStreamDestroy(st->stream);
-        delete st;
-        return nullptr;
-    }
-    std::memset(st->h_stage, 0, 128); /* the completion word starts below the first block's sequence number */
+    st->h_stage = pool_piece(); /* zeroed: the completion word starts below the first block's sequence number */
+    st->d_stage = mapped_or_die(st->h_stage);
     return st;
 }
 
 static void ecb_state_free(hip_ctr_state *st)
 {
-    {
-        DeviceGuard g(st->eng->device);
-        (void)hipStreamSynchronize(st->stream); /* the last block's kernel may still be retiring (plugin_wait) */
-        ptls_hip_keyset_free(st->ks);
-        if (st->h_stage != nullptr)
-            std::memset(st->h_stage, 0, 128);
-        (void)hipHostFree(st->h_stage);
-        (void)hipStreamDestroy(st->stream);
-    }
+    /* the last block's kernel wrote its completion word after its last access to the staging or the slot (plugin_wait):
+     * nothing waits here */
+    ptls_hip_keyset_free(st->ks);
+    pool_piece_put(st->h_stage);
     std::memset(st->bits, 0, sizeof(st->bits));
     delete st;
 }
@@ -2344,7 +2638,7 @@ static uint8_t *mapped_or_die(uint8_t *h)
 
 static void state_reserve(hip_aead_state *st, size_t len, size_t aadlen)
 {
-    if (len <= st->cap && aadlen <= st->aad_cap)
+    if (st->h_io != nullptr && len <= st->cap && aadlen <= st->aad_cap)
         return;
     size_t cap = std::max(st->cap, (size_t)2048), aad_cap = std::max(st->aad_cap, (size_t)256);
     while (cap < len)
@@ -2353,8 +2647,7 @@ static void state_reserve(hip_aead_state *st, size_t len, size_t aadlen)
         aad_cap *= 2;
     cap = (cap + 15) & ~(size_t)15;
     aad_cap = (aad_cap + 15) & ~(size_t)15;
-    /* a previous call's kernel may still be retiring after its completion word (plugin_wait) */
-    plugin_check(hipStreamSynchronize(st->stream), "hipStreamSynchronize");
+    /* a previous call's kernel wrote its completion word after its last access to this staging (plugin_wait) */
     if (st->h_io != nullptr) {
         std::memset(st->h_io, 0, st->cap + st->cap + 16 + st->aad_cap);
         plugin_check(hipHostFree(st->h_io), "hipHostFree");
@@ -2385,52 +2678,119 @@ struct PluginSupp {
     uint8_t *output; /* host: supp->output */
 };
 
-/* pinned / device staging layout of one plugin call (256 B): result @128, supp descriptor @160, header-protection
+/* pinned / device staging layout of a launched plugin call (256 B): result @128, supp descriptor @160, header-protection
  * mask @192, completion word @224 (the record descriptor travels in the kernel arguments) */
 static const size_t ST_RESULT = 128, ST_SUPP = 160, ST_MASK = 192, ST_DONE = 224;
 
+/* the record's input (with a detached tag: ptls_fusion_aesgcm_decrypt, lib/fusion.c:660-661) and AAD into pinned memory
+ * the kernel reads */
+static void stage_record(uint8_t *dst_in, uint8_t *dst_aad, const void *input, size_t len, size_t in_len, const void *tag,
+                         const void *aad, size_t aadlen)
+{
+    if (tag != nullptr) {
+        if (len != 0)
+            std::memcpy(dst_in, input, len);
+        std::memcpy(dst_in + len, tag, 16);
+    } else if (in_len != 0) {
+        std::memcpy(dst_in, input, in_len);
+    }
+    if (aadlen != 0)
+        std::memcpy(dst_aad, aad, aadlen);
+}
 
-/* run one record: in/out/aad are the caller's (unpinned) host buffers.  The sparse kernel (one wave per record,
- * its own 8 KiB H^64 table, none for records of <= 64 GHASH elements) serves a single record without building
- * a workgroup-wide 64 KiB table. */
+/* run one record: in/out/aad are the caller's (unpinned) host buffers.  The sparse kernel's single-record path (one wave
+ * per record, its own 8 KiB H^64 table, none for records of <= 64 GHASH elements; two waves for longer ones) serves it
+ * without building a workgroup-wide 64 KiB table; through the worker, no launch at all. */
 static uint64_t plugin_run(hip_aead_state *st, bool open, void *output, const void *input, size_t len, uint64_t seq,
                            const void *aad, size_t aadlen, const PluginSupp *ps = nullptr, const void *tag = nullptr)
 {
     DeviceGuard g(st->eng->device);
-    const size_t in_len = open ? len + 16 : len;
-    state_reserve(st, in_len, aadlen);
-    /* through the worker, a record that fits goes inline into the mailbox instead of the context's staging */
+    const size_t in_len = open ? len + 16 : len, out_len = open ? len : len + 16;
     const size_t aad_pad = (aadlen + 15) & ~(size_t)15;
-    const bool use_worker = worker_enabled() && !STAMP_PHASES;
-    const bool inline_rec = use_worker && aad_pad + in_len <= (size_t)WORKER_DATA;
-    if (st->iv_dirty) {
-        if (ptls_hip_keyset_set_iv(st->ks, 0, st->iv, st->stream) != 0)
-            plugin_die("set_iv");
-        st->iv_dirty = false;
-    }
-    uint8_t *h_in = st->h_io, *h_out = st->h_io + st->cap, *h_aad = st->h_io + st->cap + st->cap + 16;
-    uint8_t *d_in = st->d_io, *d_out = st->d_io + st->cap, *d_aad = st->d_io + st->cap + st->cap + 16;
     ptls_hip_record_t rec{};
     rec.seq = seq;
     rec.len = (uint32_t)len;
     rec.aad_len = (uint32_t)aadlen;
     const ptls_hip_supp_t sp{ps != nullptr ? ps->sample_off : 0, 0, 0, PTLS_HIP_SUPP_ENABLE};
-    std::memcpy(st->h_stage + ST_SUPP, &sp, sizeof(sp));
-    /* the record's input (with a detached tag: ptls_fusion_aesgcm_decrypt, lib/fusion.c:660-661) and AAD into pinned
-     * memory the kernel reads */
-    auto stage = [&](uint8_t *dst_in, uint8_t *dst_aad) {
-        if (tag != nullptr) {
-            if (len != 0)
-                std::memcpy(dst_in, input, len);
-            std::memcpy(dst_in + len, tag, 16);
-        } else if (in_len != 0) {
-            std::memcpy(dst_in, input, in_len);
+    uint64_t result = len;
+    if (worker_enabled() && !STAMP_PHASES) {
+        PluginWorker &w = g_worker;
+        if (w.h_mb == nullptr) {
+            std::lock_guard<std::mutex> lk(w.launch_mu);
+            worker_init(w, st->eng);
         }
-        if (aadlen != 0)
-            std::memcpy(dst_aad, aad, aadlen);
-    };
-    if (!inline_rec)
-        stage(h_in, h_aad);
+        /* the record, its output, result, mask and completion word live in the mailbox when they fit (a TLS record always
+         * does: 16 KiB + 256 B); a longer one uses the context's staging */
+        const bool inline_rec = aad_pad + in_len <= (size_t)WORKER_DATA && out_len <= (size_t)WORKER_DATA;
+        if (!inline_rec) {
+            state_reserve(st, in_len, aadlen);
+            stage_record(st->h_io, st->h_io + st->cap + st->cap + 16, input, len, in_len, tag, aad, aadlen);
+        }
+        const unsigned j = worker_acquire(w);
+        WorkerSlot *h = &w.h_mb[j], *d = &w.d_mb[j];
+        WorkerReq rq{};
+        rq.rec = rec;
+        if (inline_rec) {
+            stage_record(h->data + aad_pad, h->data, input, len, in_len, tag, aad, aadlen);
+            rq.rec.aad_off = 0;
+            rq.rec.in_off = aad_pad;
+            rq.in = rq.aad = d->data;
+            rq.out = d->out;
+        } else {
+            rq.in = st->d_io;
+            rq.aad = st->d_io + st->cap + st->cap + 16;
+            rq.out = st->d_io + st->cap;
+        }
+        rq.result = reinterpret_cast<uint64_t *>(d->aux + WAUX_RESULT);
+        rq.slots = st->ks->d_slots;
+        rq.basis = st->ks->d_basis;
+        if (ps != nullptr) {
+            std::memcpy(h->aux + WAUX_SUPP, &sp, sizeof(sp));
+            rq.supp = reinterpret_cast<const ptls_hip_supp_t *>(d->aux + WAUX_SUPP);
+            rq.hp_slots = ps->hp_slots;
+            rq.mask = d->aux + WAUX_MASK;
+        }
+        rq.done = reinterpret_cast<uint32_t *>(d->aux + WAUX_DONE);
+        rq.done_seq = ++w.mbox[j].done_seq;
+        /* the context's IV travels with the request: IV changes never touch device memory the worker may have cached */
+        std::memcpy(rq.iv, st->iv, 12);
+        rq.flags = (open ? WREQ_OPEN : 0u) | (st->ks->key_size == 32 ? WREQ_AES256 : 0u) | WREQ_IV | (inline_rec ? WREQ_INLINE : 0u);
+        worker_call(j, rq, h->aux + WAUX_DONE);
+        const uint8_t *h_out = inline_rec ? h->out : st->h_io + st->cap;
+        if (open)
+            std::memcpy(&result, h->aux + WAUX_RESULT, 8);
+        if (out_len != 0)
+            std::memcpy(output, h_out, out_len);
+        if (ps != nullptr)
+            std::memcpy(ps->output, h->aux + WAUX_MASK, 16);
+        /* the record's bytes do not stay in the mailbox or the staging */
+        if (inline_rec) {
+            std::memset(h->data, 0, aad_pad + in_len);
+            std::memset(h->out, 0, out_len);
+        } else {
+            std::memset(st->h_io, 0, in_len);
+            std::memset(st->h_io + st->cap, 0, out_len);
+        }
+        std::memset(h->aux + WAUX_MASK, 0, 16);
+        w.mbox[j].mu.unlock();
+        return result;
+    }
+    /* one launch per call (PTLS_HIP_PLUGIN_WORKER=0) */
+    state_reserve(st, in_len, aadlen);
+    if (st->h_stage == nullptr) {
+        st->h_stage = pool_piece();
+        st->d_stage = mapped_or_die(st->h_stage);
+    }
+    hipStream_t stream = pool_stream();
+    if (st->iv_dirty) {
+        if (ptls_hip_keyset_set_iv(st->ks, 0, st->iv, stream) != 0)
+            plugin_die("set_iv");
+        st->iv_dirty = false;
+    }
+    uint8_t *h_in = st->h_io, *h_out = st->h_io + st->cap, *h_aad = st->h_io + st->cap + st->cap + 16;
+    uint8_t *d_in = st->d_io, *d_out = st->d_io + st->cap, *d_aad = st->d_io + st->cap + st->cap + 16;
+    std::memcpy(st->h_stage + ST_SUPP, &sp, sizeof(sp));
+    stage_record(h_in, h_aad, input, len, in_len, tag, aad, aadlen);
     KernelArgs a{};
     a.one = rec; /* by value in the kernel arguments (recs_ord stays null): the kernel's first dependent host read is
                     the record's own bytes */
@@ -2449,61 +2809,27 @@ static uint64_t plugin_run(hip_aead_state *st, bool open, void *output, const vo
     }
     a.done = reinterpret_cast<uint32_t *>(st->d_stage + ST_DONE);
     a.done_seq = ++st->done_seq;
-    if (use_worker) {
-        WorkerReq rq{};
-        rq.rec = rec;
-        rq.in = a.in;
-        rq.aad = a.aad;
-        rq.out = a.out;
-        rq.result = a.result;
-        rq.slots = a.slots;
-        rq.basis = a.basis;
-        rq.supp = a.supp;
-        rq.hp_slots = a.hp_slots;
-        rq.mask = a.mask;
-        rq.done = a.done;
-        rq.done_seq = a.done_seq;
-        rq.flags = (open ? WREQ_OPEN : 0u) | (st->ks->key_size == 32 ? WREQ_AES256 : 0u);
-        std::lock_guard<std::mutex> lk(g_worker.mu);
-        g_worker.eng = st->eng;
-        if (inline_rec) {
-            WorkerSlot *mb = worker_mailbox(g_worker);
-            stage(mb->data + aad_pad, mb->data);
-            rq.rec.aad_off = 0;
-            rq.rec.in_off = aad_pad;
-            rq.in = rq.aad = g_worker.d_mb->data;
-            rq.flags |= WREQ_INLINE;
-        }
-        worker_call(rq, st->h_stage + ST_DONE);
-        if (inline_rec) /* the record's bytes do not stay in the mailbox */
-            std::memset(g_worker.h_mb->data, 0, aad_pad + in_len);
-    } else {
 #if STAMP_PHASES
-        if (g_diag_stamps == nullptr)
-            plugin_check(hipMalloc(&g_diag_stamps, 16 * sizeof(uint64_t)), "hipMalloc(stamps)");
-        a.clk = g_diag_stamps;
+    if (g_diag_stamps == nullptr)
+        plugin_check(hipMalloc(&g_diag_stamps, 16 * sizeof(uint64_t)), "hipMalloc(stamps)");
+    a.clk = g_diag_stamps;
 #endif
-        const int e = launch_batch(SPARSE_LANES, st->ks->key_size == 16 ? 10 : 14, open, 0, 1, st->stream, a, true);
-        if (e != 0) {
-            g_err = hipGetErrorString((hipError_t)e);
-            plugin_die("launch");
-        }
-        plugin_wait(st->stream, st->h_stage + ST_DONE, a.done_seq);
+    const int e = launch_batch(SPARSE_LANES, st->ks->key_size == 16 ? 10 : 14, open, 0, 1, stream, a, true);
+    if (e != 0) {
+        g_err = hipGetErrorString((hipError_t)e);
+        plugin_die("launch");
     }
-    uint64_t result = len;
-    if (open) {
-        if (len != 0)
-            std::memcpy(output, h_out, len);
+    plugin_wait(stream, st->h_stage + ST_DONE, a.done_seq);
+    pool_stream_put(stream);
+    if (open)
         std::memcpy(&result, st->h_stage + ST_RESULT, 8);
-    } else {
-        std::memcpy(output, h_out, len + 16);
-    }
+    if (out_len != 0)
+        std::memcpy(output, h_out, out_len);
     if (ps != nullptr)
         std::memcpy(ps->output, st->h_stage + ST_MASK, 16);
     /* the record's bytes do not stay in the staging */
-    if (!inline_rec)
-        std::memset(h_in, 0, in_len);
-    std::memset(h_out, 0, open ? len : len + 16);
+    std::memset(h_in, 0, in_len);
+    std::memset(h_out, 0, out_len);
     return result;
 }
 
@@ -2511,17 +2837,15 @@ static void state_free(hip_aead_state *st)
 {
     {
         DeviceGuard g(st->eng->device);
-        (void)hipStreamSynchronize(st->stream); /* the last call's kernel may still be retiring (plugin_wait) */
+        /* the last call's kernel (or worker request) wrote its completion word after its last access to the staging and
+         * the slot: nothing waits here */
         ptls_hip_keyset_free(st->ks);
         if (st->h_io != nullptr) {
             std::memset(st->h_io, 0, st->cap + st->cap + 16 + st->aad_cap);
             (void)hipHostFree(st->h_io);
         }
-        if (st->h_stage != nullptr) {
-            std::memset(st->h_stage, 0, 256);
-            (void)hipHostFree(st->h_stage);
-        }
-        (void)hipStreamDestroy(st->stream);
+        if (st->h_stage != nullptr)
+            pool_piece_put(st->h_stage);
     }
     std::memset(st->iv, 0, sizeof(st->iv));
     delete st;
@@ -2635,25 +2959,11 @@ static hip_aead_state *state_new(const void *key, const void *iv, size_t key_siz
     DeviceGuard g(eng->device);
     auto *st = new hip_aead_state();
     st->eng = eng;
-    if (hipStreamCreateWithFlags(&st->stream, hipStreamNonBlocking) != hipSuccess) {
+    st->ks = pool_keyset(eng, key_size, key, iv);
+    if (st->ks == nullptr) {
         delete st;
         return nullptr;
     }
-    st->ks = ptls_hip_keyset_new(eng, key_size, 1);
-    void *d_stage = nullptr;
-    bool ok = st->ks != nullptr && hipHostMalloc(&st->h_stage, 256, staging_flags()) == hipSuccess &&
-              hipHostGetDevicePointer(&d_stage, st->h_stage, 0) == hipSuccess &&
-              ptls_hip_keyset_set(st->ks, 0, 1, key, iv, st->stream) == 0;
-    if (!ok) {
-        if (st->ks != nullptr)
-            ptls_hip_keyset_free(st->ks);
-        (void)hipHostFree(st->h_stage);
-        (void)hipStreamDestroy(st->stream);
-        delete st;
-        return nullptr;
-    }
-    st->d_stage = static_cast<uint8_t *>(d_stage);
-    std::memset(st->h_stage, 0, 256); /* the completion word starts below the first call's sequence number */
     std::memcpy(st->iv, iv, 12);
     st->iv_dirty = false;
     return st;
@@ -2841,7 +3151,9 @@ extern "C" ptls_hip_aesgcm_context_t *ptls_hip_aesgcm_set_capacity(ptls_hip_aesg
 {
     /* capacity = AAD + payload, as fusion's (lib/fusion.c:1017-1040); the staging also grows on demand */
     DeviceGuard g(ctx->st->eng->device);
-    state_reserve(ctx->st, capacity + 16, 0);
+    /* through the worker, records up to a mailbox's size need no staging of their own */
+    if (!worker_enabled() || capacity + 16 > (size_t)WORKER_DATA)
+        state_reserve(ctx->st, capacity + 16, 0);
     return ctx;
 }
 

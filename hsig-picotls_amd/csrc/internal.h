@@ -136,11 +136,13 @@ struct KernelArgs {
 /* chunk-queue slots per engine: launches take them round robin, so two launches in flight never share one */
 constexpr uint32_t QUEUE_SLOTS = 4096;
 
-/* The plugin worker (sparse_kernel.hip plugin_worker_kernel, engine.cpp): a resident one-wave kernel that serves the
- * plugin's single-record calls from a mailbox in fine-grained pinned host memory instead of one kernel launch per call.
- * The host writes the request, then (release) seq; the wave serves it, stores the call's completion word (as a launched
- * call's kernel does), then `served`. */
-enum : uint32_t { WREQ_OPEN = 1, WREQ_AES256 = 2, WREQ_INLINE = 8 };
+/* The plugin worker (sparse_kernel.hip plugin_worker_kernel, engine.cpp): a resident kernel whose workgroups each serve
+ * the plugin's single-record calls from their own mailbox in fine-grained pinned host memory instead of one kernel launch
+ * per call.  The host writes the request, then (release) seq; the workgroup serves it, stores the call's completion word
+ * (as a launched call's kernel does), then `served`. */
+enum : uint32_t { WREQ_OPEN = 1, WREQ_AES256 = 2, WREQ_INLINE = 8, WREQ_IV = 16 };
+/* WREQ_IV: the nonce's static IV is the request's iv[] (the context's current IV), not the key slot's: an IV change
+ * (ptls_aead_set_iv / xor_iv) stays on the host. */
 /* WREQ_INLINE: the record sits in the mailbox's data area (AAD padded to 16 bytes, then the input: element i of the GHASH
  * input at data + 16 i), read in the same PCIe round trip as the request.  Records that do not fit stay in the caller's
  * pinned staging. */
@@ -158,7 +160,8 @@ struct WorkerReq {
     uint32_t *done;           /* the call's completion word */
     uint32_t done_seq;
     uint32_t flags;           /* WREQ_* */
-    uint32_t pad[14];
+    uint32_t iv[3];           /* WREQ_IV: the static IV (raw bytes as little-endian words, KeySlot::iv's layout) */
+    uint32_t pad[11];
 };
 static_assert(sizeof(WorkerReq) == 192, "WorkerReq: 192 bytes");
 struct WorkerSlot {
@@ -173,12 +176,17 @@ struct WorkerSlot {
     uint64_t stamps[13]; /* worker -> host: WORKER_STAMPS builds' phase stamps of the last request (100 MHz counter) */
     WorkerReq req;
     uint8_t data[WORKER_DATA]; /* WREQ_INLINE records */
+    uint8_t out[WORKER_DATA];  /* the output of a request whose record fits (ciphertext + tag, or plaintext) */
+    uint8_t aux[256];          /* the request's result @0 (8 B), header-protection descriptor @32 (ptls_hip_supp_t) and mask
+                                  @64 (16 B), completion word @128 */
 };
-static_assert(sizeof(WorkerSlot) == 448 + WORKER_DATA, "WorkerSlot: seq / quit, served / exited, request on separate 128-B lines");
+static_assert(sizeof(WorkerSlot) == 448 + 2 * WORKER_DATA + 256, "WorkerSlot: seq / quit, served / exited, request on separate 128-B lines");
+constexpr uint32_t WAUX_RESULT = 0, WAUX_SUPP = 32, WAUX_MASK = 64, WAUX_DONE = 128;
 static_assert(__builtin_offsetof(WorkerSlot, quit) == 4, "the worker polls {seq, quit} as one 8-byte word");
 
 /* host-side launchers, defined next to the kernels (aesgcm_kernels.hip, batch_g*.hip) */
-int launch_plugin_worker(WorkerSlot *mb, uint32_t epoch, const uint32_t *t0, uint64_t idle_ticks, uint64_t life_ticks, void *stream);
+int launch_plugin_worker(WorkerSlot *mb, unsigned nmb, uint32_t epoch, const uint32_t *t0, uint64_t idle_ticks, uint64_t life_ticks,
+                         uint64_t *activity, void *stream);
 int launch_batch_g1(int rounds, bool open, int wg, unsigned grid, void *stream, const KernelArgs &a, bool aligned);
 int launch_batch_g2(int rounds, bool open, int wg, unsigned grid, void *stream, const KernelArgs &a, bool aligned);
 int launch_batch_g4(int rounds, bool open, int wg, unsigned grid, void *stream, const KernelArgs &a, bool aligned);

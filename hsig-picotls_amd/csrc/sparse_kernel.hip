@@ -237,7 +237,7 @@ __device__ __forceinline__ void sparse_record(uint8_t *lds, int lane, uint32_t l
                                               const uint32_t *__restrict__ basis, const ptls_hip_supp_t *__restrict__ supp,
                                               const KeySlot *__restrict__ hp_slots, uint32_t hp_nslots, uint8_t *mask, bool prefetch,
                                               const V4 (&pre)[2], uint64_t *__restrict__ clk, bool stamps, bool bstamps, PhaseAcc &pa,
-                                              uint32_t ctab, int vw = 0, uint32_t xslot = 0)
+                                              uint32_t ctab, int vw = 0, uint32_t xslot = 0, uint4 ivo = uint4{0, 0, 0, 0})
 {
     /* S = 64: one wave per record (lane l: elements l + 64 m, Horner with H^64).  S = 128 (a single long record on two
      * waves, vw = this wave's index 0 / 1): the two waves act as one 128-lane wave, virtual lane vl = 64 vw + l takes
@@ -267,9 +267,11 @@ __device__ __forceinline__ void sparse_record(uint8_t *lds, int lane, uint32_t l
     const uint8_t *in_p = in + rec.in_off;
     uint8_t *out_p = out + rec.out_off;
     const uint8_t *aad_p = aad + rec.aad_off;
-    const uint32_t n0 = __builtin_amdgcn_readfirstlane(slot->iv[0]),
-                   n1 = __builtin_amdgcn_readfirstlane(slot->iv[1] ^ bswap32((uint32_t)(rec.seq >> 32))),
-                   n2 = __builtin_amdgcn_readfirstlane(slot->iv[2] ^ bswap32((uint32_t)rec.seq));
+    /* ivo.w != 0: the static IV travels in the request (the plugin worker: an IV change never writes device memory) */
+    const bool ov = __builtin_amdgcn_readfirstlane(ivo.w) != 0;
+    const uint32_t n0 = __builtin_amdgcn_readfirstlane(ov ? ivo.x : slot->iv[0]),
+                   n1 = __builtin_amdgcn_readfirstlane((ov ? ivo.y : slot->iv[1]) ^ bswap32((uint32_t)(rec.seq >> 32))),
+                   n2 = __builtin_amdgcn_readfirstlane((ov ? ivo.z : slot->iv[2]) ^ bswap32((uint32_t)rec.seq));
     const int iters = (N + S - 1) >> LOG2S;
     const bool horner = SPARSE_ABLATE != 3 && iters > 1; /* N <= S: one element per lane, no Horner step */
     V4 b[4];
@@ -547,7 +549,8 @@ __device__ __forceinline__ void mw_record(uint8_t *lds, int wave, int lane, uint
                                           const ptls_hip_record_t &rec, const uint8_t *in, const uint8_t *__restrict__ aad,
                                           uint8_t *out, uint64_t *__restrict__ result, const KeySlot *__restrict__ slots,
                                           const uint32_t *__restrict__ basis, const ptls_hip_supp_t *__restrict__ supp,
-                                          const KeySlot *__restrict__ hp_slots, uint32_t hp_nslots, uint8_t *mask, V4 pre)
+                                          const KeySlot *__restrict__ hp_slots, uint32_t hp_nslots, uint8_t *mask, V4 pre,
+                                          uint4 ivo = uint4{0, 0, 0, 0})
 {
     const uint32_t key = __builtin_amdgcn_readfirstlane(rec.key);
     const KeySlot *__restrict__ slot = slots + key;
@@ -566,9 +569,10 @@ __device__ __forceinline__ void mw_record(uint8_t *lds, int wave, int lane, uint
     V4 z = V4{0, 0, 0, 0}, ek0 = V4{0, 0, 0, 0};
     if (wave < 2) {
         const uint4 hp = bs[NPOW * 128 + (i < N ? N - i - 1 : 0)]; /* H^(N - i) */
-        const uint32_t n0 = __builtin_amdgcn_readfirstlane(slot->iv[0]),
-                       n1 = __builtin_amdgcn_readfirstlane(slot->iv[1] ^ bswap32((uint32_t)(rec.seq >> 32))),
-                       n2 = __builtin_amdgcn_readfirstlane(slot->iv[2] ^ bswap32((uint32_t)rec.seq));
+        const bool ov = __builtin_amdgcn_readfirstlane(ivo.w) != 0;
+        const uint32_t n0 = __builtin_amdgcn_readfirstlane(ov ? ivo.x : slot->iv[0]),
+                       n1 = __builtin_amdgcn_readfirstlane((ov ? ivo.y : slot->iv[1]) ^ bswap32((uint32_t)(rec.seq >> 32))),
+                       n2 = __builtin_amdgcn_readfirstlane((ov ? ivo.z : slot->iv[2]) ^ bswap32((uint32_t)rec.seq));
         CtrConst cc = ctr_const(lds, lb_aes, rk, n0, n1, n2);
         cc.k10 = __builtin_amdgcn_readfirstlane(cc.k10);
         cc.k11 = __builtin_amdgcn_readfirstlane(cc.k11);
@@ -850,7 +854,8 @@ __device__ __forceinline__ uint64_t poll_word(const WorkerSlot *ms)
 constexpr int WORKER_WG = 128; /* two waves: wave 0 polls; both serve a two-wave record (mw_record) */
 
 __global__ void __launch_bounds__(WORKER_WG)
-    plugin_worker_kernel(WorkerSlot *mb, uint32_t epoch, const uint32_t *__restrict__ t0, uint64_t idle_ticks, uint64_t life_ticks)
+    plugin_worker_kernel(WorkerSlot *mb, uint32_t epoch, const uint32_t *__restrict__ t0, uint64_t idle_ticks, uint64_t life_ticks,
+                         uint64_t *activity)
 {
     /* AES tables | wave 0's Horner table | wave 1's | wave 0's lane-combination table | wave 1's | the poll's verdict | the
      * long record's hand-over */
@@ -861,7 +866,7 @@ __global__ void __launch_bounds__(WORKER_WG)
     const uint32_t tab = SP_TAB;
     build_aes_tables<WORKER_WG>(lds, 0, t0);
     __syncthreads();
-    WorkerSlot *ms = mb;
+    WorkerSlot *ms = mb + blockIdx.x; /* one mailbox per workgroup (engine.cpp PluginWorker: one per calling thread) */
     const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
     uint64_t t_last = t_start;
     uint32_t last = __builtin_amdgcn_readfirstlane(__hip_atomic_load(&ms->served, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
@@ -891,6 +896,14 @@ __global__ void __launch_bounds__(WORKER_WG)
                     if (seq == last && (int32_t)(sv - last) > 0)
                         seq = sv;
                     const uint64_t now = __builtin_amdgcn_s_memrealtime();
+                    if (seq == last && now - t_last > idle_ticks) {
+                        /* idle here: the workgroups of the dispatch leave together, when none of them has served a request
+                         * for idle_ticks (the last one served is in `activity`), so a caller rarely finds its own
+                         * workgroup gone while the others still hold the dispatch */
+                        const uint64_t a = __builtin_amdgcn_readfirstlane(
+                            __hip_atomic_load(activity, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+                        t_last = a > t_last ? a : t_last;
+                    }
                     if (seq == last && (quit != 0 || now - t_last > idle_ticks || now - t_start > life_ticks))
                         leave = true;
                     ring[k] = poll_word(ms);
@@ -927,6 +940,7 @@ __global__ void __launch_bounds__(WORKER_WG)
             pin[m] = load_full(ms->data + 16 * (size_t)(lane + 64 * wave + 64 * m));
         const ptls_hip_record_t rec = rq.rec;
         const uint32_t flags = __builtin_amdgcn_readfirstlane(rq.flags);
+        const uint4 ivo = (flags & WREQ_IV) ? uint4{rq.iv[0], rq.iv[1], rq.iv[2], 1u} : uint4{0, 0, 0, 0};
         const uint8_t *in = as_global(rq.in), *aad = as_global(rq.aad);
         uint8_t *out = as_global(rq.out);
         const KeySlot *slots = as_global(rq.slots);
@@ -973,27 +987,27 @@ __global__ void __launch_bounds__(WORKER_WG)
             const uint32_t tab_w = wave == 0 ? tab : TAB1, ctab_w = wave == 0 ? CTAB0 : CTAB1;
             if (open && a256)
                 sparse_record<14, true, true, true, 128>(lds, lane, lb_aes, tab_w, rec, 0, in, aad, out, result, slots, basis, supp,
-                                                         hp_slots, 1, mask, true, p2, nullptr, false, false, pa, ctab_w, wave, XSLOT);
+                                                         hp_slots, 1, mask, true, p2, nullptr, false, false, pa, ctab_w, wave, XSLOT, ivo);
             else if (open)
                 sparse_record<10, true, true, true, 128>(lds, lane, lb_aes, tab_w, rec, 0, in, aad, out, result, slots, basis, supp,
-                                                         hp_slots, 1, mask, true, p2, nullptr, false, false, pa, ctab_w, wave, XSLOT);
+                                                         hp_slots, 1, mask, true, p2, nullptr, false, false, pa, ctab_w, wave, XSLOT, ivo);
             else if (a256)
                 sparse_record<14, false, true, true, 128>(lds, lane, lb_aes, tab_w, rec, 0, in, aad, out, result, slots, basis, supp,
-                                                          hp_slots, 1, mask, true, p2, nullptr, false, false, pa, ctab_w, wave, XSLOT);
+                                                          hp_slots, 1, mask, true, p2, nullptr, false, false, pa, ctab_w, wave, XSLOT, ivo);
             else
                 sparse_record<10, false, true, true, 128>(lds, lane, lb_aes, tab_w, rec, 0, in, aad, out, result, slots, basis, supp,
-                                                          hp_slots, 1, mask, true, p2, nullptr, false, false, pa, ctab_w, wave, XSLOT);
+                                                          hp_slots, 1, mask, true, p2, nullptr, false, false, pa, ctab_w, wave, XSLOT, ivo);
         } else if (mw) {
             const V4 mine = (flags & WREQ_INLINE) ? pin[0] : elem_block(lane + 64 * wave);
             const uint32_t ctab_w = wave == 0 ? CTAB0 : CTAB1;
             if (open && a256)
-                mw_record<14, true, true>(lds, wave, lane, lb_aes, ctab_w, tab, rec, in, aad, out, result, slots, basis, supp, hp_slots, 1, mask, mine);
+                mw_record<14, true, true>(lds, wave, lane, lb_aes, ctab_w, tab, rec, in, aad, out, result, slots, basis, supp, hp_slots, 1, mask, mine, ivo);
             else if (open)
-                mw_record<10, true, true>(lds, wave, lane, lb_aes, ctab_w, tab, rec, in, aad, out, result, slots, basis, supp, hp_slots, 1, mask, mine);
+                mw_record<10, true, true>(lds, wave, lane, lb_aes, ctab_w, tab, rec, in, aad, out, result, slots, basis, supp, hp_slots, 1, mask, mine, ivo);
             else if (a256)
-                mw_record<14, false, true>(lds, wave, lane, lb_aes, ctab_w, tab, rec, in, aad, out, result, slots, basis, supp, hp_slots, 1, mask, mine);
+                mw_record<14, false, true>(lds, wave, lane, lb_aes, ctab_w, tab, rec, in, aad, out, result, slots, basis, supp, hp_slots, 1, mask, mine, ivo);
             else
-                mw_record<10, false, true>(lds, wave, lane, lb_aes, ctab_w, tab, rec, in, aad, out, result, slots, basis, supp, hp_slots, 1, mask, mine);
+                mw_record<10, false, true>(lds, wave, lane, lb_aes, ctab_w, tab, rec, in, aad, out, result, slots, basis, supp, hp_slots, 1, mask, mine, ivo);
         } else if (wave == 0) {
             {
                 /* the record's first two elements per lane, as the launched single-record kernel reads them */
@@ -1008,16 +1022,16 @@ __global__ void __launch_bounds__(WORKER_WG)
                 const uint32_t ctab = CTAB0;
                 if (open && a256)
                     sparse_record<14, true, true, true>(lds, lane, lb_aes, tab, rec, 0, in, aad, out, result, slots, basis, supp,
-                                                        hp_slots, 1, mask, true, pre, wclk, WORKER_STAMPS, false, pa, ctab);
+                                                        hp_slots, 1, mask, true, pre, wclk, WORKER_STAMPS, false, pa, ctab, 0, 0, ivo);
                 else if (open)
                     sparse_record<10, true, true, true>(lds, lane, lb_aes, tab, rec, 0, in, aad, out, result, slots, basis, supp,
-                                                        hp_slots, 1, mask, true, pre, wclk, WORKER_STAMPS, false, pa, ctab);
+                                                        hp_slots, 1, mask, true, pre, wclk, WORKER_STAMPS, false, pa, ctab, 0, 0, ivo);
                 else if (a256)
                     sparse_record<14, false, true, true>(lds, lane, lb_aes, tab, rec, 0, in, aad, out, result, slots, basis, supp,
-                                                         hp_slots, 1, mask, true, pre, wclk, WORKER_STAMPS, false, pa, ctab);
+                                                         hp_slots, 1, mask, true, pre, wclk, WORKER_STAMPS, false, pa, ctab, 0, 0, ivo);
                 else
                     sparse_record<10, false, true, true>(lds, lane, lb_aes, tab, rec, 0, in, aad, out, result, slots, basis, supp,
-                                                         hp_slots, 1, mask, true, pre, wclk, WORKER_STAMPS, false, pa, ctab);
+                                                         hp_slots, 1, mask, true, pre, wclk, WORKER_STAMPS, false, pa, ctab, 0, 0, ivo);
             }
         }
         /* the wave holding the tag (wave 1 of a two-wave record; wave 0 otherwise): every store of the call reaches system
@@ -1045,16 +1059,19 @@ __global__ void __launch_bounds__(WORKER_WG)
         __syncthreads(); /* both waves are done with the request (its LDS tables, the verdict slot) */
         last = seq;
         t_last = __builtin_amdgcn_s_memrealtime();
+        if (threadIdx.x == 0)
+            __hip_atomic_fetch_max(activity, t_last, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
     if (threadIdx.x == 0)
         __hip_atomic_store(&ms->exited, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-int launch_plugin_worker(WorkerSlot *mb, uint32_t epoch, const uint32_t *t0, uint64_t idle_ticks, uint64_t life_ticks, void *stream)
+int launch_plugin_worker(WorkerSlot *mb, unsigned nmb, uint32_t epoch, const uint32_t *t0, uint64_t idle_ticks, uint64_t life_ticks,
+                         uint64_t *activity, void *stream)
 {
-    hipLaunchKernelGGL(plugin_worker_kernel, dim3(1), dim3(WORKER_WG), 0, static_cast<hipStream_t>(stream), mb, epoch, t0, idle_ticks,
-                       life_ticks);
+    hipLaunchKernelGGL(plugin_worker_kernel, dim3(nmb), dim3(WORKER_WG), 0, static_cast<hipStream_t>(stream), mb, epoch, t0, idle_ticks,
+                       life_ticks, activity);
     return (int)hipGetLastError();
 }
 

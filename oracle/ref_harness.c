@@ -182,9 +182,107 @@ Exit:
     return ret;
 }
 
+/* ---- t/ptlsbench.c's loop on several threads at once, each with its own contexts (a server's worker threads) ----
+ * Every thread makes its own encrypt and decrypt context with ptls_aead_new (bench_run_aead :218-225), then, behind a
+ * barrier, runs `n` rounds of bench_run_one's body: ptls_aead_encrypt of the zero input into one of 16 outputs (AAD =
+ * uint64_t h[4], h[0] = seq) and ptls_aead_decrypt of it, checking the length.  Returns calls (encrypt + decrypt) per
+ * second over all threads, wall clock from the barrier to the last thread's end; -1 on a failed decrypt. */
+struct mt_job {
+    const ptls_aead_algorithm_t *aead;
+    size_t n, l;
+    pthread_barrier_t *bar;
+    double t_end;
+    int err;
+};
+
+static void *mt_worker(void *p)
+{
+    struct mt_job *j = p;
+    uint8_t secret[PTLS_MAX_SECRET_SIZE];
+    memset(secret, 'z', sizeof(secret));
+    ptls_aead_context_t *e = ptls_aead_new((ptls_aead_algorithm_t *)j->aead, &ptls_minicrypto_sha256, 1, secret, NULL);
+    ptls_aead_context_t *d = ptls_aead_new((ptls_aead_algorithm_t *)j->aead, &ptls_minicrypto_sha256, 0, secret, NULL);
+    uint8_t *in = calloc(1, j->l + 1), *dec = malloc(j->l + 1), *enc = malloc(16 * (j->l + PTLS_MAX_DIGEST_SIZE));
+    uint64_t h[4] = {0};
+    pthread_barrier_wait(j->bar);
+    j->err = e == NULL || d == NULL;
+    for (size_t i = 0; i < j->n && !j->err; ++i) {
+        uint8_t *o = enc + (i & 15) * (j->l + PTLS_MAX_DIGEST_SIZE);
+        h[0] = i + 1;
+        size_t el = ptls_aead_encrypt(e, o, in, j->l, h[0], h, sizeof(h));
+        if (ptls_aead_decrypt(d, dec, o, el, h[0], h, sizeof(h)) != j->l)
+            j->err = 1;
+    }
+    j->t_end = now();
+    if (e != NULL)
+        ptls_aead_free(e);
+    if (d != NULL)
+        ptls_aead_free(d);
+    free(in);
+    free(dec);
+    free(enc);
+    return NULL;
+}
+
+double ref_ptlsbench_mt(const ptls_aead_algorithm_t *aead, int threads, size_t n, size_t l)
+{
+    pthread_t th[256];
+    struct mt_job jobs[256];
+    pthread_barrier_t bar;
+    if (threads < 1 || threads > 256)
+        return -1;
+    pthread_barrier_init(&bar, NULL, (unsigned)threads + 1);
+    for (int t = 0; t < threads; ++t) {
+        jobs[t] = (struct mt_job){aead, n, l, &bar, 0, 0};
+        pthread_create(&th[t], NULL, mt_worker, &jobs[t]);
+    }
+    pthread_barrier_wait(&bar);
+    double t0 = now(), t1 = t0;
+    int err = 0;
+    for (int t = 0; t < threads; ++t) {
+        pthread_join(th[t], NULL);
+        err |= jobs[t].err;
+        if (jobs[t].t_end > t1)
+            t1 = jobs[t].t_end;
+    }
+    pthread_barrier_destroy(&bar);
+    return err ? -1 : 2.0 * (double)n * threads / (t1 - t0);
+}
+
+/* ---- context lifecycle (lib/picotls.c:6458-6479): `n` rounds of ptls_aead_new_direct, one seal, ptls_aead_free; the
+ * microseconds of each new / seal / free go to the three arrays ---- */
+int ref_aead_lifecycle(const ptls_aead_algorithm_t *aead, size_t n, size_t l, double *new_us, double *seal_us, double *free_us)
+{
+    uint8_t key[32], iv[12], *in = calloc(1, l + 1), *out = malloc(l + 16);
+    memset(key, 0x42, sizeof(key));
+    memset(iv, 0x24, sizeof(iv));
+    int ret = 0;
+    for (size_t i = 0; i < n; ++i) {
+        key[0] = (uint8_t)i;
+        double t0 = now();
+        ptls_aead_context_t *c = ptls_aead_new_direct((ptls_aead_algorithm_t *)aead, 1, key, iv);
+        double t1 = now();
+        if (c == NULL) {
+            ret = -1;
+            break;
+        }
+        ptls_aead_encrypt(c, out, in, l, i, iv, sizeof(iv));
+        double t2 = now();
+        ptls_aead_free(c);
+        double t3 = now();
+        new_us[i] = (t1 - t0) * 1e6;
+        seal_us[i] = (t2 - t1) * 1e6;
+        free_us[i] = (t3 - t2) * 1e6;
+    }
+    free(in);
+    free(out);
+    return ret;
+}
+
 /* ---- CPU baseline: lib/fusion.c over a batch of distinct record buffers, 1..N pinned threads ---- */
 
 struct bench_job {
+    const ptls_aead_algorithm_t *aead;
     int bits, cpu, do_open;
     const uint8_t *key, *iv;
     uint8_t *in;     /* nrec * stride bytes */
@@ -206,7 +304,7 @@ static void *bench_worker(void *p)
         pthread_setaffinity_np(pthread_self(), sizeof(s), &s);
     }
     /* one ptls_aead_context_t per thread per key */
-    ptls_aead_context_t *ctx = ptls_aead_new_direct(pick(j->bits), !j->do_open, j->key, j->iv);
+    ptls_aead_context_t *ctx = ptls_aead_new_direct((ptls_aead_algorithm_t *)j->aead, !j->do_open, j->key, j->iv);
     pthread_barrier_wait(j->bar);
     double t0 = now();
     for (int pass = 0; pass < j->passes; ++pass) {
@@ -226,9 +324,25 @@ static void *bench_worker(void *p)
 /* Seals (do_open = 0) or opens (do_open = 1) records i = 0..nrec-1 held at in + i*stride, writing to
  * out + i*stride, `passes` times over; record i uses seq = i and aad + i*aadlen.  Returns the wall time of
  * the slowest thread (all threads start behind a barrier).  cpus: cpu ids to pin to (NULL = no pinning). */
+double ref_bench_algo(int nt, int bits, int do_open, const void *key, const void *iv, void *in, void *out, size_t nrec, size_t len,
+                      size_t stride, const void *aad, size_t aadlen, int threads, const int *cpus, int passes);
+
 double ref_bench(int bits, int do_open, const void *key, const void *iv, void *in, void *out, size_t nrec, size_t len,
                  size_t stride, const void *aad, size_t aadlen, int threads, const int *cpus, int passes)
 {
+    return ref_bench_algo(0, bits, do_open, key, iv, in, out, nrec, len, stride, aad, aadlen, threads, cpus, passes);
+}
+
+/* nt = 1: the reference's non-temporal engine, ptls_non_temporal_aes{128,256}gcm (lib/fusion.c:2109-2179): encrypt through
+ * non_temporal_encrypt_v256 (VAES / VPCLMULQDQ, 256-bit lanes) when ptls_fusion_can_aesni256, decrypt through
+ * non_temporal_decrypt128; the same bytes as ptls_fusion_aes*gcm.  ptls_fusion_is_supported_by_cpu() is what sets
+ * ptls_fusion_can_aesni256 (:2219-2249), so it runs first. */
+double ref_bench_algo(int nt, int bits, int do_open, const void *key, const void *iv, void *in, void *out, size_t nrec, size_t len,
+                      size_t stride, const void *aad, size_t aadlen, int threads, const int *cpus, int passes)
+{
+    (void)ptls_fusion_is_supported_by_cpu();
+    const ptls_aead_algorithm_t *aead =
+        nt ? (bits == 256 ? &ptls_non_temporal_aes256gcm : &ptls_non_temporal_aes128gcm) : pick(bits);
     pthread_t th[512];
     struct bench_job jobs[512];
     pthread_barrier_t bar;
@@ -239,7 +353,7 @@ double ref_bench(int bits, int do_open, const void *key, const void *iv, void *i
     pthread_barrier_init(&bar, NULL, (unsigned)threads);
     for (int t = 0; t < threads; ++t) {
         size_t a = nrec * (size_t)t / (size_t)threads, b = nrec * (size_t)(t + 1) / (size_t)threads;
-        jobs[t] = (struct bench_job){bits, cpus != NULL ? cpus[t] : -1, do_open, key, iv, in, out, a, b - a, len, stride, aadlen,
+        jobs[t] = (struct bench_job){aead, bits, cpus != NULL ? cpus[t] : -1, do_open, key, iv, in, out, a, b - a, len, stride, aadlen,
                                      aad, &bar, passes < 1 ? 1 : passes, 0};
         pthread_create(&th[t], NULL, bench_worker, &jobs[t]);
     }

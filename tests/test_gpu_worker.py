@@ -1,11 +1,15 @@
-"""The plugin worker (engine.cpp worker_call, sparse_kernel.hip plugin_worker_kernel): a resident two-wave kernel that
-serves plugin calls from a pinned mailbox instead of one launch per call.  Its lifecycle is exercised through the
+"""The plugin worker (engine.cpp worker_call, sparse_kernel.hip plugin_worker_kernel): a resident kernel whose workgroups
+serve plugin calls from pinned mailboxes (one per calling thread) instead of one launch per call.  Its lifecycle is exercised through the
 reference's own picotls lifecycle code (tests/plugin_driver.py) and every output is compared with lib/fusion.c
 (oracle/_ref): calls separated by gaps longer than the worker's idle timeout (it leaves, the next call relaunches it),
-IV changes (ptls_aead_xor_iv: the worker leaves before the key slot's IV is rewritten), contexts created and freed
-between calls (a freed key slot's address comes back with other keys), header-protection ECB blocks (one launch each) and
+IV changes (ptls_aead_xor_iv: the IV travels in the request), contexts created and freed between calls (a freed pooled
+key slot comes back with other keys once no resident workgroup can hold it), header-protection ECB blocks (one launch each) and
 fused header protection interleaved with AEAD calls on the worker, and two threads sharing it.  Each case runs in its
-own process, with the worker on (the default) and off (PTLS_HIP_PLUGIN_WORKER=0: one launch per call)."""
+own process, with the worker on (the default) and off (PTLS_HIP_PLUGIN_WORKER=0: one launch per call).
+test_plugin_worker_threads: eight threads with their own contexts at once over 1, 4 and 8 mailboxes (shared homes, the
+try-lock hand-off, a workgroup leaving while the others serve), with IV changes, context churn on every thread (pooled
+slots recycled while other threads' requests run), records too long for a mailbox (the context's own staging) and gaps
+past the idle timeout and the lifetime, every output against lib/fusion.c."""
 import os
 import subprocess
 import sys
@@ -96,6 +100,71 @@ for t in ts:
 assert not errors, errors
 print("ok")
 """
+
+
+_CASE_MT = r"""
+import sys, time, threading
+sys.path[:0] = {paths!r}
+import numpy as np
+import plugin_driver
+from oracle_lib import Ref, tls_aad
+drv, ref = plugin_driver.PluginDriver(), Ref()
+errors = []
+
+def thread_main(t):
+    try:
+        r = np.random.default_rng(1000 + t)
+        rb = lambda n: r.integers(0, 256, n, dtype=np.uint8).tobytes()  # noqa: E731
+        bits = 128 if t % 2 == 0 else 256
+        key, iv = rb(bits // 8), rb(12)
+        e, d = drv.new(bits, key, iv, 1), drv.new(bits, key, iv, 0)
+        for i in range(60):
+            if i % 15 == 7:  # a new connection on this thread: the old contexts go back to the pool
+                drv.free(e)
+                drv.free(d)
+                key, iv = rb(bits // 8), rb(12)
+                e, d = drv.new(bits, key, iv, 1), drv.new(bits, key, iv, 0)
+            if i % 11 == 5:
+                x = rb(int(r.integers(1, 13)))
+                drv.xor_iv(e, x)
+                drv.xor_iv(d, x)
+                iv = bytes(a ^ b for a, b in zip(iv, x + bytes(12 - len(x))))
+            if i % 20 == 13:
+                time.sleep(0.003)  # past the idle timeout and the lifetime of the dispatch
+            L = int(r.choice([0, 1, 15, 16, 17, 700, 1350, 1500, 4096, 16384, 17000, 20000]))
+            pt, aad = rb(L), tls_aad(L)
+            ct = drv.encrypt(e, pt, i, aad)
+            assert ct == ref.seal(key, iv, i, aad, pt), ("seal", t, i, L)
+            assert drv.decrypt(d, ct, i, aad) == pt, ("open", t, i, L)
+            bad = bytearray(ct)
+            if bad:
+                bad[-1] ^= 1
+                assert drv.decrypt(d, bytes(bad), i, aad) is None, ("tamper", t, i, L)
+        drv.free(e)
+        drv.free(d)
+    except Exception as ex:  # noqa: BLE001
+        errors.append(repr(ex))
+
+ts = [threading.Thread(target=thread_main, args=(t,)) for t in range(8)]
+for t in ts:
+    t.start()
+for t in ts:
+    t.join()
+assert not errors, errors
+print("ok")
+"""
+
+
+@pytest.mark.parametrize("workers", ["1", "4", "8"])
+def test_plugin_worker_threads(workers):
+    from oracle_lib import Ref
+    if not Ref.available:
+        pytest.skip("oracle/_ref not built")
+    paths = [os.path.join(ROOT, "tests"), os.path.join(ROOT, "hsig-picotls_amd"), ROOT]
+    env = dict(os.environ, PTLS_HIP_PLUGIN_WORKER="1", PTLS_HIP_PLUGIN_WORKERS=workers)
+    r = subprocess.run([sys.executable, "-c", _CASE_MT.format(paths=paths)], env=env, capture_output=True, text=True,
+                       timeout=240)
+    assert r.returncode == 0 and r.stdout.strip().endswith("ok"), (r.returncode, r.stdout[-2000:], r.stderr[-3000:])
 
 
 @pytest.mark.parametrize("worker", ["1", "0"])
