@@ -525,6 +525,109 @@ def host_e2e(args, cfg, eng, ks, recs, lens, d_pt, d_aad, aad_len):
     return out
 
 
+def node_e2e(args, cfg, devices):
+    """The host-resident path over several devices in ONE process (ptls_hip_node_*): the config's
+    records (1 GiB by default) in host memory whose per-device ranges are bound to each device's NUMA node
+    (ptls_hip_node_host_alloc), byte-balanced contiguous ranges per device, one host thread per device (pinned to that
+    device's node) running its zero-copy pipeline; wall clock around each node seal / open.  Whole node = payload bytes /
+    the slowest device's seconds (ptls_hip_node_last_split).  Parity: every record opens to its bytes, and the sealed
+    records that have a lib/fusion.c digest in tests/golden/configs.json are compared with it."""
+    import torch
+    import ptls_hip
+    idx, recs, in_total, out_total, lens = make_workload(cfg, 0, 1, "weak", CONFIGS[args.config]["n"])
+    L_mean = float(lens.mean())
+    n = args.e2e_records or max(1, min(len(recs), int((1 << 30) / L_mean)))
+    sub, idx, lens = recs[:n].copy(), idx[:n], lens[:n]
+    in_lo, out_lo = int(sub["in_off"][0]), int(sub["out_off"][0])
+    sub["in_off"] -= np.uint64(in_lo)
+    sub["out_off"] -= np.uint64(out_lo)
+    in_bytes = int(sub["in_off"][-1] + sub["len"][-1] + 16)
+    out_bytes = int(sub["out_off"][-1] + sub["len"][-1] + 16)
+    aad = build_aad(cfg, idx, lens)
+    sub["aad_off"] = np.arange(n, dtype=np.uint64) * np.uint64(16)
+    nd = len(devices)
+    node = ptls_hip.Node(devices, cfg["key_len"], cfg["keys"], transport=ptls_hip.TRANSPORT_MAPPED)
+    keys, ivs = make_keys(cfg)
+    node.set_keys(0, keys, ivs)
+    bounds = ptls_hip.partition_bytes(sub, nd)
+
+    def splits(field, total):
+        return [0] + [int(sub[field][bounds[d]]) if bounds[d] < n else total for d in range(1, nd)] + [total]
+    h_in = node.host_alloc(in_bytes, splits("in_off", in_bytes))
+    h_pt = node.host_alloc(in_bytes, splits("in_off", in_bytes))
+    h_ct = node.host_alloc(out_bytes, splits("out_off", out_bytes))
+    h_aad = torch.from_numpy(aad).pin_memory()
+    h_res = torch.zeros(n, dtype=torch.int64).pin_memory()
+    try:
+        # the records' bytes: the same splitmix64 streams as the device-resident run, generated on the first device
+        eng = ptls_hip.Engine(devices[0])
+        gb = ptls_hip.Batch(eng, sub)
+        d_buf = torch.zeros(in_bytes, dtype=torch.uint8, device=f"cuda:{devices[0]}")
+        d_idx = torch.from_numpy(idx.astype(np.int64)).to(d_buf.device)
+        gb.fill(d_buf, SEED_DATA, index=d_idx)
+        torch.cuda.synchronize(d_buf.device)
+        torch.from_numpy(h_in).copy_(d_buf.cpu())
+        del d_buf, d_idx
+        gb.close()
+        eng.close()
+        sub_o = sub.copy()
+        sub_o["in_off"], sub_o["out_off"] = sub["out_off"], sub["in_off"]
+        node.seal(sub, h_in, h_aad, h_ct)  # warm-up
+        ts, to, dev_s, dev_o = [], [], [], []
+        for _ in range(3):
+            t0 = time.perf_counter()
+            node.seal(sub, h_in, h_aad, h_ct)
+            ts.append(time.perf_counter() - t0)
+            dev_s.append(node.last_split()[0])
+            h_pt[:] = 0
+            h_res.zero_()
+            t0 = time.perf_counter()
+            node.open(sub_o, h_ct, h_aad, h_pt, h_res)
+            to.append(time.perf_counter() - t0)
+            dev_o.append(node.last_split()[0])
+        sumL = float(lens.sum())
+        edge = np.zeros(in_bytes + 1, dtype=np.int32)
+        np.add.at(edge, sub["in_off"].astype(np.int64), 1)
+        np.add.at(edge, (sub["in_off"] + sub["len"]).astype(np.int64), -1)
+        mask = np.cumsum(edge[:-1]) > 0
+        ok_open = bool((h_res.numpy() == lens.astype(np.int64)).all())
+        ok_pt = bool(np.array_equal(h_pt[mask], h_in[mask]))
+        d_ct = torch.from_numpy(h_ct).to("cuda")
+        golden_n = golden_check(args.config, idx, sub, d_ct)
+        del d_ct
+        if not (ok_open and ok_pt):
+            raise AssertionError(f"node host-resident round trip failed (status ok={ok_open}, bytes ok={ok_pt})")
+        numa = node.numa_nodes()
+        placement = []
+        sp_in = splits("in_off", in_bytes)
+        for d in range(nd):
+            pages = ptls_hip.page_nodes(h_in[sp_in[d]:sp_in[d + 1]], stride=16)
+            placement.append(round(float((pages == numa[d]).mean()), 3) if numa[d] >= 0 and len(pages) else None)
+        t_s, t_o = float(np.median(ts)), float(np.median(to))
+        per_dev = []
+        for d in range(nd):
+            share = float(lens[bounds[d]:bounds[d + 1]].sum())
+            s_d = float(np.median([x[d] for x in dev_s]))
+            o_d = float(np.median([x[d] for x in dev_o]))
+            per_dev.append(dict(device=devices[d], numa_node=numa[d], records=[bounds[d], bounds[d + 1]], payload_bytes=int(share),
+                                seal_s=round(s_d, 4), open_s=round(o_d, 4),
+                                seal_open_gibps=round(2 * share / (s_d + o_d) / GIB, 2) if s_d + o_d > 0 else None,
+                                input_pages_on_its_node=placement[d]))
+        return dict(devices=devices, records=n, payload_bytes=int(sumL), transport="mapped (zero-copy)",
+                    seal_gibps=round(sumL / t_s / GIB, 2), open_gibps=round(sumL / t_o / GIB, 2),
+                    seal_open_gibps=round(2 * sumL / (t_s + t_o) / GIB, 2),
+                    whole_node_from_slowest_device_gibps=round(2 * sumL / (max(float(np.median([max(x) for x in dev_s])), 1e-9) +
+                                                                           max(float(np.median([max(x) for x in dev_o])), 1e-9)) / GIB, 2),
+                    per_device=per_dev, numa_nodes=numa,
+                    parity=dict(open_all_ok=ok_open, roundtrip_bytes_equal=ok_pt, golden_records_checked=golden_n),
+                    note="host buffers from ptls_hip_node_host_alloc: each device's range bound to its NUMA node; "
+                         "wall clock around ptls_hip_node_seal / open, every byte crossing PCIe inside the timed call")
+    finally:
+        for a in (h_in, h_pt, h_ct):
+            ptls_hip.Node.host_free(a)
+        node.close()
+
+
 def report_ranks(result, per_rank, world, steps, elapsed):
     """per-rank and whole-node rates from every rank's [seconds, plaintext bytes per step, seal ms, open ms, first record,
     end record, golden records checked]: whole node = sum of all ranks' bytes / the slowest rank's time"""
@@ -585,6 +688,9 @@ def main():
                     help="every rank on this device (default: LOCAL_RANK); rehearses N ranks on a one-GPU box")
     ap.add_argument("--scaling", default="weak", choices=["weak", "strong"],
                     help="weak: every rank its own shard of the config's size; strong: one batch split by bytes")
+    ap.add_argument("--node-e2e", default="",
+                    help="only the host-resident path over these devices in one process (ptls_hip_node_*), e.g. 0,1,2,3; "
+                         "a device may repeat (one-GPU rehearsal: 0,0)")
     ap.add_argument("--dry-run", action="store_true", help=argparse.SUPPRESS)  # CPU rehearsal of the rank logic (tests)
     args = ap.parse_args()
     launch_ranks(args)  # N > 1 without a launcher: re-run as N ranks, before any GPU call
@@ -601,6 +707,14 @@ def main():
     import torch
     import torch.distributed as dist
     import ptls_hip
+    if args.node_e2e:
+        devices = [int(x) for x in args.node_e2e.split(",")]
+        res = {"metric": "GiB/s AES-GCM seal+open, host-resident, one process over a node's GPUs (ptls_hip_node_*)",
+               "config": {"workload": cfg["desc"], "key_bits": cfg["key_len"] * 8}, "unit": "GiB/s"}
+        res.update(node_e2e(args, cfg, devices))
+        res["value"] = res["seal_open_gibps"]
+        print(json.dumps(res), flush=True)
+        return
     dev = local if args.device < 0 else args.device
     torch.cuda.set_device(dev)
     if world > 1:
@@ -793,6 +907,15 @@ def main():
     for o in (seal_b, open_b):
         o.close()
     del d_pt, d_ct, d_out, d_aad, d_res, clk_s, clk_o
+    if not args.no_e2e and world > 1:
+        # the host-resident figure for the whole node: ONE process (rank 0) drives every rank's device through the node
+        # API, each device's records in host memory on its own NUMA node; the other ranks wait (their GPUs idle)
+        torch.cuda.empty_cache()
+        devs = [int(r[0]) for r in gather_ranks([float(dev)], world)]
+        dist.barrier()
+        if rank == 0:
+            result["host_e2e_node"] = node_e2e(args, cfg, devs)
+        dist.barrier()
     if rank == 0 and world == 1 and not args.no_plugin:
         result["plugin_ptlsbench"] = plugin_ptlsbench()
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -10,7 +10,8 @@ import os
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.environ.get("PTLS_HIP_LIB") or os.path.join(HERE, "libptls_hip.so")
+PRODUCT_LIB = os.path.join(HERE, "libptls_hip.so")
+LIB_PATH = os.environ.get("PTLS_HIP_LIB") or PRODUCT_LIB
 UINT64_MAX = (1 << 64) - 1
 
 RECORD_DTYPE = np.dtype([("in_off", "<u8"), ("out_off", "<u8"), ("aad_off", "<u8"), ("seq", "<u8"),
@@ -100,6 +101,11 @@ SIGNATURES = {
     "ptls_hip_node_seal": (_i, [_vp, _vp, _sz, _vp, _vp, _vp]),
     "ptls_hip_node_open": (_i, [_vp, _vp, _sz, _vp, _vp, _vp, _vp]),
     "ptls_hip_node_last_split": (_i, [_vp, _vp, _vp]),
+    "ptls_hip_device_numa_node": (_i, [_i]),
+    "ptls_hip_node_numa": (_i, [_vp, _vp]),
+    "ptls_hip_node_host_alloc": (_vp, [_vp, _sz, _vp]),
+    "ptls_hip_node_host_free": (None, [_vp, _sz]),
+    "ptls_hip_host_page_nodes": (_sz, [_vp, _sz, _sz, _vp, _sz]),
 }
 DATA_SYMBOLS = ("ptls_hip_aes128ctr", "ptls_hip_aes128gcm", "ptls_hip_aes256ctr", "ptls_hip_aes256gcm",
                 "ptls_hip_non_temporal_aes128gcm", "ptls_hip_non_temporal_aes256gcm")
@@ -117,10 +123,13 @@ def lib():
         if not os.path.exists(LIB_PATH):
             raise HipError(f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'`")
         L = ctypes.CDLL(LIB_PATH)
+        product = os.path.realpath(LIB_PATH) == os.path.realpath(PRODUCT_LIB)
         for name, (res, args) in SIGNATURES.items():
             f = getattr(L, name, None)
-            if f is None:  # an older build loaded by an A/B tool (PTLS_HIP_LIB); tests/test_abi.py checks the product
-                continue
+            if f is None:
+                if product:  # the product library must export every entry point of include/ptls_hip.h
+                    raise HipError(f"{LIB_PATH} does not export {name}: stale or broken build")
+                continue  # an older build loaded by an A/B tool (PTLS_HIP_LIB)
             f.restype = res
             f.argtypes = args
         _lib = L
@@ -351,10 +360,36 @@ class Node:
         _check(lib().ptls_hip_node_last_split(self.ptr, sec.ctypes.data, b.ctypes.data), "node_last_split")
         return sec.tolist(), [int(x) for x in b]
 
+    def numa_nodes(self):
+        """each device's NUMA node (-1: unknown)"""
+        out = np.zeros(self.ndev, dtype=np.int32)
+        _check(lib().ptls_hip_node_numa(self.ptr, out.ctypes.data), "node_numa")
+        return [int(x) for x in out]
+
+    def host_alloc(self, nbytes, splits):
+        """a uint8 numpy array over `nbytes` of host memory whose byte range [splits[d], splits[d + 1]) lives on device d's
+        NUMA node, registered with every device (ptls_hip_node_host_alloc); free it with host_free"""
+        sp = np.ascontiguousarray(splits, dtype=np.uint64)
+        p = lib().ptls_hip_node_host_alloc(self.ptr, nbytes, sp.ctypes.data)
+        if not p:
+            raise HipError(f"ptls_hip_node_host_alloc: {last_error()}")
+        return np.ctypeslib.as_array((ctypes.c_uint8 * nbytes).from_address(p))
+
+    @staticmethod
+    def host_free(arr):
+        lib().ptls_hip_node_host_free(arr.ctypes.data, arr.nbytes)
+
     def close(self):
         if self.ptr:
             lib().ptls_hip_node_free(self.ptr)
             self.ptr = None
+
+
+def page_nodes(arr, stride=1, cap=1 << 16):
+    """the NUMA node of every stride-th page of a host array (move_pages)"""
+    out = np.zeros(cap, dtype=np.int32)
+    n = lib().ptls_hip_host_page_nodes(arr.ctypes.data, arr.nbytes, stride, out.ctypes.data, cap)
+    return out[:n]
 
 
 def clock_of(stamps, grid):

@@ -359,6 +359,18 @@ int ptls_hip_node_seal(ptls_hip_node_t *node, const ptls_hip_record_t *recs, siz
 int ptls_hip_node_open(ptls_hip_node_t *node, const ptls_hip_record_t *recs, size_t n, const void *h_in, const void *h_aad,
                        void *h_out, uint64_t *h_result);
 int ptls_hip_node_last_split(ptls_hip_node_t *node, double *seconds, size_t *bounds);
+/* NUMA placement (each GPU's records in host memory on its own NUMA node).  device_numa_node: the node
+ * a device's PCI function hangs off (sysfs), -1 if unknown.  node_numa: that node for every device of the node (ndev
+ * ints).  Each device's host thread runs on its node's CPUs.  node_host_alloc: `bytes` of host memory whose range
+ * [splits[d], splits[d + 1]) (ndev + 1 byte offsets, 0 .. bytes; whole pages, a shared page goes with the lower range)
+ * is bound to device d's node and faulted in there, registered with every device (mapped, portable) so both transports
+ * use it zero-copy; released with node_host_free(ptr, bytes).  host_page_nodes: the node of every stride-th page of
+ * [ptr, ptr + bytes) (move_pages), at most cap of them; returns how many were written. */
+int ptls_hip_device_numa_node(int device);
+int ptls_hip_node_numa(ptls_hip_node_t *node, int *numa_nodes);
+void *ptls_hip_node_host_alloc(ptls_hip_node_t *node, size_t bytes, const size_t *splits);
+void ptls_hip_node_host_free(void *ptr, size_t bytes);
+size_t ptls_hip_host_page_nodes(const void *ptr, size_t bytes, size_t stride, int *nodes, size_t cap);
 
 /* ------------------------------------------------------------------------------------------ *
  * 3. synthetic workload (bench / tests): the payload of descriptor i is the splitmix64 stream     *

@@ -26,7 +26,7 @@ def _bench(*args, timeout=300):
 
 def test_bench_two_ranks_on_one_device():
     rc, lines, err = _bench("--gpus", "2", "--device", "0", "--config", "c5", "--records", "65536", "--steps", "2",
-                            "--warmup", "1", "--no-cpu-baseline", "--no-e2e", "--no-plugin")
+                            "--warmup", "1", "--no-cpu-baseline", "--e2e-records", "20000", "--no-plugin")
     assert rc == 0, err[-4000:]
     assert len(lines) == 1
     r = lines[0]
@@ -37,3 +37,25 @@ def test_bench_two_ranks_on_one_device():
     assert r["parity"]["open_all_ok"] and r["parity"]["roundtrip_bytes_equal"]
     assert r["value"] > 0 and all(x["seal_gibps"] > 0 for x in r["per_rank"])
     assert r["clock_in_run"]["seal_ghz"] > 0.5
+    # the whole node's host-resident figure, driven by rank 0 through the node API over both ranks' devices
+    e = r["host_e2e_node"]
+    assert e["devices"] == [0, 0] and len(e["per_device"]) == 2 and e["seal_open_gibps"] > 0
+    assert e["parity"]["open_all_ok"] and e["parity"]["roundtrip_bytes_equal"] and e["parity"]["golden_records_checked"] >= 64
+
+
+def test_bench_node_e2e_device_listed_twice():
+    """bench.py --node-e2e: the host-resident path over a node's devices in one process (ptls_hip_node_*), each device's
+    records in host memory bound to its NUMA node; here device 0 listed twice (two engines, two host threads).  Reports the
+    NUMA node every device's range went to, and the share of its input pages found there (move_pages)."""
+    rc, lines, err = _bench("--node-e2e", "0,0", "--config", "c4", "--e2e-records", "30000")
+    assert rc == 0, err[-4000:]
+    r = lines[-1]
+    assert r["devices"] == [0, 0] and r["records"] == 30000 and len(r["per_device"]) == 2
+    assert r["parity"]["open_all_ok"] and r["parity"]["roundtrip_bytes_equal"]
+    assert r["parity"]["golden_records_checked"] >= 64  # configs[3]'s first 64 records against lib/fusion.c
+    assert all(isinstance(x, int) for x in r["numa_nodes"]) and r["numa_nodes"][0] == r["numa_nodes"][1]
+    for d in r["per_device"]:
+        assert d["seal_s"] > 0 and d["records"][1] > d["records"][0]
+        if d["numa_node"] >= 0:  # a known node: the range's pages were bound there
+            assert d["input_pages_on_its_node"] == 1.0, d
+    print(json.dumps({k: r[k] for k in ("seal_open_gibps", "numa_nodes", "per_device")}))
