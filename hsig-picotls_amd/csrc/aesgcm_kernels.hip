@@ -4,6 +4,7 @@
  * header-protection ECB kernel, key setup, the synthetic record generator, and the host launchers.
  */
 #include "batch_kernel.h"
+#include "gf128.h"
 
 namespace ptls_hip {
 
@@ -115,10 +116,6 @@ __global__ void __launch_bounds__(64) aesecb_one_kernel(uint4 blk, const KeySlot
  *  key setup: one thread per key slot (setup_crypto, lib/fusion.c:1184-1206, :984-1010)    *
  * ======================================================================================= */
 
-struct U128 {
-    uint64_t hi, lo; /* big-endian view: hi holds raw bytes 0..7 (byte 0 most significant) */
-};
-
 __device__ __forceinline__ U128 u128_from_raw(V4 v)
 {
     return U128{__builtin_bswap64((uint64_t)v.w0 | ((uint64_t)v.w1 << 32)), __builtin_bswap64((uint64_t)v.w2 | ((uint64_t)v.w3 << 32))};
@@ -128,30 +125,6 @@ __device__ __forceinline__ V4 u128_to_raw(U128 u)
 {
     const uint64_t a = __builtin_bswap64(u.hi), b = __builtin_bswap64(u.lo);
     return V4{(uint32_t)a, (uint32_t)(a >> 32), (uint32_t)b, (uint32_t)(b >> 32)};
-}
-
-/* multiply by x in GCM's reflected bit order (SP 800-38D: V >> 1, xor R if the dropped bit was set) */
-__device__ __forceinline__ U128 gf_mulx(U128 v)
-{
-    const uint64_t carry = v.lo & 1;
-    U128 o{v.hi >> 1, (v.lo >> 1) | (v.hi << 63)};
-    if (carry)
-        o.hi ^= 0xe100000000000000ull;
-    return o;
-}
-
-__device__ U128 gf_mul_slow(U128 x, U128 y)
-{
-    U128 z{0, 0}, v = y;
-    for (int i = 0; i < 128; ++i) {
-        const uint64_t bit = i < 64 ? (x.hi >> (63 - i)) & 1 : (x.lo >> (127 - i)) & 1;
-        if (bit) {
-            z.hi ^= v.hi;
-            z.lo ^= v.lo;
-        }
-        v = gf_mulx(v);
-    }
-    return z;
 }
 
 __device__ __forceinline__ uint8_t sbox_of(const uint32_t *t0, uint8_t x)
@@ -249,7 +222,7 @@ __global__ void keysetup_kernel(KeySlot *slots, uint32_t *basis, const uint8_t *
     uint4 *bs = reinterpret_cast<uint4 *>(basis) + (size_t)(first + k) * BASIS_VECS;
     for (int t = 0; t < NPOW; ++t) {
         if (t != 0)
-            p = gf_mul_slow(p, p);
+            p = gf_square(p);
         const V4 pr = u128_to_raw(p);
         slot->hpow[t][0] = pr.w0;
         slot->hpow[t][1] = pr.w1;
@@ -259,7 +232,7 @@ __global__ void keysetup_kernel(KeySlot *slots, uint32_t *basis, const uint8_t *
         for (int e = 0; e < 128; ++e) {
             const V4 br = u128_to_raw(b);
             bs[t * 128 + e] = make_uint4(br.w0, br.w1, br.w2, br.w3);
-            b = gf_mulx(b);
+            b = gf_mul_xpow(b, 1);
         }
     }
     /* H^1 .. H^128 (the sparse kernel's lane q multiplies its partial sum by H^(q+1); a two-wave single record element i
@@ -269,7 +242,7 @@ __global__ void keysetup_kernel(KeySlot *slots, uint32_t *basis, const uint8_t *
     for (int q = 0; q < LANE_POWS; ++q) {
         const V4 pr = u128_to_raw(pk);
         bs[NPOW * 128 + q] = make_uint4(pr.w0, pr.w1, pr.w2, pr.w3);
-        pk = gf_mul_slow(pk, hh);
+        pk = gf_mul_bitserial(pk, hh);
     }
 #if HYBRID
     /* round keys 1..rounds in the bit-sliced form of the batch kernel's hybrid waves (bs8_aes.h) */
@@ -278,14 +251,20 @@ __global__ void keysetup_kernel(KeySlot *slots, uint32_t *basis, const uint8_t *
 }
 
 /* The same outputs with one 64-lane wave per key slot, for a few slots at a time (picotls's setup_crypto keys ONE
- * context): keysetup_kernel does a slot's ~70 serial GF(2^128) multiplies and 896 basis vectors in one thread
- * (~540 us for a single slot); here every lane expands the key and squares H up to H^64 itself (no LDS, no
- * barrier), lane j then writes basis vectors e = j and j + 64 of every plane and the lane power H^(j+1) (at most
- * six multiplies of the squares), lane 0 the slot's round keys and powers. */
+ * context, so this is the latency of ptls_aead_new): every lane expands the key and squares H up to H^(2^(NPOW-1))
+ * itself (squaring is linear: a bit spread and one fold, gf128.h), lane j writes basis vectors e = j and j + 64 of
+ * every plane (P * x^e by one shift and fold each), the planes of H^1 .. H^64 go to LDS and become 4-bit window tables
+ * (32 positions x 16 values), and the lane powers H^(j+1), H^(j+65) are at most seven table products (32 lookups each)
+ * of the squares.  Round 3 did the squarings and products bit-serially (1 408 VALU each) and the basis by up to 127
+ * single shifts per vector: 75 us per slot. */
+constexpr int KS_TABS = 7; /* window tables of H^(2^t), t < 7: the factors of H^1 .. H^128 */
+
 __global__ void __launch_bounds__(64) keysetup_wide_kernel(KeySlot *slots, uint32_t *basis, const uint8_t *keys,
                                                            const uint8_t *ivs, uint32_t first, int key_size, const uint32_t *t0)
 {
-    static_assert(LANE_POWS == 128 && NPOW >= 7, "two lane powers per lane; H^(j+1), H^(j+65) from the squares H^(2^t), t < 7");
+    static_assert(LANE_POWS == 128 && NPOW >= KS_TABS, "two lane powers per lane; H^(j+1), H^(j+65) from the squares H^(2^t), t < 7");
+    __shared__ U128 planes[KS_TABS * 128];
+    __shared__ U128 tabs[KS_TABS * 32 * 16];
     const uint32_t k = blockIdx.x;
     const int j = (int)threadIdx.x;
     KeySlot *slot = slots + first + k;
@@ -293,45 +272,67 @@ __global__ void __launch_bounds__(64) keysetup_wide_kernel(KeySlot *slots, uint3
     uint32_t w[60];
     int rounds;
     const V4 h = expand_key_h(keys + (size_t)k * key_size, key_size, t0, w, rounds);
-    V4 pw[NPOW];
-    pw[0] = h;
+    U128 pw[NPOW];
+    pw[0] = u128_from_raw(h);
     for (int t = 1; t < NPOW; ++t)
-        pw[t] = gf_mul_valu(pw[t - 1], pw[t - 1]);
+        pw[t] = gf_square(pw[t - 1]);
     if (j == 0) {
         write_slot_keys(slot, w, rounds, ivs + 12 * (size_t)k);
         for (int t = 0; t < NPOW; ++t) {
-            slot->hpow[t][0] = pw[t].w0;
-            slot->hpow[t][1] = pw[t].w1;
-            slot->hpow[t][2] = pw[t].w2;
-            slot->hpow[t][3] = pw[t].w3;
+            const V4 r = u128_to_raw(pw[t]);
+            slot->hpow[t][0] = r.w0;
+            slot->hpow[t][1] = r.w1;
+            slot->hpow[t][2] = r.w2;
+            slot->hpow[t][3] = r.w3;
         }
 #if HYBRID
         bs8::slice_key(w, rounds, reinterpret_cast<uint32_t *>(bs + BS_KEY_OFF));
 #endif
     }
     for (int t = 0; t < NPOW; ++t) {
-        U128 b = u128_from_raw(pw[t]);
-        for (int e = 0; e < j; ++e)
-            b = gf_mulx(b);
-        V4 br = u128_to_raw(b);
-        bs[t * 128 + j] = make_uint4(br.w0, br.w1, br.w2, br.w3);
-        for (int e = 0; e < 64; ++e)
-            b = gf_mulx(b);
-        br = u128_to_raw(b);
-        bs[t * 128 + 64 + j] = make_uint4(br.w0, br.w1, br.w2, br.w3);
+        const U128 v0 = gf_mul_xpow(pw[t], j), v1 = gf_mul_xpow(v0, 64);
+        const V4 r0 = u128_to_raw(v0), r1 = u128_to_raw(v1);
+        bs[t * 128 + j] = make_uint4(r0.w0, r0.w1, r0.w2, r0.w3);
+        bs[t * 128 + 64 + j] = make_uint4(r1.w0, r1.w1, r1.w2, r1.w3);
+        if (t < KS_TABS) {
+            planes[t * 128 + j] = v0;
+            planes[t * 128 + 64 + j] = v1;
+        }
     }
+    __syncthreads();
+    /* table t, position p, value v = XOR of P * x^(4p + 3 - b) over the set bits b of v (gf128.h gf_nibble's order);
+     * lane j fills position j / 2, values 8 (j & 1) .. + 7 */
+    for (int t = 0; t < KS_TABS; ++t) {
+        const int p = j >> 1;
+        for (int v = 8 * (j & 1); v < 8 * (j & 1) + 8; ++v) {
+            U128 e{0, 0};
+            for (int b = 0; b < 4; ++b)
+                if ((v >> b) & 1)
+                    e = u128_xor(e, planes[t * 128 + 4 * p + 3 - b]);
+            tabs[(t * 32 + p) * 16 + v] = e;
+        }
+    }
+    __syncthreads();
+    auto mul_tab = [&](U128 a, int t) {
+        U128 z{0, 0};
+        for (int p = 0; p < 32; ++p)
+            z = u128_xor(z, tabs[(t * 32 + p) * 16 + gf_nibble(a, p)]);
+        return z;
+    };
     const int q1 = j + 1; /* 1 .. 64 */
-    V4 acc = V4{0, 0, 0, 0};
+    U128 acc{0, 0};
     bool any = false;
-    for (int t = 0; t < 7; ++t) {
+    for (int t = 0; t < KS_TABS; ++t) {
         if ((q1 >> t) & 1) {
-            acc = any ? gf_mul_valu(acc, pw[t]) : pw[t];
+            acc = any ? mul_tab(acc, t) : pw[t];
             any = true;
         }
     }
-    bs[NPOW * 128 + j] = make_uint4(acc.w0, acc.w1, acc.w2, acc.w3);
-    acc = gf_mul_valu(acc, pw[6]); /* H^(j + 65) = H^(j + 1) * H^64 */
-    bs[NPOW * 128 + 64 + j] = make_uint4(acc.w0, acc.w1, acc.w2, acc.w3);
+    V4 r = u128_to_raw(acc);
+    bs[NPOW * 128 + j] = make_uint4(r.w0, r.w1, r.w2, r.w3);
+    acc = mul_tab(acc, 6); /* H^(j + 65) = H^(j + 1) * H^64 */
+    r = u128_to_raw(acc);
+    bs[NPOW * 128 + 64 + j] = make_uint4(r.w0, r.w1, r.w2, r.w3);
 }
 
 /* ======================================================================================= *
