@@ -14,7 +14,9 @@ import threading
 import time
 
 import numpy as np
+import torch
 
+torch.zeros(1, device="cuda")  # torch's HIP runtime first (bench.py's order): initialised after the plugin's, it finds no GPU
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [os.path.join(ROOT, "tests"), os.path.join(ROOT, "hsig-picotls_amd"), ROOT]
 import ptls_hip  # noqa: E402
@@ -65,8 +67,6 @@ def traffic():
     while not stop.is_set():
         R.ref_ptlsbench_mt(hip_algo, 4, 500, 1500)
 
-
-import torch  # noqa: E402
 
 eng = ptls_hip.Engine(0)
 nrec, L = 65536, 16384
