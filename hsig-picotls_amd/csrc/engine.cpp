@@ -111,6 +111,87 @@ struct st_ptls_hip_engine_t {
     uint32_t *d_t0;
     uint32_t *d_queue;                /* QUEUE_SLOTS x {next chunk, workgroups done}: the batch kernel's chunk queues */
     std::atomic<uint32_t> queue_next; /* the slot the next batch launch takes */
+    hipStream_t util;                 /* descriptor / keyset allocation, zeroing and release (dev_alloc / dev_free) */
+};
+
+/* Device memory of keysets and batches.  hipFree synchronizes the whole device, so it would wait for a resident plugin
+ * worker (up to its lifetime) and for other threads' work; stream-ordered allocation on the engine's own stream does
+ * not (the objects' users are waited for through their launch events, Uses below).  hipMalloc where the runtime has no
+ * stream-ordered allocator. */
+static bool async_alloc_ok(void)
+{
+    static const bool ok = [] {
+        int dev = 0, v = 0;
+        return hipGetDevice(&dev) == hipSuccess && hipDeviceGetAttribute(&v, hipDeviceAttributeMemoryPoolsSupported, dev) == hipSuccess &&
+               v != 0;
+    }();
+    return ok;
+}
+
+static hipError_t dev_alloc(ptls_hip_engine_t *e, void **p, size_t bytes)
+{
+    *p = nullptr;
+    if (!async_alloc_ok())
+        return hipMalloc(p, bytes);
+    hipError_t r = hipMallocAsync(p, bytes, e->util);
+    if (r == hipSuccess)
+        r = hipStreamSynchronize(e->util); /* usable from any stream once the call returns */
+    return r;
+}
+
+static void dev_free(ptls_hip_engine_t *e, void *p)
+{
+    if (p == nullptr)
+        return;
+    if (!async_alloc_ok())
+        (void)hipFree(p);
+    else
+        (void)hipFreeAsync(p, e->util);
+}
+
+/* the streams launches on an object went to, each with an event recorded after its last such launch: freeing the object
+ * (or re-planning a batch) waits for exactly that work */
+struct Uses {
+    std::mutex mu;
+    std::vector<std::pair<hipStream_t, hipEvent_t>> v;
+
+    void note(void *stream)
+    {
+        hipStream_t st = static_cast<hipStream_t>(stream);
+        std::lock_guard<std::mutex> lk(mu);
+        for (auto &u : v)
+            if (u.first == st) {
+                (void)hipEventRecord(u.second, st);
+                return;
+            }
+        hipEvent_t ev = nullptr;
+        if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) == hipSuccess && hipEventRecord(ev, st) == hipSuccess)
+            v.emplace_back(st, ev);
+        else /* no event: the wait falls back to the whole device */
+            v.emplace_back(st, nullptr);
+    }
+
+    void wait()
+    {
+        std::lock_guard<std::mutex> lk(mu);
+        bool device_wide = false;
+        for (auto &u : v) {
+            if (u.second == nullptr) {
+                device_wide = true;
+                continue;
+            }
+            (void)hipEventSynchronize(u.second);
+        }
+        if (device_wide)
+            (void)hipDeviceSynchronize();
+    }
+
+    ~Uses()
+    {
+        for (auto &u : v)
+            if (u.second != nullptr)
+                (void)hipEventDestroy(u.second);
+    }
 };
 
 /* the chunk-queue words of one batch-kernel launch (batch_kernel.h QUEUE): zero when handed out, and the launch leaves
@@ -128,29 +209,14 @@ struct st_ptls_hip_keyset_t {
     uint32_t *d_basis;
     std::vector<uint8_t> ivs; /* host mirror of every slot's static IV (do_get_iv) */
     int64_t pool_id = -1;     /* >= 0: a plugin context's slot from the plugin pool (pool_keyset), not its own allocation */
-    /* the streams launches on this keyset went to, each with an event recorded after its last such launch: keyset_free
-     * waits for exactly that work */
-    std::mutex use_mu;
-    std::vector<std::pair<hipStream_t, hipEvent_t>> uses;
+    Uses uses; /* launches that read this keyset: keyset_free waits for exactly that work */
 };
 
 /* after a launch on `stream` that reads ks */
 static void keyset_note_use(ptls_hip_keyset_t *ks, void *stream)
 {
-    if (ks == nullptr || ks->pool_id >= 0)
-        return;
-    hipStream_t s = static_cast<hipStream_t>(stream);
-    std::lock_guard<std::mutex> lk(ks->use_mu);
-    for (auto &u : ks->uses)
-        if (u.first == s) {
-            (void)hipEventRecord(u.second, s);
-            return;
-        }
-    hipEvent_t ev = nullptr;
-    if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) == hipSuccess && hipEventRecord(ev, s) == hipSuccess)
-        ks->uses.emplace_back(s, ev);
-    else /* no event: keyset_free falls back to waiting for the device */
-        ks->uses.emplace_back(s, nullptr);
+    if (ks != nullptr && ks->pool_id < 0)
+        ks->uses.note(stream);
 }
 
 struct st_ptls_hip_batch_t {
@@ -173,6 +239,7 @@ struct st_ptls_hip_batch_t {
     uint32_t nsplit;  /* wave tasks the plan deals as two part tasks (split records) */
     uint64_t *d_clk;  /* diagnostic clock stamps of the next launches (ptls_hip_batch_set_clock), or nullptr */
     size_t clk_bytes;
+    Uses uses;        /* launches that read the descriptors and the plan: re-planning and batch_free wait for them */
 };
 
 /* CUs a batch is planned and launched for: the device's, or fewer when the batch caps its grid */
@@ -244,12 +311,16 @@ extern "C" ptls_hip_engine_t *ptls_hip_engine_new(int device)
     make_t0(t0);
     e->d_queue = nullptr;
     e->queue_next = 0;
+    e->util = nullptr;
     if (hipMalloc(&e->d_t0, sizeof(t0)) != hipSuccess || hipMemcpy(e->d_t0, t0, sizeof(t0), hipMemcpyHostToDevice) != hipSuccess ||
         hipMalloc(&e->d_queue, 2 * sizeof(uint32_t) * QUEUE_SLOTS) != hipSuccess ||
-        hipMemset(e->d_queue, 0, 2 * sizeof(uint32_t) * QUEUE_SLOTS) != hipSuccess) {
+        hipMemset(e->d_queue, 0, 2 * sizeof(uint32_t) * QUEUE_SLOTS) != hipSuccess ||
+        hipStreamCreateWithFlags(&e->util, hipStreamNonBlocking) != hipSuccess) {
         fail(PTLS_HIP_ENOMEM, "cannot allocate the AES table / chunk queues on device %d", device);
         (void)hipFree(e->d_t0);
         (void)hipFree(e->d_queue);
+        if (e->util != nullptr)
+            (void)hipStreamDestroy(e->util);
         delete e;
         return nullptr;
     }
@@ -267,6 +338,8 @@ extern "C" void ptls_hip_engine_free(ptls_hip_engine_t *e)
     if (e == nullptr)
         return;
     DeviceGuard g(e->device);
+    (void)hipStreamSynchronize(e->util);
+    (void)hipStreamDestroy(e->util);
     (void)hipFree(e->d_t0);
     (void)hipFree(e->d_queue);
     delete e;
@@ -300,14 +373,16 @@ extern "C" ptls_hip_keyset_t *ptls_hip_keyset_new(ptls_hip_engine_t *eng, size_t
     ks->key_size = key_size;
     ks->nslots = nslots;
     ks->ivs.assign(nslots * 12, 0);
-    if (hipMalloc(&ks->d_slots, nslots * sizeof(KeySlot)) != hipSuccess ||
-        hipMalloc(&ks->d_basis, nslots * BASIS_WORDS_PER_SLOT * 4) != hipSuccess) {
+    if (dev_alloc(eng, reinterpret_cast<void **>(&ks->d_slots), nslots * sizeof(KeySlot)) != hipSuccess ||
+        dev_alloc(eng, reinterpret_cast<void **>(&ks->d_basis), nslots * BASIS_WORDS_PER_SLOT * 4) != hipSuccess) {
         fail(PTLS_HIP_ENOMEM, "keyset_new: cannot allocate %zu key slots", nslots);
-        (void)hipFree(ks->d_slots);
+        dev_free(eng, ks->d_slots);
+        dev_free(eng, ks->d_basis);
         delete ks;
         return nullptr;
     }
-    (void)hipMemset(ks->d_slots, 0, nslots * sizeof(KeySlot));
+    (void)hipMemsetAsync(ks->d_slots, 0, nslots * sizeof(KeySlot), eng->util);
+    (void)hipStreamSynchronize(eng->util);
     return ks;
 }
 
@@ -326,27 +401,15 @@ extern "C" void ptls_hip_keyset_free(ptls_hip_keyset_t *ks)
     }
     /* the launches that read this keyset (keyset_note_use), not the whole device: a resident plugin worker or another
      * thread's batches are not waited for */
-    bool device_wide = false;
-    for (auto &u : ks->uses) {
-        if (u.second == nullptr) {
-            device_wide = true;
-            continue;
-        }
-        (void)hipEventSynchronize(u.second);
-        (void)hipEventDestroy(u.second);
-    }
-    ks->uses.clear();
-    if (device_wide)
-        (void)hipDeviceSynchronize();
-    /* zeroize key material before release (ptls_clear_memory in aesgcm_dispose_crypto, lib/fusion.c:1102-1107, :1042-1048) */
-    hipStream_t s = nullptr;
-    (void)hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
-    (void)hipMemsetAsync(ks->d_slots, 0, ks->nslots * sizeof(KeySlot), s);
-    (void)hipMemsetAsync(ks->d_basis, 0, ks->nslots * BASIS_WORDS_PER_SLOT * 4, s);
-    (void)hipStreamSynchronize(s);
-    (void)hipStreamDestroy(s);
-    (void)hipFree(ks->d_slots);
-    (void)hipFree(ks->d_basis);
+    ks->uses.wait();
+    /* zeroize key material before release (ptls_clear_memory in aesgcm_dispose_crypto, lib/fusion.c:1102-1107, :1042-1048),
+     * then release in the same stream order */
+    ptls_hip_engine_t *e = ks->eng;
+    (void)hipMemsetAsync(ks->d_slots, 0, ks->nslots * sizeof(KeySlot), e->util);
+    (void)hipMemsetAsync(ks->d_basis, 0, ks->nslots * BASIS_WORDS_PER_SLOT * 4, e->util);
+    dev_free(e, ks->d_slots);
+    dev_free(e, ks->d_basis);
+    (void)hipStreamSynchronize(e->util);
     std::fill(ks->ivs.begin(), ks->ivs.end(), 0);
     delete ks;
 }
@@ -729,12 +792,10 @@ static int plan_chunks(ptls_hip_batch_t *b)
     std::vector<uint32_t> order;
     build_chunks(b->h_recs.data(), b->n, b->lanes, batch_cus(b), ch, order, b->all_aligned);
     b->wg = b->forced_wg ? b->forced_wg : plan_wg(ch, b->lanes);
-    if (b->d_chunks != nullptr)
-        (void)hipFree(b->d_chunks);
-    if (b->d_order != nullptr)
-        (void)hipFree(b->d_order);
-    if (b->d_recs_ord != nullptr)
-        (void)hipFree(b->d_recs_ord);
+    b->uses.wait(); /* an earlier launch may still read the old plan */
+    dev_free(b->eng, b->d_chunks);
+    dev_free(b->eng, b->d_order);
+    dev_free(b->eng, b->d_recs_ord);
     b->d_chunks = nullptr;
     b->d_order = nullptr;
     b->d_recs_ord = nullptr;
@@ -744,16 +805,16 @@ static int plan_chunks(ptls_hip_batch_t *b)
         b->nsplit += (c.flags >> 8) & 0xffu;
     if (ch.empty())
         return 0;
-    HIP_TRY(hipMalloc(&b->d_chunks, ch.size() * sizeof(Chunk)), PTLS_HIP_ENOMEM);
+    HIP_TRY(dev_alloc(b->eng, reinterpret_cast<void **>(&b->d_chunks), ch.size() * sizeof(Chunk)), PTLS_HIP_ENOMEM);
     HIP_TRY(hipMemcpy(b->d_chunks, ch.data(), ch.size() * sizeof(Chunk), hipMemcpyHostToDevice), PTLS_HIP_ENODEV);
     if (identity_order(order, order.size()))
         return 0; /* d_order and d_recs_ord stay null: run_batch passes d_recs and no order */
-    HIP_TRY(hipMalloc(&b->d_order, order.size() * sizeof(uint32_t)), PTLS_HIP_ENOMEM);
+    HIP_TRY(dev_alloc(b->eng, reinterpret_cast<void **>(&b->d_order), order.size() * sizeof(uint32_t)), PTLS_HIP_ENOMEM);
     HIP_TRY(hipMemcpy(b->d_order, order.data(), order.size() * sizeof(uint32_t), hipMemcpyHostToDevice), PTLS_HIP_ENODEV);
     std::vector<ptls_hip_record_t> ord(order.size());
     for (size_t k = 0; k < order.size(); ++k)
         ord[k] = b->h_recs[order[k]];
-    HIP_TRY(hipMalloc(&b->d_recs_ord, ord.size() * sizeof(ptls_hip_record_t)), PTLS_HIP_ENOMEM);
+    HIP_TRY(dev_alloc(b->eng, reinterpret_cast<void **>(&b->d_recs_ord), ord.size() * sizeof(ptls_hip_record_t)), PTLS_HIP_ENOMEM);
     HIP_TRY(hipMemcpy(b->d_recs_ord, ord.data(), ord.size() * sizeof(ptls_hip_record_t), hipMemcpyHostToDevice), PTLS_HIP_ENODEV);
     return 0;
 }
@@ -775,10 +836,11 @@ extern "C" ptls_hip_batch_t *ptls_hip_batch_new(ptls_hip_engine_t *eng, const pt
         b->max_key = std::max(b->max_key, recs[i].key);
     b->auto_lanes = b->lanes = choose_lanes(b->h_recs.data(), b->h_recs.size());
     if (n != 0) {
-        if (hipMalloc(&b->d_recs, n * sizeof(ptls_hip_record_t)) != hipSuccess ||
+        if (dev_alloc(eng, reinterpret_cast<void **>(&b->d_recs), n * sizeof(ptls_hip_record_t)) != hipSuccess ||
             hipMemcpy(b->d_recs, recs, n * sizeof(ptls_hip_record_t), hipMemcpyHostToDevice) != hipSuccess) {
             fail(PTLS_HIP_ENOMEM, "batch_new: cannot upload %zu descriptors", n);
-            (void)hipFree(b->d_recs);
+            dev_free(eng, b->d_recs);
+            (void)hipStreamSynchronize(eng->util);
             delete b;
             return nullptr;
         }
@@ -795,10 +857,12 @@ extern "C" void ptls_hip_batch_free(ptls_hip_batch_t *b)
     if (b == nullptr)
         return;
     DeviceGuard g(b->eng->device);
-    (void)hipFree(b->d_recs);
-    (void)hipFree(b->d_recs_ord);
-    (void)hipFree(b->d_chunks);
-    (void)hipFree(b->d_order);
+    b->uses.wait();
+    dev_free(b->eng, b->d_recs);
+    dev_free(b->eng, b->d_recs_ord);
+    dev_free(b->eng, b->d_chunks);
+    dev_free(b->eng, b->d_order);
+    (void)hipStreamSynchronize(b->eng->util);
     delete b;
 }
 
@@ -916,6 +980,7 @@ static int run_batch(ptls_hip_batch_t *b, ptls_hip_keyset_t *ks, const void *in,
         return fail(PTLS_HIP_ELAUNCH, "kernel launch failed: %s", hipGetErrorString((hipError_t)e));
     keyset_note_use(ks, stream);
     keyset_note_use(hp_ks, stream);
+    b->uses.note(stream);
     return 0;
 }
 
@@ -1080,6 +1145,7 @@ extern "C" int ptls_hip_fill_records(ptls_hip_batch_t *b, void *buf, uint64_t se
     int e = launch_fill(b->d_recs, (uint32_t)b->n, static_cast<uint8_t *>(buf), seed, index_base, index, grid, stream);
     if (e != 0)
         return fail(PTLS_HIP_ELAUNCH, "fill launch failed: %s", hipGetErrorString((hipError_t)e));
+    b->uses.note(stream);
     return 0;
 }
 
@@ -2183,7 +2249,16 @@ static unsigned staging_flags(void);
  * when asked; a call that finds its workgroup gone waits for the whole dispatch to drain and launches the next one.
  * On by default; PTLS_HIP_PLUGIN_WORKER=0 (environment) makes every call launch its own kernel instead;
  * PTLS_HIP_PLUGIN_WORKERS=n sets the number of mailboxes / workgroups (default 8, 1..64). */
-static const uint64_t WORKER_IDLE_US = 200, WORKER_LIFE_US = 2000;
+static uint64_t worker_env_us(const char *name, uint64_t dflt)
+{
+    const char *e = getenv(name);
+    const long long v = e != nullptr ? atoll(e) : -1;
+    return v > 0 ? (uint64_t)v : dflt;
+}
+/* PTLS_HIP_WORKER_IDLE_US / PTLS_HIP_WORKER_LIFE_US (environment) override: a hipFree anywhere in the process synchronizes
+ * the device and so waits for a resident dispatch, at most the lifetime */
+static const uint64_t WORKER_IDLE_US = worker_env_us("PTLS_HIP_WORKER_IDLE_US", 200),
+                      WORKER_LIFE_US = worker_env_us("PTLS_HIP_WORKER_LIFE_US", 2000);
 static const unsigned WORKER_MAX = 64;
 
 struct Mailbox {
