@@ -93,6 +93,11 @@ __host__ __device__ constexpr uint32_t lds_bytes(int log2g)
 #define CHUNK_QUEUE 1 /* workgroups take their chunks after the first from a device-wide queue (one returning atomic add per
                          chunk) instead of the static grid stride blockIdx.x + k * gridDim.x */
 #endif
+#ifndef KS_STAMPS
+#define KS_STAMPS 0 /* DIAGNOSTIC builds only (tools/keyswitch_stamps.py): every wave sums the shader cycles it spends at key
+                       switches (first barrier, table build, second barrier) and in total, into clk after the 4 x grid
+                       workgroup stamps: [workgroup][wave][total, barrier 1, build, barrier 2, switches] */
+#endif
 /* the chunk sequence a workgroup's waves walk: a ring in LDS of {sequence number, chunk} entries */
 constexpr int QRING = 32;
 constexpr uint32_t Q_END = 0xffffffffu;
@@ -1339,6 +1344,8 @@ __global__ void __launch_bounds__(WGT)
 
     clock_stamp(clk, 0);
     build_aes_tables<WGT>(lds, LDS_AES, t0);
+    uint64_t ks_acc[5] = {0, 0, 0, 0, 0}; /* KS_STAMPS: total, barrier 1, build, barrier 2, switches */
+    const uint64_t ks_t0 = KS_STAMPS ? __builtin_amdgcn_s_memtime() : 0;
     uint32_t cur_key = 0xffffffffu;
     /* DYN: g = the wave's next task in the workgroup's same-key run of chunks (drawn, not yet used);
      * cbase = tasks of the run's chunks before the current one; sbase = split tasks of those chunks (slot numbering) */
@@ -1352,7 +1359,9 @@ __global__ void __launch_bounds__(WGT)
              * and the waves' cursors run on across keys as across the chunks of one key run */
             cur_key = ch.key;
         } else if (SPLIT_PROBE != 1 && ch.key != cur_key) {
+            const uint64_t s0 = KS_STAMPS ? __builtin_amdgcn_s_memtime() : 0;
             __syncthreads();
+            const uint64_t s1 = KS_STAMPS ? __builtin_amdgcn_s_memtime() : 0;
             if (KEYSWITCH_PROBE != 1 || cur_key == 0xffffffffu)
                 build_ghash_tables(lds, basis + (size_t)ch.key * (BASIS_VECS * 4), LOG2G, !(VALU_TREE != 0 || G >= 32), WINCOMB);
             if (DYN && threadIdx.x == 0)
@@ -1360,7 +1369,17 @@ __global__ void __launch_bounds__(WGT)
             if (SPLIT)
                 for (int k = (int)threadIdx.x; k < SPLIT_SLOTS; k += WGT)
                     reinterpret_cast<uint32_t *>(lds + LDS_SPLIT_CTR)[k] = 0;
+            if (KS_STAMPS)
+                __builtin_amdgcn_s_waitcnt(0); /* the wave's own table stores are done: what remains is waiting for others */
+            const uint64_t s2 = KS_STAMPS ? __builtin_amdgcn_s_memtime() : 0;
             __syncthreads();
+            if (KS_STAMPS) {
+                const uint64_t s3 = __builtin_amdgcn_s_memtime();
+                ks_acc[1] += s1 - s0;
+                ks_acc[2] += s2 - s1;
+                ks_acc[3] += s3 - s2;
+                ks_acc[4] += 1;
+            }
             cur_key = ch.key;
             cbase = 0;
             sbase = 0;
@@ -1781,6 +1800,12 @@ __global__ void __launch_bounds__(WGT)
         if (DEAL_MUTANT != 2)
             cbase += (uint32_t)ntasks;
         sbase += (uint32_t)nsplit;
+    }
+    if (KS_STAMPS && clk != nullptr) {
+        ks_acc[0] = __builtin_amdgcn_s_memtime() - ks_t0;
+        uint64_t *o = clk + 4 * (size_t)gridDim.x + 5 * ((size_t)blockIdx.x * NW + (size_t)wave);
+        if (lane < 5)
+            o[lane] = lane == 0 ? ks_acc[0] : lane == 1 ? ks_acc[1] : lane == 2 ? ks_acc[2] : lane == 3 ? ks_acc[3] : ks_acc[4];
     }
     if (clk != nullptr) { /* the workgroup's end: after its last wave */
         __syncthreads();

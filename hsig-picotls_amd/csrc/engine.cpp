@@ -128,6 +128,20 @@ static bool async_alloc_ok(void)
     return ok;
 }
 
+/* the device's default pool keeps what is freed into it (release threshold: never): otherwise every stream-ordered free
+ * returns memory to the driver at the next synchronization and the next allocation maps it again, which waits for the
+ * device like hipMalloc / hipFree do */
+static void pool_keep_memory(int device)
+{
+    if (!async_alloc_ok())
+        return;
+    hipMemPool_t pool = nullptr;
+    uint64_t keep = UINT64_MAX;
+    if (hipDeviceGetDefaultMemPool(&pool, device) == hipSuccess)
+        (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep);
+    (void)hipGetLastError();
+}
+
 static hipError_t dev_alloc(ptls_hip_engine_t *e, void **p, size_t bytes)
 {
     *p = nullptr;
@@ -324,6 +338,7 @@ extern "C" ptls_hip_engine_t *ptls_hip_engine_new(int device)
         delete e;
         return nullptr;
     }
+    pool_keep_memory(device);
     if (engine_self_check(e) != 0) {
         const std::string why = g_err;
         ptls_hip_engine_free(e);
@@ -2248,7 +2263,8 @@ static unsigned staging_flags(void);
  * without a request on any of them, after WORKER_LIFE_US in any case (the dispatch must not hold its hardware queue), or
  * when asked; a call that finds its workgroup gone waits for the whole dispatch to drain and launches the next one.
  * On by default; PTLS_HIP_PLUGIN_WORKER=0 (environment) makes every call launch its own kernel instead;
- * PTLS_HIP_PLUGIN_WORKERS=n sets the number of mailboxes / workgroups (default 8, 1..64). */
+ * PTLS_HIP_PLUGIN_WORKERS=n sets the number of mailboxes / workgroups (default 16, 1..64: 16 threads measured 13.6x one
+ * thread's calls per second, tools/plugin_mt.py; the dispatch holds that many CUs while it is resident). */
 static uint64_t worker_env_us(const char *name, uint64_t dflt)
 {
     const char *e = getenv(name);
@@ -2294,7 +2310,7 @@ static unsigned worker_count(void)
 {
     static const unsigned n = [] {
         const char *e = getenv("PTLS_HIP_PLUGIN_WORKERS");
-        const int v = e != nullptr ? atoi(e) : 8;
+        const int v = e != nullptr ? atoi(e) : 16;
         return (unsigned)std::max(1, std::min(v, (int)WORKER_MAX));
     }();
     return n;

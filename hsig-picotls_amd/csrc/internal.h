@@ -20,7 +20,8 @@
  * measurement switches that stay bit-exact (VALU_TREE, HYBRID, GEN_MASK, ...) are tested as alternate builds. */
 #if defined(PTLS_HIP_PRODUCT)
 #if (defined(CTRHI_PROBE) && CTRHI_PROBE) || (defined(SPLIT_PROBE) && SPLIT_PROBE) || (defined(KEYSWITCH_PROBE) && KEYSWITCH_PROBE) || \
-    (defined(DEAL_MUTANT) && DEAL_MUTANT) || (defined(SPARSE_ABLATE) && SPARSE_ABLATE) || (defined(PLUGIN_PROBE) && PLUGIN_PROBE)
+    (defined(DEAL_MUTANT) && DEAL_MUTANT) || (defined(SPARSE_ABLATE) && SPARSE_ABLATE) || (defined(PLUGIN_PROBE) && PLUGIN_PROBE) || \
+    (defined(KS_STAMPS) && KS_STAMPS)
 #error "libptls_hip.so is built with a timing-probe, ablation or test-mutant switch set: such builds compute wrong output"
 #endif
 #endif

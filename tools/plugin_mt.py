@@ -30,7 +30,7 @@ R.ref_aead_lifecycle.restype = c.c_int
 R.ref_aead_lifecycle.argtypes = [c.c_void_p, c.c_size_t, c.c_size_t] + [c.POINTER(c.c_double)] * 3
 hip_algo = c.addressof(c.c_char.in_dll(ptls_hip.lib(), "ptls_hip_aes128gcm"))
 fus_algo = Ref().algo("ptls_fusion_aes128gcm")
-out = {"workers": int(os.environ.get("PTLS_HIP_PLUGIN_WORKERS", "8")),
+out = {"workers": int(os.environ.get("PTLS_HIP_PLUGIN_WORKERS", "16")),
        "worker": os.environ.get("PTLS_HIP_PLUGIN_WORKER", "1")}
 
 
