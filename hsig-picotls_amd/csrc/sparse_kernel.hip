@@ -834,6 +834,22 @@ __device__ __forceinline__ T *as_global(T *p)
     asm volatile("" : "+v"(v)); /* an opaque integer: the global pointer made from it cannot be folded back to a flat one */
     return (T *)((__attribute__((address_space(1))) T *)v);
 }
+/* WORKER_CONST (measurement switch, DESIGN.md §4.7 "worker key loads"): the key slot and basis pointers of a request are
+ * constant-address-space pointers, so the round keys come through the scalar unit (s_load) as in a launched kernel.  Valid
+ * because a slot the resident dispatch may have read never changes while it is resident (engine.cpp slot pool: a freed
+ * slot is reused only after that dispatch has left; the IV travels in the request).  The round-3 build of this faulted;
+ * that build also had 36 B of scratch in the worker (tests/test_kernel_resources.py keeps it at 0). */
+#ifndef WORKER_CONST
+#define WORKER_CONST 0
+#endif
+template <typename T>
+__device__ __forceinline__ const T *as_const(const T *p)
+{
+    uint64_t v = (uint64_t)(uintptr_t)p;
+    asm volatile("" : "+v"(v));
+    v = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32)) << 32) | __builtin_amdgcn_readfirstlane((uint32_t)v);
+    return (const T *)((const __attribute__((address_space(4))) T *)v);
+}
 #ifndef WORKER_STAMPS
 #define WORKER_STAMPS 0 /* diagnostic builds only (Makefile `diag`, tools/worker_stamps.py): the worker stamps the 100 MHz counter
                            at its phase boundaries into WorkerSlot::stamps (seen, request read, record done, released) */
@@ -943,14 +959,14 @@ __global__ void __launch_bounds__(WORKER_WG)
         const uint4 ivo = (flags & WREQ_IV) ? uint4{rq.iv[0], rq.iv[1], rq.iv[2], 1u} : uint4{0, 0, 0, 0};
         const uint8_t *in = as_global(rq.in), *aad = as_global(rq.aad);
         uint8_t *out = as_global(rq.out);
-        const KeySlot *slots = as_global(rq.slots);
+        const KeySlot *slots = WORKER_CONST ? as_const(rq.slots) : as_global(rq.slots);
         uint32_t *done = as_global(rq.done);
         const uint32_t done_seq = __builtin_amdgcn_readfirstlane(rq.done_seq);
         const ptls_hip_supp_t *supp = rq.supp != nullptr ? as_global(rq.supp) : nullptr;
         const KeySlot *hp_slots = rq.hp_slots != nullptr ? as_global(rq.hp_slots) : nullptr;
         uint8_t *mask = rq.mask != nullptr ? as_global(rq.mask) : nullptr;
         uint64_t *result = as_global(rq.result);
-        const uint32_t *basis = as_global(rq.basis);
+        const uint32_t *basis = WORKER_CONST ? as_const(rq.basis) : as_global(rq.basis);
         const bool open = (flags & WREQ_OPEN) != 0, a256 = (flags & WREQ_AES256) != 0;
         const int na1 = ((int)rec.aad_len + 15) >> 4, nc1 = ((int)rec.len + 15) >> 4;
         const int n1 = na1 + nc1 + 1;
