@@ -2732,11 +2732,45 @@ static const hip_ctr_state *ctr_state_of(const ptls_cipher_context_t *c)
 static const size_t ECB_DONE = 64;
 
 /* one AES-ECB block on the device with the state's key (fusion: aesecb_encrypt, lib/fusion.c:322-334) */
+static bool ecb_by_launch(void)
+{
+    static const bool on = [] { /* PTLS_HIP_ECB_LAUNCH=1 (environment): one launch per block even with the worker (A/B) */
+        const char *e = getenv("PTLS_HIP_ECB_LAUNCH");
+        return e != nullptr && atoi(e) != 0;
+    }();
+    return on;
+}
+
 static void ecb_block(hip_ctr_state *st, const void *src, uint8_t dst[16])
 {
     DeviceGuard g(st->eng->device);
-    /* one launch per block even with the plugin worker resident: measured faster than a worker request (9.5 against
-     * 11.2 us per block): the kernel's block travels in its arguments, while a request adds a PCIe read of the mailbox */
+    if (worker_enabled() && !ecb_by_launch()) {
+        /* through the worker: the block travels in the mailbox with the request (WREQ_ECB) */
+        PluginWorker &w = g_worker;
+        if (w.h_mb == nullptr) {
+            std::lock_guard<std::mutex> lk(w.launch_mu);
+            worker_init(w, st->eng);
+        }
+        const unsigned j = worker_acquire(w);
+        WorkerSlot *h = &w.h_mb[j], *d = &w.d_mb[j];
+        std::memcpy(h->data, src, 16);
+        WorkerReq rq{};
+        rq.in = rq.aad = d->data;
+        rq.out = d->out;
+        rq.result = reinterpret_cast<uint64_t *>(d->aux + WAUX_RESULT);
+        rq.slots = st->ks->d_slots;
+        rq.basis = st->ks->d_basis;
+        rq.done = reinterpret_cast<uint32_t *>(d->aux + WAUX_DONE);
+        rq.done_seq = ++w.mbox[j].done_seq;
+        rq.flags = WREQ_ECB | WREQ_INLINE | (st->ks->key_size == 32 ? WREQ_AES256 : 0u);
+        worker_call(j, rq, h->aux + WAUX_DONE);
+        std::memcpy(dst, h->out, 16);
+        std::memset(h->out, 0, 16);
+        std::memset(h->data, 0, 16);
+        w.mbox[j].mu.unlock();
+        return;
+    }
+    /* one launch per block (worker off, or PTLS_HIP_ECB_LAUNCH=1): the block travels in the kernel arguments */
     /* the block goes in the kernel arguments; the result comes back through the pinned staging (@48) */
     hipStream_t stream = pool_stream();
     const int e = launch_aesecb_one(st->ks->key_size == 16 ? 10 : 14, static_cast<const uint8_t *>(src), st->ks->d_slots,

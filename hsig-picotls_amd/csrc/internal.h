@@ -141,7 +141,9 @@ constexpr uint32_t QUEUE_SLOTS = 4096;
  * the plugin's single-record calls from their own mailbox in fine-grained pinned host memory instead of one kernel launch
  * per call.  The host writes the request, then (release) seq; the workgroup serves it, stores the call's completion word
  * (as a launched call's kernel does), then `served`. */
-enum : uint32_t { WREQ_OPEN = 1, WREQ_AES256 = 2, WREQ_INLINE = 8, WREQ_IV = 16 };
+enum : uint32_t { WREQ_OPEN = 1, WREQ_AES256 = 2, WREQ_INLINE = 8, WREQ_IV = 16, WREQ_ECB = 32 };
+/* WREQ_ECB: one AES block (ptls_hip_aes*ctr's do_init, the fusion-style ECB API) with the request's key slot: input block at
+ * data[0..16), output at out[0..16) */
 /* WREQ_IV: the nonce's static IV is the request's iv[] (the context's current IV), not the key slot's: an IV change
  * (ptls_aead_set_iv / xor_iv) stays on the host. */
 /* WREQ_INLINE: the record sits in the mailbox's data area (AAD padded to 16 bytes, then the input: element i of the GHASH

@@ -847,7 +847,10 @@ __device__ __forceinline__ const T *as_const(const T *p)
 {
     uint64_t v = (uint64_t)(uintptr_t)p;
     asm volatile("" : "+v"(v));
-    v = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32)) << 32) | __builtin_amdgcn_readfirstlane((uint32_t)v);
+    /* __builtin_amdgcn_readfirstlane returns int: each half goes through uint32_t, or an address with bit 31 set would
+     * sign-extend over the high half (the fault of this call's first version, tools/calls_r04/r04_call7.sh) */
+    v = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32)) << 32) |
+        (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)v);
     return (const T *)((const __attribute__((address_space(4))) T *)v);
 }
 #ifndef WORKER_STAMPS
@@ -916,8 +919,9 @@ __global__ void __launch_bounds__(WORKER_WG)
                         /* idle here: the workgroups of the dispatch leave together, when none of them has served a request
                          * for idle_ticks (the last one served is in `activity`), so a caller rarely finds its own
                          * workgroup gone while the others still hold the dispatch */
-                        const uint64_t a = __builtin_amdgcn_readfirstlane(
-                            __hip_atomic_load(activity, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+                        const uint64_t av = __hip_atomic_load(activity, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        const uint64_t a = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(av >> 32)) << 32) |
+                                           (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)av);
                         t_last = a > t_last ? a : t_last;
                     }
                     if (seq == last && (quit != 0 || now - t_last > idle_ticks || now - t_start > life_ticks))
@@ -970,8 +974,9 @@ __global__ void __launch_bounds__(WORKER_WG)
         const bool open = (flags & WREQ_OPEN) != 0, a256 = (flags & WREQ_AES256) != 0;
         const int na1 = ((int)rec.aad_len + 15) >> 4, nc1 = ((int)rec.len + 15) >> 4;
         const int n1 = na1 + nc1 + 1;
-        const bool mw = n1 >= MW_MIN_N && n1 <= MW_MAX_N;
-        const bool longrec = n1 > MW_MAX_N; /* both waves at stride 128 (sparse_record S = 128) */
+        const bool ecb = (flags & WREQ_ECB) != 0;
+        const bool mw = !ecb && n1 >= MW_MIN_N && n1 <= MW_MAX_N;
+        const bool longrec = !ecb && n1 > MW_MAX_N; /* both waves at stride 128 (sparse_record S = 128) */
         if (WORKER_STAMPS)
             st[2] = worker_stamp();
         /* WORKER_STAMPS builds (with STAMP_PHASES): the record's phase stamps (shader cycles) go to the end of the data area,
@@ -991,7 +996,16 @@ __global__ void __launch_bounds__(WORKER_WG)
                 v = load_full(in + rec.in_off + 16 * (size_t)(i - na1));
             return v;
         };
-        if (longrec) {
+        if (ecb) {
+            /* one block with the slot's round keys (the block was read with the request: pin[0], lane 0's element) */
+            if (wave == 0) {
+                const V4 blk = V4{(uint32_t)__builtin_amdgcn_readfirstlane(pin[0].w0), (uint32_t)__builtin_amdgcn_readfirstlane(pin[0].w1),
+                                  (uint32_t)__builtin_amdgcn_readfirstlane(pin[0].w2), (uint32_t)__builtin_amdgcn_readfirstlane(pin[0].w3)};
+                const V4 m = a256 ? aes_encrypt<14>(lds, lb_aes, slots->rk, blk) : aes_encrypt<10>(lds, lb_aes, slots->rk, blk);
+                if (lane == 0)
+                    store_full(out, m);
+            }
+        } else if (longrec) {
             V4 p2[2];
             if (flags & WREQ_INLINE) {
                 p2[0] = pin[0];
