@@ -834,13 +834,15 @@ __device__ __forceinline__ T *as_global(T *p)
     asm volatile("" : "+v"(v)); /* an opaque integer: the global pointer made from it cannot be folded back to a flat one */
     return (T *)((__attribute__((address_space(1))) T *)v);
 }
-/* WORKER_CONST (measurement switch, DESIGN.md §4.7 "worker key loads"): the key slot and basis pointers of a request are
- * constant-address-space pointers, so the round keys come through the scalar unit (s_load) as in a launched kernel.  Valid
- * because a slot the resident dispatch may have read never changes while it is resident (engine.cpp slot pool: a freed
- * slot is reused only after that dispatch has left; the IV travels in the request).  The round-3 build of this faulted;
- * that build also had 36 B of scratch in the worker (tests/test_kernel_resources.py keeps it at 0). */
+/* WORKER_CONST: the key slot and basis pointers of a request are constant-address-space pointers, so the round keys come
+ * through the scalar unit (s_load) as in a launched kernel (16 KiB record 28 -> 24 us per call, one ECB block 10.1 ->
+ * 9.3 us; tools/calls_r04/r04_call8.sh).  Valid because a slot the resident dispatch may have read never changes while it
+ * is resident (engine.cpp slot pool: a freed slot is reused only after that dispatch has left; the IV travels in the
+ * request).  The round-3 attempt faulted, and so did this one's first build (r04_call7.sh): both rebuilt the 64-bit
+ * pointer from two readfirstlane results, which return int, so an address with bit 31 set sign-extended over the high
+ * half (s_bfe_i64 in the disassembly); as_const widens each half through uint32_t. */
 #ifndef WORKER_CONST
-#define WORKER_CONST 0
+#define WORKER_CONST 1
 #endif
 template <typename T>
 __device__ __forceinline__ const T *as_const(const T *p)
