@@ -40,6 +40,9 @@ namespace ptls_hip {
 #ifndef PLUGIN_PROBE
 #define PLUGIN_PROBE 0 /* timing probe only (wrong output): 1 = no AES table build */
 #endif
+#ifndef SPARSE_QUEUE
+#define SPARSE_QUEUE 1 /* waves claim records from the launch's queue word (greedy, longest first) instead of a static stride */
+#endif
 #ifndef SPARSE_PE
 #define SPARSE_PE 2 /* GHASH elements (AES blocks) per lane per main-loop iteration */
 #endif
@@ -644,7 +647,7 @@ __global__ void __launch_bounds__(WG)
                          uint8_t *out, uint64_t *__restrict__ result, const KeySlot *__restrict__ slots,
                          const uint32_t *__restrict__ basis, const uint32_t *__restrict__ t0, const ptls_hip_supp_t *__restrict__ supp,
                          const KeySlot *__restrict__ hp_slots, uint32_t hp_nslots, uint8_t *mask, ptls_hip_record_t one,
-                         uint32_t *done, uint32_t done_seq, uint64_t *__restrict__ clk)
+                         uint32_t *done, uint32_t done_seq, uint64_t *__restrict__ clk, uint32_t *queue)
 {
     /* BYVAL: 16 KiB more for wave 1's windowed table of a two-wave record (mw_record, or a long record at stride 128),
      * then 2 KiB for wave 1's prefetched elements of a long record and 64 B for the waves' hand-over */
@@ -774,14 +777,34 @@ __global__ void __launch_bounds__(WG)
     }
     const uint32_t waves = gridDim.x * (WG / 64);
     const uint32_t w0 = __builtin_amdgcn_readfirstlane(blockIdx.x * (WG / 64) + (threadIdx.x >> 6));
-
-    for (uint32_t pos = w0; pos < nrecs; pos += waves) {
+    /* SPARSE_QUEUE: every wave claims its next record from the launch's queue word (records sorted by decreasing length,
+     * so the longest go first: a greedy longest-first deal) instead of the static stride w0 + k * waves, whose fixed share
+     * leaves the slowest waves (the youngest on each SIMD, the CUs of the slowest XCD) on the critical path.  The claim
+     * for the next record is issued when a record starts, so its latency runs under the record.  The last wave to claim
+     * past the end resets the words (engine.cpp queue_slot). */
+    const bool dyn = SPARSE_QUEUE && !by_value && queue != nullptr;
+    auto claim = [&]() -> uint32_t { /* lane 0's returned value; read (readfirstlane) only when it is needed */
+        uint32_t v = 0;
+        if (lane == 0)
+            v = __hip_atomic_fetch_add(queue, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return v;
+    };
+    uint32_t pos = dyn ? (uint32_t)__builtin_amdgcn_readfirstlane(claim()) : w0;
+    while (pos < nrecs) {
+        const uint32_t next_v = dyn ? claim() : 0u;
         phase_acc(pa, bstamps, 1);
         const ptls_hip_record_t rec = by_value ? one : recs_ord[pos];
         const uint32_t rec_i = by_value ? 0u : order != nullptr ? order[pos] : pos;
         /* a single record's wave 0 takes the unused table areas of waves 1 and 2 for its lane-combination table */
         sparse_record<ROUNDS, OPEN, ALIGNED, BYVAL>(lds, lane, lb_aes, tab, rec, rec_i, in, aad, out, result, slots, basis, supp,
                                                    hp_slots, hp_nslots, mask, prefetch, pre, clk, stamps, bstamps, pa, SP_TAB + 8192u);
+        pos = dyn ? (uint32_t)__builtin_amdgcn_readfirstlane(next_v) : pos + waves;
+    }
+    if (dyn && lane == 0 &&
+        __hip_atomic_fetch_add(queue + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == waves - 1) {
+        /* every wave has claimed past the end: no more adds to either word in this launch */
+        __hip_atomic_store(queue, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(queue + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     if (done != nullptr && w0 == 0) {
         /* the by-value record's wave: every store above (the whole wave's, s_waitcnt is wave-wide) reaches system
@@ -1113,11 +1136,11 @@ static hipError_t launch_sparse_bv(unsigned grid, hipStream_t s, const KernelArg
     if (aligned)
         hipLaunchKernelGGL((aesgcm_sparse_kernel<R, O, true, BV>), dim3(grid), dim3(BV ? BYVAL_WG : SPARSE_WG), 0, s, a.recs_ord, a.order, a.chunks,
                            a.nchunks, a.in, a.aad, a.out, a.result, a.slots, a.basis, a.t0, a.supp, a.hp_slots, a.hp_nslots, a.mask, a.one,
-                           a.done, a.done_seq, a.clk);
+                           a.done, a.done_seq, a.clk, a.queue);
     else
         hipLaunchKernelGGL((aesgcm_sparse_kernel<R, O, false, BV>), dim3(grid), dim3(BV ? BYVAL_WG : SPARSE_WG), 0, s, a.recs_ord, a.order, a.chunks,
                            a.nchunks, a.in, a.aad, a.out, a.result, a.slots, a.basis, a.t0, a.supp, a.hp_slots, a.hp_nslots, a.mask, a.one,
-                           a.done, a.done_seq, a.clk);
+                           a.done, a.done_seq, a.clk, a.queue);
     return hipGetLastError();
 }
 

@@ -6,6 +6,9 @@ tag=${1:-r02}; shift || true
 cfgs=${*:-c2 c3 c4 c4s}
 for c in $cfgs; do
   cp gpurun_out/prof_${tag}_$c/trace/run_kernel_stats.csv profiles/${tag}_${c}_kernel_stats.csv
+  # per-launch seal / open durations of the batch kernels, the engine self-check dispatches dropped (rocprofv3's stats
+  # average them in), from the very trace the stats came from
+  python3 tools/trace_summary.py gpurun_out/prof_${tag}_$c/trace/run_kernel_trace.csv > profiles/${tag}_${c}_kernel_trace_summary.json
   cp gpurun_out/prof_${tag}_$c/traffic_$c.json profiles/traffic_$c.json
   cp gpurun_out/pmc_$c/lds_$c.json profiles/lds_$c.json
   cp gpurun_out/pmc_$c/summary.txt profiles/${tag}_${c}_pmc_sq_summary.txt
