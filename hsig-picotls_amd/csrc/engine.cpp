@@ -2365,7 +2365,13 @@ static void worker_init(PluginWorker &w, ptls_hip_engine_t *eng)
     const unsigned n = worker_count();
     void *d = nullptr;
     WorkerSlot *h = nullptr;
-    if (hipStreamCreateWithFlags(&w.stream, hipStreamNonBlocking) != hipSuccess ||
+    /* the dispatch's stream at the device's greatest priority: the runtime gives each priority its own pool of hardware
+     * queues (GPU_MAX_HW_QUEUES each), so no other stream of the process shares the worker's queue and waits behind the
+     * resident dispatch (a key setup on a pooled stream that did: ptls_aead_new 244 us = the worker's idle exit + 44) */
+    int prio_least = 0, prio_greatest = 0;
+    if (hipDeviceGetStreamPriorityRange(&prio_least, &prio_greatest) != hipSuccess)
+        prio_greatest = prio_least = 0;
+    if (hipStreamCreateWithPriority(&w.stream, hipStreamNonBlocking, prio_greatest) != hipSuccess ||
         hipHostMalloc(reinterpret_cast<void **>(&h), n * sizeof(WorkerSlot), hipHostMallocCoherent) != hipSuccess ||
         hipHostGetDevicePointer(&d, h, 0) != hipSuccess || hipMalloc(&w.d_activity, sizeof(uint64_t)) != hipSuccess ||
         hipMemset(w.d_activity, 0, sizeof(uint64_t)) != hipSuccess) {
@@ -2599,7 +2605,9 @@ static uint32_t pool_take_locked(ptls_hip_engine_t *eng, int c)
 {
     auto &ret = g_pool.retired[c];
     for (size_t k = 0; k < ret.size();) {
-        if (hipEventQuery(ret[k].zeroed) == hipSuccess && (ret[k].epoch == 0 || worker_drained(g_worker, ret[k].epoch))) {
+        /* the epoch test first: a slot of the resident dispatch costs no runtime call (the list holds at most one
+         * dispatch lifetime of frees, WORKER_LIFE_US) */
+        if ((ret[k].epoch == 0 || worker_drained(g_worker, ret[k].epoch)) && hipEventQuery(ret[k].zeroed) == hipSuccess) {
             g_pool.free_ids[c].push_back(ret[k].id);
             g_pool.events.push_back(ret[k].zeroed);
             ret[k] = ret.back();

@@ -69,6 +69,17 @@ GF128_FN U128 gf_mul_xpow(U128 p, int s)
     return u128_xor(r, u128_shl(d, 121 - s));
 }
 
+/* P * x^s for a per-lane 0 <= s <= 31, branch-free (every shift amount stays within 0..63, where 64-bit shifts are
+ * defined on host and device alike): the s dropped bits D = the low s bits of lo fold back as D << (64 - s), << (63 - s),
+ * << (62 - s), << (57 - s), all inside hi.  D << (64 - s) is written (D << 1) << (63 - s) so that s = 0 shifts by 63. */
+GF128_FN U128 gf_mul_xpow31(U128 p, uint32_t s)
+{
+    const uint64_t d = p.lo & ((1ull << s) - 1ull);
+    U128 r{p.hi >> s, (p.lo >> s) | ((p.hi << 1) << (63u - s))};
+    r.hi ^= ((d << 1) << (63u - s)) ^ (d << (63u - s)) ^ (d << (62u - s)) ^ (d << (57u - s));
+    return r;
+}
+
 /* bit m of the 32-bit x to bit 2m of the result */
 GF128_FN uint64_t spread32(uint64_t x)
 {

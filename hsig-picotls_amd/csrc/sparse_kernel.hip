@@ -22,6 +22,7 @@
 #include <type_traits>
 
 #include "batch_kernel.h"
+#include "gf128.h"
 
 namespace ptls_hip {
 
@@ -41,7 +42,10 @@ namespace ptls_hip {
 #define PLUGIN_PROBE 0 /* timing probe only (wrong output): 1 = no AES table build */
 #endif
 #ifndef SPARSE_QUEUE
-#define SPARSE_QUEUE 1 /* waves claim records from the launch's queue word (greedy, longest first) instead of a static stride */
+#define SPARSE_QUEUE 3 /* the deal of records to waves (aesgcm_sparse_kernel): 0 static stride, 1 queue, 2 snake, 3 snake + queue tail */
+#endif
+#ifndef SPARSE_TAIL
+#define SPARSE_TAIL 4 /* SPARSE_QUEUE 3: the last nrecs / SPARSE_TAIL records (the shortest) come from the queue */
 #endif
 #ifndef SPARSE_PE
 #define SPARSE_PE 2 /* GHASH elements (AES blocks) per lane per main-loop iteration */
@@ -116,8 +120,9 @@ __device__ __forceinline__ void wave_lds_sync()
  * Lane l writes position l/2, values 8(l&1) .. 8(l&1) + 7: load_wave_basis fetches the lane's four basis
  * vectors (issued early to hide their latency), store_wave_table writes the eight combinations. */
 #ifndef SPARSE_DERIVE
-#define SPARSE_DERIVE 1 /* 1: each lane loads ONE basis vector and derives the other three by multiplying by x (VALU): a
-                           quarter of the per-record basis reads (c4s: 4 KiB -> 1 KiB per record); 0: four loads */
+#define SPARSE_DERIVE 2 /* 2: each lane loads P x^(32 w) (one of four vectors, four cache lines per record), moves it to its
+                           own P x^(e0 - 3) by a 0..28-bit multiply by x^r and derives the other three by multiplying by x
+                           (VALU); 1: loads P x^(e0 - 3) itself (32 vectors over 16 lines); 0: four loads per lane */
 #endif
 
 /* v * x in GF(2^128), GCM bit order, raw byte order words: the 128-bit big-endian string shifted right by one bit,
@@ -130,12 +135,33 @@ __device__ __forceinline__ V4 mulx_raw(V4 v)
               bswap32(__builtin_amdgcn_alignbit(a1, a2, 1)), bswap32(__builtin_amdgcn_alignbit(a2, a3, 1))};
 }
 
+/* v * x^r for a per-lane r <= 31 (gf128.h's gf_mul_xpow31 on the raw words) */
+__device__ __forceinline__ V4 mulxpow_raw(V4 v, uint32_t r)
+{
+    const U128 p{(uint64_t)bswap32(v.w0) << 32 | bswap32(v.w1), (uint64_t)bswap32(v.w2) << 32 | bswap32(v.w3)};
+    const U128 z = gf_mul_xpow31(p, r);
+    return V4{bswap32((uint32_t)(z.hi >> 32)), bswap32((uint32_t)z.hi), bswap32((uint32_t)(z.lo >> 32)), bswap32((uint32_t)z.lo)};
+}
+
+/* the lane's smallest exponent e0 - 3 = 32 w + r (below): its offset r inside the lane's 32-vector group */
+__device__ __forceinline__ uint32_t basis_r(int lane)
+{
+    const int j = (lane >> 1) & 7;
+    return (uint32_t)(8 * (j >> 1) + 4 - 4 * (j & 1));
+}
+
 __device__ __forceinline__ void load_wave_basis(const uint4 *__restrict__ bp, int lane, V4 (&b)[4])
 {
     asm volatile("" : "+v"(lane)); /* the lane's basis offset computed here, not hoisted out of the record loop (scratch) */
     const int p = lane >> 1, w = p >> 3, j = p & 7;
     /* the lane's four vectors are P x^(e0), P x^(e0 - 1), P x^(e0 - 2), P x^(e0 - 3) for one e0 (bits 4j .. 4j + 3 of
-     * word w lie in one byte): SPARSE_DERIVE loads the last and store_wave_table derives the others */
+     * word w lie in one byte): e0 - 3 = 32 w + basis_r(lane).  SPARSE_DERIVE 1 loads P x^(e0 - 3), 2 loads P x^(32 w);
+     * store_wave_table derives the rest */
+    if (SPARSE_DERIVE == 2) {
+        const uint4 v = bp[32 * w];
+        b[3] = V4{v.x, v.y, v.z, v.w};
+        return;
+    }
 #pragma unroll
     for (int t = SPARSE_DERIVE ? 3 : 0; t < 4; ++t) {
         const int u = 4 * j + t; /* bit u of little-endian word w = raw byte 4w + u/8, bit u%8 */
@@ -146,6 +172,11 @@ __device__ __forceinline__ void load_wave_basis(const uint4 *__restrict__ bp, in
 
 __device__ __forceinline__ void store_wave_table(uint8_t *lds, uint32_t tab, V4 (&b)[4], int lane)
 {
+    if (SPARSE_DERIVE == 2) {
+        int ln = lane;
+        asm volatile("" : "+v"(ln));
+        b[3] = mulxpow_raw(b[3], basis_r(ln));
+    }
     if (SPARSE_DERIVE) {
         b[2] = mulx_raw(b[3]);
         b[1] = mulx_raw(b[2]);
@@ -777,28 +808,51 @@ __global__ void __launch_bounds__(WG)
     }
     const uint32_t waves = gridDim.x * (WG / 64);
     const uint32_t w0 = __builtin_amdgcn_readfirstlane(blockIdx.x * (WG / 64) + (threadIdx.x >> 6));
-    /* SPARSE_QUEUE: every wave claims its next record from the launch's queue word (records sorted by decreasing length,
-     * so the longest go first: a greedy longest-first deal) instead of the static stride w0 + k * waves, whose fixed share
-     * leaves the slowest waves (the youngest on each SIMD, the CUs of the slowest XCD) on the critical path.  The claim
-     * for the next record is issued when a record starts, so its latency runs under the record.  The last wave to claim
-     * past the end resets the words (engine.cpp queue_slot). */
-    const bool dyn = SPARSE_QUEUE && !by_value && queue != nullptr;
+    /* The deal of records (sorted by decreasing length) to the launch's waves, SPARSE_QUEUE:
+     *   0  static stride: wave w takes w, w + waves, w + 2 waves, ...; wave 0 takes the longest record of every round;
+     *   1  every record from the launch's queue word (greedy, longest first): ~65 K agent-scope atomics on one word per
+     *      c4s launch, whose return the record's first load wait takes (c4s 446 against 467-475 GiB/s static, one box);
+     *   2  snake: round k goes forward on even k and backward on odd k, so each wave's lengths pair long with short;
+     *   3  snake over the first nrecs - nrecs / SPARSE_TAIL records, the shortest tail from the queue word (a few claims
+     *      per wave, taking up what the waves' different speeds leave: the youngest wave on each SIMD, the slowest XCD).
+     * A queued claim is issued when the record before it starts, so its latency runs under that record; the last wave to
+     * claim past the end resets the words (engine.cpp queue_slot). */
+    const bool dyn = (SPARSE_QUEUE & 1) && !by_value && queue != nullptr;
+    const uint32_t nstat = !dyn ? nrecs : SPARSE_QUEUE == 1 ? 0u : nrecs - nrecs / SPARSE_TAIL;
+    auto stat_pos = [&](uint32_t k) -> uint32_t {
+        if (SPARSE_QUEUE >= 2)
+            return k * waves + ((k & 1u) ? waves - 1u - w0 : w0);
+        return w0 + k * waves;
+    };
     auto claim = [&]() -> uint32_t { /* lane 0's returned value; read (readfirstlane) only when it is needed */
         uint32_t v = 0;
         if (lane == 0)
             v = __hip_atomic_fetch_add(queue, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         return v;
     };
-    uint32_t pos = dyn ? (uint32_t)__builtin_amdgcn_readfirstlane(claim()) : w0;
+    uint32_t kk = 0, pos = stat_pos(0);
+    bool in_dyn = dyn && pos >= nstat;
+    if (in_dyn)
+        pos = nstat + (uint32_t)__builtin_amdgcn_readfirstlane(claim());
     while (pos < nrecs) {
-        const uint32_t next_v = dyn ? claim() : 0u;
+        const uint32_t sp = stat_pos(kk + 1);
+        const bool nd = dyn && (in_dyn || sp >= nstat);
+        const uint32_t next_v = nd ? claim() : 0u;
         phase_acc(pa, bstamps, 1);
         const ptls_hip_record_t rec = by_value ? one : recs_ord[pos];
         const uint32_t rec_i = by_value ? 0u : order != nullptr ? order[pos] : pos;
         /* a single record's wave 0 takes the unused table areas of waves 1 and 2 for its lane-combination table */
         sparse_record<ROUNDS, OPEN, ALIGNED, BYVAL>(lds, lane, lb_aes, tab, rec, rec_i, in, aad, out, result, slots, basis, supp,
                                                    hp_slots, hp_nslots, mask, prefetch, pre, clk, stamps, bstamps, pa, SP_TAB + 8192u);
-        pos = dyn ? (uint32_t)__builtin_amdgcn_readfirstlane(next_v) : pos + waves;
+        if (by_value)
+            break;
+        if (nd) {
+            pos = nstat + (uint32_t)__builtin_amdgcn_readfirstlane(next_v);
+            in_dyn = true;
+        } else {
+            ++kk;
+            pos = sp;
+        }
     }
     if (dyn && lane == 0 &&
         __hip_atomic_fetch_add(queue + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == waves - 1) {

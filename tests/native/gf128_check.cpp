@@ -47,6 +47,10 @@ int main()
                 printf("mul_xpow s=%d it=%d\n", s, it);
                 return 1;
             }
+            if (s <= 31 && !eq(gf_mul_xpow31(p, (uint32_t)s), r)) {
+                printf("mul_xpow31 s=%d it=%d\n", s, it);
+                return 1;
+            }
             r = mulx_ref(r);
         }
         if (!eq(gf_square(a), mul_ref(a, a))) {
