@@ -38,6 +38,9 @@ namespace ptls_hip {
 #ifndef SPARSE_PURE
 #define SPARSE_PURE 1 /* the branch-free skewed stretch over full blocks (0: every element on the generic path) */
 #endif
+#ifndef SPARSE_PURE1
+#define SPARSE_PURE1 1 /* an odd full-block element after the stretch's KP-block iterations takes a single-block step */
+#endif
 #ifndef PLUGIN_PROBE
 #define PLUGIN_PROBE 0 /* timing probe only (wrong output): 1 = no AES table build */
 #endif
@@ -417,9 +420,13 @@ __device__ __forceinline__ void sparse_record(uint8_t *lds, int lane, uint32_t l
      * record, tools/sparse_stamps.py) is gone. */
     const int ml = vl < na ? (na - vl + S - 1) >> LOG2S : 0;                      /* the lane's first data element */
     const int mhl = lastc + na - vl >= 0 ? ((lastc + na - vl) >> LOG2S) + 1 : 0;  /* its elements m < mhl: full blocks */
-    const int npure = SPARSE_PURE ? -wave_max_sp(-max(mhl - ml, 0)) / KP : 0;
+    const int fmin = -wave_max_sp(-max(mhl - ml, 0)); /* full-block elements every lane has */
+    const int npure = SPARSE_PURE ? fmin / KP : 0;
+    /* SPARSE_PURE1: an odd full element left over by the KP-block iterations takes one single-block step of the stretch
+     * instead of the generic path */
+    const int npx = SPARSE_PURE1 && npure > 0 && fmin - npure * KP > 0 ? 1 : 0;
     const int iters_l = vl < N ? ((N - 1 - vl) >> LOG2S) + 1 : 0;                /* the lane's elements */
-    const int pm1 = ml + npure * KP;                                              /* the lane's first after the stretch */
+    const int pm1 = ml + npure * KP + npx;                                        /* the lane's first after the stretch */
     if (!npure) { /* head and tail are one range: elements share one round trip to the record's memory (the plugin) */
         generic_range(std::integral_constant<bool, BYVAL>{}, 0, iters);
     } else { /* the lane's AAD elements: GHASH only */
@@ -486,6 +493,9 @@ __device__ __forceinline__ void sparse_record(uint8_t *lds, int lane, uint32_t l
                 }
             }
         };
+        /* the single-block step (npx): data block c0 + npure KP S of the lane */
+        const size_t ox = (size_t)npure * KP * 16 * S;
+        uint32_t cwx[1] = {bswap32((uint32_t)(c0 + 2 + npure * KP * S))};
         if (OPEN) {
             pure_iter(0, false, bufA, bufB);
             int it = 1;
@@ -495,13 +505,32 @@ __device__ __forceinline__ void sparse_record(uint8_t *lds, int lane, uint32_t l
             }
             if (it < npure)
                 pure_iter(it, true, bufB, bufA);
+            if (npx) { /* hashes its own input ciphertext, as the iterations do */
+                const V4 dx[1] = {load_full(src + ox)};
+                V4 kx[1] = {V4{n0, n1, n2, cwx[0]}};
+                ctr_ghash_skewed<ROUNDS, 1, true>(lds, lb_aes, rk, cc, cwx, kx, y, dx, GhNibble{tab});
+                store_full(dst + ox, v4xor(dx[0], kx[0]));
+            }
         } else {
             pure_iter(0, false, bufA, bufA);
             for (int it = 1; it < npure; ++it)
                 pure_iter(it, true, bufA, bufA);
+            if (npx) { /* the last iteration's ciphertext blocks hashed here but its last, which goes under the step's AES */
+                const V4 dx = load_full(src + ox);
 #pragma unroll
-            for (int b = 0; b < KP; ++b)
-                y = v4xor(gh_mul_nibble(lds, tab, y), pend[b]);
+                for (int b = 0; b + 1 < KP; ++b)
+                    y = v4xor(gh_mul_nibble(lds, tab, y), pend[b]);
+                const V4 hx[1] = {pend[KP - 1]};
+                V4 kx[1] = {V4{n0, n1, n2, cwx[0]}};
+                ctr_ghash_skewed<ROUNDS, 1, true>(lds, lb_aes, rk, cc, cwx, kx, y, hx, GhNibble{tab});
+                const V4 cx = v4xor(dx, kx[0]);
+                store_full(dst + ox, cx);
+                y = v4xor(gh_mul_nibble(lds, tab, y), cx);
+            } else {
+#pragma unroll
+                for (int b = 0; b < KP; ++b)
+                    y = v4xor(gh_mul_nibble(lds, tab, y), pend[b]);
+            }
         }
     }
     phase_stamp(clk, stamps, lane, 5);
@@ -1020,8 +1049,9 @@ __global__ void __launch_bounds__(WORKER_WG)
         /* the request (and the record, inline or in the caller's pinned staging) was written before seq.  Ordering the
          * loads is not enough: the vector L1 keeps the previous request's lines at the same addresses (measured: a
          * workgroup-scope acquire served request 2 with request 1's completion pointer), so the acquire is at system
-         * scope, which invalidates the L1 and the L2's lines of host memory.  Device key material is never modified
-         * while a worker is resident (engine.cpp worker_quiesce), so no cache can hold a stale key slot. */
+         * scope, which invalidates the L1 and the L2's lines of host memory.  A key slot this dispatch may have read is never
+         * rewritten while it is resident (engine.cpp slot pool: a freed slot is handed out again only after the dispatch
+         * that could hold it has left), so neither the scalar nor the vector caches can hold a stale key slot. */
         uint64_t st[5] = {0, 0, 0, 0, 0};
         if (WORKER_STAMPS)
             st[0] = worker_stamp();

@@ -9,7 +9,11 @@ own process, with the worker on (the default) and off (PTLS_HIP_PLUGIN_WORKER=0:
 test_plugin_worker_threads: eight threads with their own contexts at once over 1, 4 and 8 mailboxes (shared homes, the
 try-lock hand-off, a workgroup leaving while the others serve), with IV changes, context churn on every thread (pooled
 slots recycled while other threads' requests run), records too long for a mailbox (the context's own staging) and gaps
-past the idle timeout and the lifetime, every output against lib/fusion.c."""
+past the idle timeout and the lifetime, every output against lib/fusion.c.
+test_plugin_calls_beside_batch_launches: four threads make plugin calls while 1 GiB batch seals run back to back on the
+same device (the worker's workgroups hold CUs the batch kernel's workgroups then start late on; neither may stall or
+corrupt the other): every plugin output against lib/fusion.c, the batch opened back in full and sampled records against
+lib/fusion.c."""
 import os
 import subprocess
 import sys
@@ -153,6 +157,98 @@ for t in ts:
 assert not errors, errors
 print("ok")
 """
+
+
+_CASE_BESIDE = r"""
+import sys, threading
+sys.path[:0] = {paths!r}
+import torch
+torch.zeros(1, device="cuda")  # torch's HIP runtime first (the plugin's own initialisation otherwise hides the GPU from it)
+import numpy as np
+import ptls_hip
+import plugin_driver
+from oracle_lib import Ref, tls_aad
+drv, ref = plugin_driver.PluginDriver(), Ref()
+eng = ptls_hip.Engine(0)
+rng = np.random.default_rng(21)
+n, L = 65536, 16384
+recs, in_total, out_total, aad_total = ptls_hip.layout_records(np.full(n, L), np.full(n, 5), np.zeros(n, np.uint32),
+                                                               np.arange(n, dtype=np.uint64), align=128)
+key, iv = rng.bytes(16), rng.bytes(12)
+ks = ptls_hip.KeySet(eng, 16, 1)
+ks.set(0, key, iv)
+sb = ptls_hip.Batch(eng, recs)
+ro = recs.copy()
+ro["in_off"], ro["out_off"] = recs["out_off"], recs["in_off"]
+ob = ptls_hip.Batch(eng, ro)
+ob.set_lanes(sb.lanes)
+pt = torch.randint(0, 256, (in_total,), dtype=torch.uint8, device="cuda")
+aad_h = np.zeros(aad_total, dtype=np.uint8)
+for i in range(n):
+    o = int(recs["aad_off"][i])
+    aad_h[o:o + 5] = np.frombuffer(tls_aad(L), dtype=np.uint8)
+aad = torch.from_numpy(aad_h).cuda()
+ct = torch.zeros(out_total, dtype=torch.uint8, device="cuda")
+back = torch.zeros(in_total, dtype=torch.uint8, device="cuda")
+res = torch.zeros(n, dtype=torch.int64, device="cuda")
+torch.cuda.synchronize()
+
+stop, errors, calls = threading.Event(), [], [0] * 4
+def caller(t):
+    try:
+        r = np.random.default_rng(300 + t)
+        bits = 128 if t % 2 == 0 else 256
+        k2, iv2 = r.bytes(bits // 8), r.bytes(12)
+        e, d = drv.new(bits, k2, iv2, 1), drv.new(bits, k2, iv2, 0)
+        i = 0
+        while not stop.is_set() or i < 50:
+            m = int(r.choice([0, 17, 1350, 1500, 4096, 16384]))
+            p, a = r.bytes(m), tls_aad(m)
+            c = drv.encrypt(e, p, i, a)
+            assert c == ref.seal(k2, iv2, i, a, p), ("seal", t, i, m)
+            assert drv.decrypt(d, c, i, a) == p, ("open", t, i, m)
+            i += 1
+        calls[t] = i
+        drv.free(e)
+        drv.free(d)
+    except Exception as ex:  # noqa: BLE001
+        errors.append(repr(ex))
+        stop.set()
+ts = [threading.Thread(target=caller, args=(t,)) for t in range(4)]
+for t in ts:
+    t.start()
+for rep in range(40):
+    sb.seal(ks, pt, aad, ct)
+    if rep % 8 == 0:
+        torch.cuda.synchronize()
+torch.cuda.synchronize()
+stop.set()
+for t in ts:
+    t.join()
+assert not errors, errors
+ob.open(ks, ct, aad, back, res)
+torch.cuda.synchronize()
+assert bool((res == L).all()), "a record failed to open"
+assert torch.equal(back, pt), "the opened plaintext differs"
+ct_h, pt_h = ct.cpu().numpy(), pt.cpu().numpy()
+for i in (0, 1, 4097, 32768, n - 1):
+    io, oo = int(recs["in_off"][i]), int(recs["out_off"][i])
+    want = ref.seal(key, iv, i, tls_aad(L), pt_h[io:io + L].tobytes())
+    assert ct_h[oo:oo + L + 16].tobytes() == want, ("batch record", i)
+print("calls", calls)
+print("ok")
+"""
+
+
+def test_plugin_calls_beside_batch_launches():
+    from oracle_lib import Ref
+    if not Ref.available:
+        pytest.skip("oracle/_ref not built")
+    paths = [os.path.join(ROOT, "tests"), os.path.join(ROOT, "hsig-picotls_amd"), ROOT]
+    env = dict(os.environ, PTLS_HIP_PLUGIN_WORKER="1")
+    r = subprocess.run([sys.executable, "-c", _CASE_BESIDE.format(paths=paths)], env=env, capture_output=True, text=True,
+                       timeout=240)
+    assert r.returncode == 0 and r.stdout.strip().endswith("ok"), (r.returncode, r.stdout[-2000:], r.stderr[-3000:])
 
 
 @pytest.mark.parametrize("workers", ["1", "4", "8"])
