@@ -1123,12 +1123,64 @@ __device__ __forceinline__ void clock_stamp(uint64_t *__restrict__ clk, int slot
     }
 }
 
+/* ---- cross-lane sums and maxima on the VALU ----
+ * Over aligned groups of N = 1 .. 64 lanes: DPP row permutations pair each lane with one in the other half of its quad
+ * (quad_perm [1,0,3,2], then [2,3,0,1]), of its 8 lanes (row_half_mirror: i <-> 7 - i) and of its 16-lane row
+ * (row_mirror: i <-> 15 - i); gfx950's v_permlane16_swap / v_permlane32_swap pair the two rows of a 32-lane half and the
+ * two halves of the wave (a swap of vdst = src = v leaves {own, partner} in the two results, in some order).  After
+ * log2(N) stages every lane holds the group's total.  No LDS instruction and no per-lane partner address: the
+ * ds_bpermute form cost one LDS instruction per stage and word on an LDS-bound kernel, waited an LDS round trip per
+ * stage, and its partner addresses were hoisted out of the record loops into long-lived registers. */
+constexpr int DPP_QUAD_XOR1 = 0xB1, DPP_QUAD_XOR2 = 0x4E, DPP_ROW_HALF_MIRROR = 0x141, DPP_ROW_MIRROR = 0x140;
+
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp_mov(uint32_t v)
+{
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xf, 0xf, false);
+}
+
+/* every lane of the v's N-lane group gets op over the group (called with every lane of the wave active) */
+template <int N, class OP>
+__device__ __forceinline__ uint32_t group_reduce(uint32_t v, OP op)
+{
+    static_assert(N >= 1 && N <= 64 && (N & (N - 1)) == 0, "group of 1 .. 64 lanes");
+    if constexpr (N >= 2)
+        v = op(v, dpp_mov<DPP_QUAD_XOR1>(v));
+    if constexpr (N >= 4)
+        v = op(v, dpp_mov<DPP_QUAD_XOR2>(v));
+    if constexpr (N >= 8)
+        v = op(v, dpp_mov<DPP_ROW_HALF_MIRROR>(v));
+    if constexpr (N >= 16)
+        v = op(v, dpp_mov<DPP_ROW_MIRROR>(v));
+    if constexpr (N >= 32) {
+        const auto p = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+        v = op((uint32_t)p[0], (uint32_t)p[1]);
+    }
+    if constexpr (N >= 64) {
+        const auto p = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+        v = op((uint32_t)p[0], (uint32_t)p[1]);
+    }
+    return v;
+}
+
+struct XorOp {
+    __device__ __forceinline__ uint32_t operator()(uint32_t a, uint32_t b) const { return a ^ b; }
+};
+struct MaxOp {
+    __device__ __forceinline__ uint32_t operator()(uint32_t a, uint32_t b) const { return (uint32_t)max((int)a, (int)b); }
+};
+
+/* the GF(2^128) sum of a V4 over each N-lane group, in every lane of the group */
+template <int N>
+__device__ __forceinline__ V4 group_xor(V4 z)
+{
+    return V4{group_reduce<N>(z.w0, XorOp{}), group_reduce<N>(z.w1, XorOp{}), group_reduce<N>(z.w2, XorOp{}),
+              group_reduce<N>(z.w3, XorOp{})};
+}
+
 __device__ __forceinline__ int wave_max(int v)
 {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1)
-        v = max(v, __shfl_xor(v, o, 64));
-    return v;
+    return (int)group_reduce<64>((uint32_t)v, MaxOp{});
 }
 
 /* Bit-sliced AES-CTR keystream of 8 counter blocks c0 + k * stride of one lane (bs8_aes.h, all on the VALU); the
@@ -1690,13 +1742,7 @@ __global__ void __launch_bounds__(WGT)
                         const uint4 hp = reinterpret_cast<const uint4 *>(basis)[(size_t)ch.key * BASIS_VECS + NPOW * 128 + q]; /* H^(q+1) */
                         s = gf_mul_valu(y, V4{hp.x, hp.y, hp.z, hp.w});
                     }
-#pragma unroll
-                    for (int o = G / 2; o > 0; o >>= 1) {
-                        s.w0 ^= __shfl_xor(s.w0, o, 64);
-                        s.w1 ^= __shfl_xor(s.w1, o, 64);
-                        s.w2 ^= __shfl_xor(s.w2, o, 64);
-                        s.w3 ^= __shfl_xor(s.w3, o, 64);
-                    }
+                    s = group_xor<G>(s); /* the sum over the record's G lanes (VALU_TREE at G < 32 too) */
                 }
             } else {
 #pragma unroll

@@ -44,6 +44,24 @@ namespace ptls_hip {
 #ifndef PLUGIN_PROBE
 #define PLUGIN_PROBE 0 /* timing probe only (wrong output): 1 = no AES table build */
 #endif
+#ifndef SPARSE_AADPF
+#define SPARSE_AADPF 1 /* batch records: the lane's first AAD block is loaded at record setup, before the counter-mode constants
+                        * and the H^64 table (its latency under that work) instead of after them: c4s seal 498-504 -> 513-519,
+                        * open 514-516 -> 520-521 GiB/s (same box, profiles/r04_c4s_prefetch_ab.log) */
+#endif
+#ifndef SPARSE_TAGPF
+#define SPARSE_TAGPF 0 /* batch open: the received tag is loaded at record setup instead of after the lane combination (measured
+                        * no faster: 505-514 against 514-516 GiB/s open) */
+#endif
+#ifndef SPARSE_HPPF
+#define SPARSE_HPPF 0 /* batch records: the lane's power H^(q+1) for the combination is loaded after the stretch, under the tail
+                       * elements, instead of at the combination (measured neutral: 516 / 521 against 517 / 524 GiB/s) */
+#endif
+#ifndef SPARSE_BASISPF
+#define SPARSE_BASISPF 0 /* batch records: the H^64 basis loads go out before the counter-mode constants (as the single record's;
+                          * measured neutral: 518 / 521 against 517 / 524 GiB/s).  Touching the next record's key slot, basis
+                          * and lane-power lines during the current record was neutral as well (501-504 against 503-511) */
+#endif
 #ifndef SPARSE_QUEUE
 #define SPARSE_QUEUE 3 /* the deal of records to waves (aesgcm_sparse_kernel): 0 static stride, 1 queue, 2 snake, 3 snake + queue tail */
 #endif
@@ -220,45 +238,30 @@ __device__ __forceinline__ void store_wave_table(uint8_t *lds, uint32_t tab, V4 
 #define SPARSE_WIN_LB 4 /* the batch instantiations' lookups in flight per group (8: 32 VGPRs, spills at 168) */
 #endif
 
-/* the wave's maximum (every lane), from an opaque lane index like wave_xor below: batch_kernel.h's wave_max lets the
- * compiler hoist its six partner addresses out of the record loop (scratch in the sparse kernel's batch instantiations) */
+/* the wave's maximum / XOR sum in every lane: batch_kernel.h's DPP + permlane reduction (no LDS instruction, no partner
+ * address; until round 4 a ds_bpermute butterfly whose partner addresses had to come from an opaque lane index, or the
+ * compiler hoisted them out of the record loop into scratch) */
 __device__ __forceinline__ int wave_max_sp(int v)
 {
-    int ln = (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
-    asm volatile("" : "+v"(ln));
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1)
-        v = max(v, __builtin_amdgcn_ds_bpermute((ln ^ o) << 2, v));
-    return v;
+    return wave_max(v);
 }
 
-/* XOR butterfly over the wave: every lane ends with the sum of the 64 lanes' values */
 __device__ __forceinline__ V4 wave_xor(V4 z)
 {
-    /* the partner lanes' addresses from an opaque lane index: hoisted out of the record loop, the five (lane ^ o) * 4 stay
-     * live across the kernel and pushed the batch instantiations into scratch (reloaded from HBM per record) */
-    int ln = (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
-    asm volatile("" : "+v"(ln));
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        const int a = (ln ^ o) << 2;
-        z.w0 ^= (uint32_t)__builtin_amdgcn_ds_bpermute(a, (int)z.w0);
-        z.w1 ^= (uint32_t)__builtin_amdgcn_ds_bpermute(a, (int)z.w1);
-        z.w2 ^= (uint32_t)__builtin_amdgcn_ds_bpermute(a, (int)z.w2);
-        z.w3 ^= (uint32_t)__builtin_amdgcn_ds_bpermute(a, (int)z.w3);
-    }
-    return z;
+    return group_xor<64>(z);
 }
 
 /* sum over the wave of (lane's GHASH sum) * H^(q+1): one multiply by the lane's own power (keysetup's H^1..H^64 table),
  * then the XOR butterfly; every lane ends with the total.  SPARSE_WIN: the multiply's table is the lane's 8 multiples of
  * H^(q+1) in the wave's own 8 KiB table area (the H^64 Horner table is dead by now). */
-__device__ __forceinline__ V4 ghash_combine(uint8_t *lds, uint32_t tab, int lane, const uint4 *__restrict__ bs, int q, V4 y)
+__device__ __forceinline__ V4 ghash_combine(uint8_t *lds, uint32_t tab, int lane, const uint4 *__restrict__ bs, int q, V4 y,
+                                          bool have_hp = false, uint4 hp = uint4{0, 0, 0, 0})
 {
     /* q made opaque here: the power's load and the table arithmetic stay after the record's elements instead of being
      * hoisted above the stretch (where their registers pushed the batch instantiations into scratch) */
     asm volatile("" : "+v"(q));
-    const uint4 hp = bs[NPOW * 128 + q]; /* H^(q+1) */
+    if (!have_hp)
+        hp = bs[NPOW * 128 + q]; /* H^(q+1) */
     const V4 p = V4{hp.x, hp.y, hp.z, hp.w};
     return wave_xor(SPARSE_WIN ? gf_mul_win4<8, SPARSE_WIN_LB>(lds, tab, lane, y, p) : gf_mul_valu(y, p));
 }
@@ -316,13 +319,20 @@ __device__ __forceinline__ void sparse_record(uint8_t *lds, int lane, uint32_t l
      * memory latency overlaps that LDS chain (in batches other waves hide it; there the early loads cost c4s open
      * 2.5 %, measured) */
     const int q = (N - 1 - vl) & (S - 1);
+    /* batch records: loads whose latency would otherwise sit after the table build (SPARSE_AADPF, SPARSE_TAGPF) */
+    V4 aad_pf = V4{0, 0, 0, 0}, tag_pf = V4{0, 0, 0, 0};
+    if (SPARSE_AADPF && !BYVAL && vl < na)
+        aad_pf = load_block<ALIGNED>(aad_p + 16 * vl, min(16, A - 16 * vl));
+    if (SPARSE_TAGPF && OPEN && !BYVAL && q == 0)
+        tag_pf = load_block<false>(in_p + L, 16);
+    (void)aad_pf, (void)tag_pf;
     /* a single record builds its lane-combination table (the 16 multiples of H^(q+1)) early, in an LDS area of its own
      * (ctab), so that only the lookups remain after its last element */
     constexpr bool early_win = BYVAL && SPARSE_WIN;
     uint4 hpe = uint4{0, 0, 0, 0};
     if (early_win)
         hpe = bs[NPOW * 128 + q]; /* H^(q+1) */
-    if (horner && by_value)
+    if (horner && (by_value || SPARSE_BASISPF))
         load_wave_basis(bs + LOG2S * 128, lane, b); /* H^S */
     /* the record (and so its counter-mode constants) is the wave's alone: keep them in SGPRs */
     CtrConst cc = ctr_const(lds, lb_aes, rk, n0, n1, n2);
@@ -341,7 +351,7 @@ __device__ __forceinline__ void sparse_record(uint8_t *lds, int lane, uint32_t l
     phase_acc(pa, bstamps, 2);
     wave_lds_sync(); /* the previous record's Horner reads of the table are done */
     if (horner) { /* (loading the basis during the previous record's VALU combine measured no faster: other waves hide it) */
-        if (!by_value)
+        if (!by_value && !SPARSE_BASISPF)
             load_wave_basis(bs + LOG2S * 128, lane, b); /* H^S */
         store_wave_table(lds, tab, b, lane);
     }
@@ -435,8 +445,9 @@ __device__ __forceinline__ void sparse_record(uint8_t *lds, int lane, uint32_t l
             if (j < ml) {
                 const int i = vl + S * j;
                 const int nb = min(16, A - 16 * i);
-                const V4 x = (BYVAL && prefetch && j < 2) ? mask_block(j == 0 ? pre[0] : pre[1], nb)
-                                                          : load_block<ALIGNED>(aad_p + 16 * i, nb);
+                const V4 x = (BYVAL && prefetch && j < 2)       ? mask_block(j == 0 ? pre[0] : pre[1], nb)
+                             : (SPARSE_AADPF && !BYVAL && j == 0) ? aad_pf
+                                                                  : load_block<ALIGNED>(aad_p + 16 * i, nb);
                 y = j == 0 ? x : v4xor(gh_mul_nibble(lds, tab, y), x);
             }
         }
@@ -535,6 +546,12 @@ __device__ __forceinline__ void sparse_record(uint8_t *lds, int lane, uint32_t l
     }
     phase_stamp(clk, stamps, lane, 5);
     phase_acc(pa, bstamps, 5);
+    uint4 hp_pf = uint4{0, 0, 0, 0};
+    if (SPARSE_HPPF && !early_win) { /* the combination's power, under the tail elements */
+        int qo = q;
+        asm volatile("" : "+v"(qo));
+        hp_pf = bs[NPOW * 128 + qo];
+    }
     if (npure) { /* the rest of each lane's elements from its own position (partial, length and leftover blocks) */
         const int rest = wave_max_sp(max(iters_l - pm1, 0));
         int j = 0;
@@ -552,7 +569,7 @@ __device__ __forceinline__ void sparse_record(uint8_t *lds, int lane, uint32_t l
         if (early_win)
             y = wave_xor(gf_win4_mul<16>(lds, w4, y));
         else
-            y = ghash_combine(lds, tab, lane, bs, q, y);
+            y = ghash_combine(lds, tab, lane, bs, q, y, SPARSE_HPPF != 0, hp_pf);
     }
     /* S = 128: the wave without the length block hands its sum over (and makes its output stores visible at system scope
      * first: the tag wave's caller stores the completion word); both waves pass the barrier */
@@ -572,7 +589,7 @@ __device__ __forceinline__ void sparse_record(uint8_t *lds, int lane, uint32_t l
     if (q == 0) {
         const V4 tag = v4xor(y, ek0);
         if (OPEN) {
-            const V4 rt = load_block<false>(in_p + L, 16);
+            const V4 rt = (SPARSE_TAGPF && !BYVAL) ? tag_pf : load_block<false>(in_p + L, 16);
             const bool ok = rt.w0 == tag.w0 && rt.w1 == tag.w1 && rt.w2 == tag.w2 && rt.w3 == tag.w3;
             result[rec_i] = ok ? (uint64_t)L : ~(uint64_t)0;
         } else {
