@@ -786,16 +786,20 @@ __device__ __forceinline__ void mulx_be(uint32_t (&v)[4])
 
 /* x * y in GF(2^128), GCM bit order, both operands per lane: gf_mul_valu's product with 4-bit windows over x (Shoup)
  * and a per-lane table of y in LDS instead of 128 single-bit steps.
- *   T[n] = n3 y + n2 y x + n1 y x^2 + n0 y x^3 (n3 = the nibble's first GCM bit); lane l keeps its NT entries at
- *   tab + l * NT * 16, entry n in slot (n + l) mod NT, so the 8 lanes of a ds_write_b128 group hit 8 bank quads.
+ *   T[n] = n3 y + n2 y x + n1 y x^2 + n0 y x^3 (n3 = the nibble's first GCM bit); entry n of lane l at
+ *   tab + n * 1024 + l * 16 (STRIDE = 1024: a row of the 64 lanes' entries n), so the 16 lanes of every ds_read_b128 /
+ *   ds_write_b128 group touch 16 consecutive 16-B slots, i.e. the 64 banks once, whatever the nibbles.  (Until round 4
+ *   lane l's entries were contiguous with a per-lane slot rotation: conflict-free stores but data-dependent 2-4-way
+ *   conflicts on the lookups, SQ_LDS_BANK_CONFLICT 4.7 % of c4s's LDS cycles.)
  *   NT = 8 holds T[0..7] and folds n3 y in on the VALU (8 KiB per wave: the sparse kernel's per-wave table area).
  *   Z = T[nib_31]; Z = Z x^4 + T[nib_j] for j = 30 .. 0.  The 4 bits each shift drops (positions 128..131) are
  *   collected in one overflow word and folded back every 8 shifts with x^128 = 1 + x + x^2 + x^7.
  * About 500 VALU + NT ds_write_b128 + 32 ds_read_b128 against gf_mul_valu's 1 408 VALU.  The caller owns the table
- * area; the wave's LDS operations complete in order, so no barrier is needed around it. */
-template <int NT>
+ * area; the wave's LDS operations complete in order, so no barrier is needed around it.  STRIDE = 512: the batch
+ * kernel's shared G = 32 tables ([n][q], build_ghash_tables), base = the record position q's column. */
+template <int NT, int STRIDE = 1024>
 struct Win4 {
-    uint32_t base, rot; /* the lane's table and its slot rotation */
+    uint32_t base;      /* entry n at base + n * STRIDE */
     uint32_t y[4];      /* NT = 8: y itself (big-endian words), folded in for the nibble's first bit */
 };
 
@@ -814,10 +818,9 @@ __device__ __forceinline__ Win4<NT> gf_win4_build(uint8_t *lds, uint32_t tab, in
     }
     Win4<NT> t;
     uint32_t ln = (uint32_t)lane;
-    asm volatile("" : "+v"(ln)); /* keeps the lane's slot arithmetic here: hoisted out of a record loop, its 8-16 values
-                                    stay live across the whole kernel (the sparse batch kernel spilled 200 B per lane) */
-    t.base = tab + ln * (uint32_t)(NT * 16);
-    t.rot = ln & (uint32_t)(NT - 1);
+    asm volatile("" : "+v"(ln)); /* keeps the lane's slot arithmetic here: hoisted out of a record loop, its values stay
+                                    live across the whole kernel (the sparse batch kernel spilled 200 B per lane) */
+    t.base = tab + ln * 16u;
 #pragma unroll
     for (int w = 0; w < 4; ++w)
         t.y[w] = m[0][w];
@@ -830,13 +833,13 @@ __device__ __forceinline__ Win4<NT> gf_win4_build(uint8_t *lds, uint32_t tab, in
 #pragma unroll
                 for (int w = 0; w < 4; ++w)
                     e[w] ^= m[k][w];
-        lds128_store(lds, t.base + (((uint32_t)n + t.rot) & (uint32_t)(NT - 1)) * 16u, V4{e[0], e[1], e[2], e[3]});
+        lds128_store(lds, t.base + (uint32_t)n * 1024u, V4{e[0], e[1], e[2], e[3]});
     }
     return t;
 }
 
-template <int NT, int LB = 8>
-__device__ __forceinline__ V4 gf_win4_mul(const uint8_t *lds, const Win4<NT> &tb, V4 xr)
+template <int NT, int LB = 8, int STRIDE>
+__device__ __forceinline__ V4 gf_win4_mul(const uint8_t *lds, const Win4<NT, STRIDE> &tb, V4 xr)
 {
     static_assert(LB == 8 || LB == 4 || LB == 2, "lookups in flight: 8, 4 or 2");
     const uint32_t x[4] = {bswap32(xr.w0), bswap32(xr.w1), bswap32(xr.w2), bswap32(xr.w3)};
@@ -849,7 +852,7 @@ __device__ __forceinline__ V4 gf_win4_mul(const uint8_t *lds, const Win4<NT> &tb
         for (int ii = 0; ii < LB; ++ii) { /* nibble j = 8 w + 7 - i: bits 4 i .. 4 i + 3 from the bottom of word w */
             const int i = i0 + ii;
             const uint32_t nib = (x[w] >> (4 * i)) & 15u;
-            t[ii] = lds128(lds, tb.base + ((nib + tb.rot) & (uint32_t)(NT - 1)) * 16u);
+            t[ii] = lds128(lds, tb.base + (nib & (uint32_t)(NT - 1)) * (uint32_t)STRIDE);
             if (NT == 8) {
                 const uint32_t mk = 0u - (nib >> 3);
                 t[ii] = V4{t[ii].w0 ^ (mk & tb.y[0]), t[ii].w1 ^ (mk & tb.y[1]), t[ii].w2 ^ (mk & tb.y[2]), t[ii].w3 ^ (mk & tb.y[3])};
@@ -969,11 +972,12 @@ __device__ void build_ghash_tables(uint8_t *lds, const uint32_t *__restrict__ ba
         }
         lds128_store(lds, LDS_GTREE + d * LDS_TREE_STRIDE + p * 256 + v * 16, acc);
     }
-    /* win (G = 32, no tree): the lane combination's shared window tables in the tree area, [q][slot (n + q) mod 16] =
+    /* win (G = 32, no tree): the lane combination's shared window tables in the tree area, [n][q] (512-B rows) =
      * n * H^(q + 1) for q < 32, n < 16, in gf_win4_mul's big-endian words (gf_win4_build's entries, shared by every lane of
-     * the workgroup whose record position is q) */
+     * the workgroup whose record position is q).  A record's 32 lanes hold 32 distinct q, so each 16-lane group of a lookup
+     * reads 16 distinct slots of its row (until round 4: [q][slot (n + q) mod 16], data-dependent conflicts) */
     for (int e = tid - t0; win && e >= 0 && e < 32 * 16; e += nt) {
-        const int q = e >> 4, n = e & 15;
+        const int q = e & 31, n = e >> 5; /* consecutive threads: consecutive slots of a row (conflict-free stores) */
         const uint32_t *hp = basis + (NPOW * 128 + q) * 4; /* H^(q + 1) */
         uint32_t m[4] = {bswap32(hp[0]), bswap32(hp[1]), bswap32(hp[2]), bswap32(hp[3])}, acc[4] = {0, 0, 0, 0};
 #pragma unroll
@@ -984,7 +988,7 @@ __device__ void build_ghash_tables(uint8_t *lds, const uint32_t *__restrict__ ba
                     acc[w] ^= m[w];
             mulx_be(m);
         }
-        lds128_store(lds, LDS_GTREE + (uint32_t)q * 256u + (uint32_t)((n + q) & 15) * 16u, V4{acc[0], acc[1], acc[2], acc[3]});
+        lds128_store(lds, LDS_GTREE + (uint32_t)n * 512u + (uint32_t)q * 16u, V4{acc[0], acc[1], acc[2], acc[3]});
     }
 }
 
@@ -1734,9 +1738,8 @@ __global__ void __launch_bounds__(WGT)
                 s = V4{0, 0, 0, 0};
                 if (SPLIT_PROBE != 1) {
                     if constexpr (WINCOMB) { /* the key's shared window table of H^(q+1) (build_ghash_tables) */
-                        Win4<16> wt;
-                        wt.base = LDS_GTREE + (uint32_t)q * 256u;
-                        wt.rot = (uint32_t)q & 15u;
+                        Win4<16, 512> wt;
+                        wt.base = LDS_GTREE + (uint32_t)q * 16u;
                         s = gf_win4_mul<16, 4>(lds, wt, y);
                     } else {
                         const uint4 hp = reinterpret_cast<const uint4 *>(basis)[(size_t)ch.key * BASIS_VECS + NPOW * 128 + q]; /* H^(q+1) */
