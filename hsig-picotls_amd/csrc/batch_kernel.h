@@ -66,6 +66,13 @@ __host__ __device__ constexpr uint32_t lds_bytes(int log2g)
 #ifndef DYN_DEAL
 #define DYN_DEAL 1 /* waves draw tasks from a workgroup counter in LDS instead of a fixed per-chunk deal: c2 +3 %, c3 +5 %, c4 +5 % */
 #endif
+#ifndef WIN_ALL
+#define WIN_ALL 1 /* 1: every G >= 2 combines its record's partial sums like G = 32 (one windowed multiply per lane by H^(q+1)
+                     from shared per-key window tables, then an XOR over the record's lanes) instead of the log2(G)-level
+                     nibble-table tree and its final multiply by H (0): 32 table lookups + ~500 VALU per lane instead of
+                     (log2 G + 1) x 32 lookups in a dependent chain.  Same box (profiles/r04_win_all_ab.log): c3 seal
+                     1 118-1 135 -> 1 140-1 151, c2 +0.3-0.5 %, c4's lengths at ~105 records per key (G = 16) 858 -> 883 */
+#endif
 #ifndef G32_WIN
 #define G32_WIN 1 /* G = 32 lane combination: 1 = shared per-key window tables (gf_win4_mul), 0 = gf_mul_valu */
 #endif
@@ -930,6 +937,10 @@ __device__ __forceinline__ void build_aes_tables(uint8_t *lds, uint32_t base, co
  * stores whose 8-lane groups hold 8 different positions p, i.e. 8 different bank quads (conflict-free).
  * (Per entry from up to 8 basis loads with lanes 256 B apart cost a key switch 8x the loads and 8-way store
  * conflicts.)  The other threads build the tree tables meanwhile. */
+/* the shared window tables' row width (slots) and copies per record position (build_ghash_tables, the lane combination) */
+__host__ __device__ constexpr int win_row(int g) { return g > 16 ? g : 16; }
+__host__ __device__ constexpr int win_copies(int g) { return g >= 16 ? 1 : 16 / g; }
+
 __device__ void build_ghash_tables(uint8_t *lds, const uint32_t *__restrict__ basis, int log2g, bool tree = true, bool win = false)
 {
     const uint32_t *bm = basis + log2g * 128 * 4;
@@ -972,12 +983,14 @@ __device__ void build_ghash_tables(uint8_t *lds, const uint32_t *__restrict__ ba
         }
         lds128_store(lds, LDS_GTREE + d * LDS_TREE_STRIDE + p * 256 + v * 16, acc);
     }
-    /* win (G = 32, no tree): the lane combination's shared window tables in the tree area, [n][q] (512-B rows) =
-     * n * H^(q + 1) for q < 32, n < 16, in gf_win4_mul's big-endian words (gf_win4_build's entries, shared by every lane of
-     * the workgroup whose record position is q).  A record's 32 lanes hold 32 distinct q, so each 16-lane group of a lookup
-     * reads 16 distinct slots of its row (until round 4: [q][slot (n + q) mod 16], data-dependent conflicts) */
-    for (int e = tid - t0; win && e >= 0 && e < 32 * 16; e += nt) {
-        const int q = e & 31, n = e >> 5; /* consecutive threads: consecutive slots of a row (conflict-free stores) */
+    /* win (no tree): the lane combination's shared window tables in the tree area, rows n < 16 of win_row(G) slots, slot
+     * q * CP + c = n * H^(q + 1) for q < G (CP = win_copies(G) copies, one per record of a 16-lane group when G < 16), in
+     * gf_win4_mul's big-endian words (gf_win4_build's entries, shared by every lane of the workgroup whose record position
+     * is q).  A lookup's 16-lane group then reads 16 distinct slots of its row, whatever the nibbles (until round 4, for
+     * G = 32 only: [q][slot (n + q) mod 16], data-dependent conflicts) */
+    const int wrow = win_row(1 << log2g), wcp = win_copies(1 << log2g);
+    for (int e = tid - t0; win && e >= 0 && e < 16 * wrow; e += nt) {
+        const int sl = e % wrow, q = sl / wcp, n = e / wrow; /* consecutive threads: consecutive slots (conflict-free stores) */
         const uint32_t *hp = basis + (NPOW * 128 + q) * 4; /* H^(q + 1) */
         uint32_t m[4] = {bswap32(hp[0]), bswap32(hp[1]), bswap32(hp[2]), bswap32(hp[3])}, acc[4] = {0, 0, 0, 0};
 #pragma unroll
@@ -988,7 +1001,7 @@ __device__ void build_ghash_tables(uint8_t *lds, const uint32_t *__restrict__ ba
                     acc[w] ^= m[w];
             mulx_be(m);
         }
-        lds128_store(lds, LDS_GTREE + (uint32_t)n * 512u + (uint32_t)q * 16u, V4{acc[0], acc[1], acc[2], acc[3]});
+        lds128_store(lds, LDS_GTREE + (uint32_t)(n * wrow + sl) * 16u, V4{acc[0], acc[1], acc[2], acc[3]});
     }
 }
 
@@ -1315,7 +1328,8 @@ __global__ void __launch_bounds__(WGT)
     constexpr bool DYN = DYN_DEAL != 0 && SPLIT_PROBE != 1; /* the counter is reset at key switches, which SPLIT_PROBE 1 skips */
     /* G = 32: the lane combination by 4-bit windows over a per-key table of H^1..H^32 in the (unused) tree area instead of
      * gf_mul_valu's 1 408 VALU per lane (G32_WIN = 0: the VALU multiply) */
-    constexpr bool WINCOMB = G >= 32 && VALU_TREE == 0 && G32_WIN != 0;
+    constexpr bool VCOMB = VALU_TREE != 0 || G >= 32 || (WIN_ALL != 0 && G >= 2);
+    constexpr bool WINCOMB = VCOMB && VALU_TREE == 0 && G32_WIN != 0;
     constexpr bool SPLIT = SPLIT_TASKS != 0 && G >= 16 && DYN && SPLIT_PROBE == 0 && HYBRID == 0 && KEYSWITCH_PROBE == 0;
     constexpr uint32_t LDS_SPLIT = lds_bytes(LOG2G) + 16;                 /* partials: [slot][part] 16 B each */
     constexpr uint32_t LDS_SPLIT_CTR = LDS_SPLIT + SPLIT_SLOTS * 32;      /* arrival counters: [slot] */
@@ -1419,7 +1433,7 @@ __global__ void __launch_bounds__(WGT)
             __syncthreads();
             const uint64_t s1 = KS_STAMPS ? __builtin_amdgcn_s_memtime() : 0;
             if (KEYSWITCH_PROBE != 1 || cur_key == 0xffffffffu)
-                build_ghash_tables(lds, basis + (size_t)ch.key * (BASIS_VECS * 4), LOG2G, !(VALU_TREE != 0 || G >= 32), WINCOMB);
+                build_ghash_tables(lds, basis + (size_t)ch.key * (BASIS_VECS * 4), LOG2G, !VCOMB, WINCOMB);
             if (DYN && threadIdx.x == 0)
                 *task_ctr = 0;
             if (SPLIT)
@@ -1731,15 +1745,15 @@ __global__ void __launch_bounds__(WGT)
              * from the end of the GHASH input; sum_q y_q * H^(q+1).  G <= 16: a log2(G)-level shuffle tree over
              * nibble tables of H, H^2, H^4 in LDS; G = 32 (or VALU_TREE): one VALU multiply per lane by its own
              * power H^(q+1) (keysetup's list) and an XOR butterfly over the record's lanes */
-            constexpr bool VCOMB = VALU_TREE != 0 || G >= 32;
             const int q = (e_hi - 1 - na - r) & (G - 1); /* (nc - r) mod G for a whole record or a part B */
             V4 s; /* the record's GHASH (VCOMB: in every lane; tree: computed below in lane q == 0) */
             if constexpr (VCOMB) {
                 s = V4{0, 0, 0, 0};
                 if (SPLIT_PROBE != 1) {
                     if constexpr (WINCOMB) { /* the key's shared window table of H^(q+1) (build_ghash_tables) */
-                        Win4<16, 512> wt;
-                        wt.base = LDS_GTREE + (uint32_t)q * 16u;
+                        constexpr int WCP = win_copies(G);
+                        Win4<16, 16 * win_row(G)> wt;
+                        wt.base = LDS_GTREE + (uint32_t)(q * WCP + (grp & (WCP - 1))) * 16u;
                         s = gf_win4_mul<16, 4>(lds, wt, y);
                     } else {
                         const uint4 hp = reinterpret_cast<const uint4 *>(basis)[(size_t)ch.key * BASIS_VECS + NPOW * 128 + q]; /* H^(q+1) */

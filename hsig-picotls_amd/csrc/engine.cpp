@@ -578,7 +578,11 @@ static int choose_lanes(const ptls_hip_record_t *recs, size_t n)
     }
     const double mean = sum / (double)n;
     const double per_run = (double)n / (double)runs;
-    const int g = mean >= 128 ? 8 : mean >= 48 ? 4 : mean >= 16 ? 2 : 1;
+    /* round 4 (the windowed lane combination for every G, batch_kernel.h WIN_ALL): G = 4 is as fast as G = 8 or faster at
+     * every length with long key runs (seal GiB/s G = 4 / 8, same box, tools/calls_r04/r04_call28.sh: 3 000 B 1 183 / 1 151,
+     * 4 096 B 1 220 / 1 188, 8 192 B 1 215 / 1 222, c2's 16 KiB 1 258 / 1 250; 2 000 B 1 154-1 163 / 1 101; c3 G = 2 / 4
+     * within 1 %).  Until then G = 8 from 128 GHASH elements (the tree's cost grew with log2 G differently) */
+    const int g = mean >= 48 ? 4 : mean >= 16 ? 2 : 1;
     /* key runs too short to amortise the per-key GHASH tables: the key-independent wave-per-record kernel */
     if (per_run < SPARSE_MAX_PER_RUN)
         return SPARSE_LANES;
@@ -588,10 +592,14 @@ static int choose_lanes(const ptls_hip_record_t *recs, size_t n)
      * GiB/s at 8 / 16 / 32 lanes, round 3 (the G = 32 window combination): 64 records per key 532 / 769 / 803, 96: 748 /
      * 813 / 620, 128: 810 / 827 / 804, 192: 838 / 644 / 806 (tools/calls_r03/r03_call17.sh); round 2 at 16 / 32 lanes
      * (sparse kernel): 8 per key 126 / 258 (503), 16: 260 / 499 (516), 24: 394 / 681 (525), 32: 518 / 715, 48: 717 / 734. */
-    if (g == 8 && mean >= 256 && per_run <= 64)
+    if (mean >= 256 && per_run <= 64)
         return 32;
-    if (g == 8 && mean >= 256 && per_run <= 128)
+    if (mean >= 256 && per_run <= 128)
         return 16;
+    /* a run of up to 512 records is at most 32 wave tasks at G = 4 for 12 waves: G = 8 doubles them (c4's lengths at ~210
+     * records per key: G = 8 883, G = 16 851 GiB/s seal, r04_call26.sh) */
+    if (mean >= 256 && per_run <= 512)
+        return 8;
     return g;
 }
 

@@ -22,7 +22,7 @@ MUTANTS = os.path.join(os.path.dirname(HERE), "hsig-picotls_amd", "mutants")
 
 
 @pytest.mark.parametrize("key_len", [16, 32])
-@pytest.mark.parametrize("lanes", [8, 16, 32])
+@pytest.mark.parametrize("lanes", [4, 8, 16, 32])
 def test_cross_chunk_dealing_parity(engine, oracle, lanes, key_len):
     assert dealing_case.mismatches(engine, oracle, key_len, lanes) == (0, 0)
 
