@@ -596,9 +596,10 @@ static int choose_lanes(const ptls_hip_record_t *recs, size_t n)
         return 32;
     if (mean >= 256 && per_run <= 128)
         return 16;
-    /* a run of up to 512 records is at most 32 wave tasks at G = 4 for 12 waves: G = 8 doubles them (c4's lengths at ~210
-     * records per key: G = 8 883, G = 16 851 GiB/s seal, r04_call26.sh) */
-    if (mean >= 256 && per_run <= 512)
+    /* a run of up to 320 records is at most 20 wave tasks at G = 4 for 12 waves: G = 8 doubles them.  c4's lengths, seal
+     * GiB/s G = 4 / 8 / 16 (tools/calls_r04/r04_call26.sh, r04_call30.sh): ~210 records per key 822 / 893 / 851, ~420 per
+     * key 898 / 869 / -, one key 932 / 927 / - */
+    if (mean >= 256 && per_run <= 320)
         return 8;
     return g;
 }
