@@ -824,6 +824,10 @@ __device__ __forceinline__ Win4<NT> gf_win4_build(uint8_t *lds, uint32_t tab, in
         mulx_be(m[k]);
     }
     Win4<NT> t;
+    /* the entries start from an opaque zero: a plain {0, 0, 0, 0} for T[0] was hoisted out of the record loop as one zero
+     * vector and spilled (a 16-byte scratch reload per record in the sparse kernel) */
+    uint32_t zero;
+    asm volatile("v_mov_b32 %0, 0" : "=v"(zero));
     uint32_t ln = (uint32_t)lane;
     asm volatile("" : "+v"(ln)); /* keeps the lane's slot arithmetic here: hoisted out of a record loop, its values stay
                                     live across the whole kernel (the sparse batch kernel spilled 200 B per lane) */
@@ -833,7 +837,7 @@ __device__ __forceinline__ Win4<NT> gf_win4_build(uint8_t *lds, uint32_t tab, in
         t.y[w] = m[0][w];
 #pragma unroll
     for (int n = 0; n < NT; ++n) {
-        uint32_t e[4] = {0, 0, 0, 0};
+        uint32_t e[4] = {zero, zero, zero, zero};
 #pragma unroll
         for (int k = 0; k < 4; ++k)
             if ((n >> (3 - k)) & 1)

@@ -291,8 +291,9 @@ __device__ __forceinline__ void sparse_record(uint8_t *lds, int lane, uint32_t l
     /* everything derived from the lane index is computed per record: hoisted out of the kernel's record loop, such values
      * (partner lanes, table slots, negative lane offsets) stayed live across the whole kernel and went to scratch, which
      * the streaming records then evicted to HBM (c4s: 84 B per lane, +4.9 KB of HBM traffic per record) */
-    lane = (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)); /* recomputed, not carried across records */
-    asm volatile("" : "+v"(lane));
+    /* recomputed, not carried across records: a volatile asm, because the compiler hoists the mbcnt builtins out of the
+     * record loop and under the register pressure spilled their value, one scratch reload and wait per record (round 4) */
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lane));
     const int vl = 64 * vw + lane; /* the virtual lane (S = 64: the lane) */
     const uint32_t key = __builtin_amdgcn_readfirstlane(rec.key);
     const KeySlot *__restrict__ slot = slots + key;
