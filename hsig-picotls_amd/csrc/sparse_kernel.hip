@@ -235,7 +235,8 @@ __device__ __forceinline__ void store_wave_table(uint8_t *lds, uint32_t tab, V4 
                         + 8 / 16 stores + 32 lookups), 0 = gf_mul_valu (1 408 VALU) */
 #endif
 #ifndef SPARSE_WIN_LB
-#define SPARSE_WIN_LB 4 /* the batch instantiations' lookups in flight per group (8: 32 VGPRs, spills at 168) */
+#define SPARSE_WIN_LB 8 /* the batch instantiations' lookups in flight per group (8 spilled at 168 VGPRs until the round-4 spill fix; now
+                          * the same 12 B of scratch as 4, c4s seal +0.3 %, open +0.7 %: profiles/r04_c4s_win_lb8_ab.log) */
 #endif
 
 /* the wave's maximum / XOR sum in every lane: batch_kernel.h's DPP + permlane reduction (no LDS instruction, no partner
