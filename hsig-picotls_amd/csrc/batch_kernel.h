@@ -948,7 +948,10 @@ __host__ __device__ constexpr int win_copies(int g) { return g >= 16 ? 1 : 16 / 
 __device__ void build_ghash_tables(uint8_t *lds, const uint32_t *__restrict__ basis, int log2g, bool tree = true, bool win = false)
 {
     const uint32_t *bm = basis + log2g * 128 * 4;
-    const int tid = (int)threadIdx.x;
+    /* the thread index made opaque: otherwise its addresses (basis vectors, table slots) are hoisted out of the kernel's
+     * chunk loop and spilled, and every key switch reloads them from scratch after its barrier (round 4) */
+    int tid = (int)threadIdx.x;
+    asm volatile("" : "+v"(tid));
     if (tid < 256) {
         const int p = tid & 15, hv = tid >> 4;
         V4 lb[4];
