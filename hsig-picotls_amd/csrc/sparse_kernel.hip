@@ -57,6 +57,11 @@ namespace ptls_hip {
 #define SPARSE_HPPF 0 /* batch records: the lane's power H^(q+1) for the combination is loaded after the stretch, under the tail
                        * elements, instead of at the combination (measured neutral: 516 / 521 against 517 / 524 GiB/s) */
 #endif
+#ifndef SPARSE_CTR_WAVE
+#define SPARSE_CTR_WAVE 0 /* 1: a record's counter-mode constants by one lookup per lane (ctr_const_wave): 2 LDS instructions instead
+                           * of 22; bit-exact (GPU suite green on it) but no faster: c4s seal 512-516 against 517-519 (same box,
+                           * profiles/r04_c4s_ctr_wave_ab.log) */
+#endif
 #ifndef SPARSE_BASISPF
 #define SPARSE_BASISPF 0 /* batch records: the H^64 basis loads go out before the counter-mode constants (as the single record's;
                           * measured neutral: 518 / 521 against 517 / 524 GiB/s).  Touching the next record's key slot, basis
@@ -239,6 +244,57 @@ __device__ __forceinline__ void store_wave_table(uint8_t *lds, uint32_t tab, V4 
                           * the same 12 B of scratch as 4, c4s seal +0.3 %, open +0.7 %: profiles/r04_c4s_win_lb8_ab.log) */
 #endif
 
+/* The counter-mode constants of a record the whole wave works on (ctr_const's values, wave-uniform): lane i < 14 makes
+ * round 1's lookup i and lane i < 8 round 2's, one ds_read_b32 per round instead of 14 + 8, and the sums are gathered
+ * with v_readlane.  ctr_const issues 22 dependent-by-round LDS instructions into a command queue the other waves keep
+ * full; this issues 2.  Per lane (bit i of each mask): the state word (two bits), its byte (two bits), T2 instead of T0,
+ * and a rotation by 8 (T1 = rotl8 T0, T3 = rotl8 T2).  The sparse kernel's tables sit at LDS offset 0. */
+__device__ __forceinline__ uint32_t ctr_lookup(const uint8_t *lds, uint32_t lb, int ln, uint32_t w0, uint32_t w1, uint32_t w2,
+                                               uint32_t w3, uint32_t mw0, uint32_t mw1, uint32_t mk0, uint32_t mk1, uint32_t mt2,
+                                               uint32_t mrot)
+{
+    const uint32_t b = 1u << (ln & 31); /* lanes 14-31 take a valid dummy lookup, lanes 32-63 repeat 0-31 (not read) */
+    const uint32_t x = (mw1 & b) ? ((mw0 & b) ? w3 : w2) : ((mw0 & b) ? w1 : w0);
+    const uint32_t k = ((mk0 & b) ? 1u : 0u) + ((mk1 & b) ? 2u : 0u);
+    const uint32_t byte = __builtin_amdgcn_ubfe(x, 8u * k, 8u);
+    const uint32_t v = lds32(lds, (byte << 8) | (lb & 0x7fu) | ((mt2 & b) ? 128u : 0u));
+    return (mrot & b) ? rotl8(v) : v;
+}
+
+__device__ __forceinline__ CtrConst ctr_const_wave(const uint8_t *lds, uint32_t lb, const uint32_t *__restrict__ rk,
+                                                   uint32_t n0, uint32_t n1, uint32_t n2)
+{
+    int ln;
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(ln));
+    const uint32_t s0 = n0 ^ rk[0], s1 = n1 ^ rk[1], s2 = n2 ^ rk[2], s3 = rk[3]; /* counter bytes 12, 13 = 0 */
+    /* round 1, lanes 0-13: k10 = T0[s0.0] ^ T1[s1.1] ^ T2[s2.2], k11 = T0[s1.0] ^ T1[s2.1] ^ T3[s0.3],
+     * t2 = T0[s2.0] ^ T1[s3.1] ^ T2[s0.2] ^ T3[s1.3], t3 = T0[s3.0] ^ T1[s0.1] ^ T2[s1.2] ^ T3[s2.3] */
+    /* per-lane masks (word bit 0, word bit 1, byte bit 0, byte bit 1, T2, rotl8) for the 14 lookups in the order above */
+    const uint32_t r1 = ctr_lookup(lds, lb, ln & 63, s0, s1, s2, s3, 0x168au, 0x24d4u, 0x2ab2u, 0x3324u, 0x3324u, 0x2ab2u);
+    uint32_t v[14];
+#pragma unroll
+    for (int i = 0; i < 14; ++i)
+        v[i] = (uint32_t)__builtin_amdgcn_readlane((int)r1, i);
+    CtrConst c;
+    c.r03 = rk[3];
+    c.k10 = v[0] ^ v[1] ^ v[2] ^ rk[4];
+    c.k11 = v[3] ^ v[4] ^ v[5] ^ rk[5];
+    const uint32_t t2 = v[6] ^ v[7] ^ v[8] ^ v[9] ^ rk[6];
+    const uint32_t t3 = v[10] ^ v[11] ^ v[12] ^ v[13] ^ rk[7];
+    /* round 2, lanes 0-7 (w 0 = t2, 1 = t3): k20 = T2[t2.2] ^ T3[t3.3], k21 = T1[t2.1] ^ T2[t3.2],
+     * k22 = T0[t2.0] ^ T1[t3.1], k23 = T0[t3.0] ^ T3[t2.3] */
+    const uint32_t r2 = ctr_lookup(lds, lb, ln & 63, t2, t3, t2, t3, 0x6au, 0x0u, 0xa6u, 0x8bu, 0x8bu, 0xa6u);
+    uint32_t u[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+        u[i] = (uint32_t)__builtin_amdgcn_readlane((int)r2, i);
+    c.k20 = u[0] ^ u[1] ^ rk[8];
+    c.k21 = u[2] ^ u[3] ^ rk[9];
+    c.k22 = u[4] ^ u[5] ^ rk[10];
+    c.k23 = u[6] ^ u[7] ^ rk[11];
+    return c;
+}
+
 /* the wave's maximum / XOR sum in every lane: batch_kernel.h's DPP + permlane reduction (no LDS instruction, no partner
  * address; until round 4 a ds_bpermute butterfly whose partner addresses had to come from an opaque lane index, or the
  * compiler hoisted them out of the record loop into scratch) */
@@ -337,7 +393,7 @@ __device__ __forceinline__ void sparse_record(uint8_t *lds, int lane, uint32_t l
     if (horner && (by_value || SPARSE_BASISPF))
         load_wave_basis(bs + LOG2S * 128, lane, b); /* H^S */
     /* the record (and so its counter-mode constants) is the wave's alone: keep them in SGPRs */
-    CtrConst cc = ctr_const(lds, lb_aes, rk, n0, n1, n2);
+    CtrConst cc = SPARSE_CTR_WAVE ? ctr_const_wave(lds, lb_aes, rk, n0, n1, n2) : ctr_const(lds, lb_aes, rk, n0, n1, n2);
     cc.k10 = __builtin_amdgcn_readfirstlane(cc.k10);
     cc.k11 = __builtin_amdgcn_readfirstlane(cc.k11);
     cc.k20 = __builtin_amdgcn_readfirstlane(cc.k20);
@@ -655,7 +711,7 @@ __device__ __forceinline__ void mw_record(uint8_t *lds, int wave, int lane, uint
         const uint32_t n0 = __builtin_amdgcn_readfirstlane(ov ? ivo.x : slot->iv[0]),
                        n1 = __builtin_amdgcn_readfirstlane((ov ? ivo.y : slot->iv[1]) ^ bswap32((uint32_t)(rec.seq >> 32))),
                        n2 = __builtin_amdgcn_readfirstlane((ov ? ivo.z : slot->iv[2]) ^ bswap32((uint32_t)rec.seq));
-        CtrConst cc = ctr_const(lds, lb_aes, rk, n0, n1, n2);
+        CtrConst cc = SPARSE_CTR_WAVE ? ctr_const_wave(lds, lb_aes, rk, n0, n1, n2) : ctr_const(lds, lb_aes, rk, n0, n1, n2);
         cc.k10 = __builtin_amdgcn_readfirstlane(cc.k10);
         cc.k11 = __builtin_amdgcn_readfirstlane(cc.k11);
         cc.k20 = __builtin_amdgcn_readfirstlane(cc.k20);
