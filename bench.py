@@ -221,6 +221,26 @@ def _cpulist(text):
     return out
 
 
+def host_topology():
+    """sockets and physical cores of the whole host from sysfs (every CPU present, not only this process's share):
+    a core = a distinct (physical_package_id, core_id)"""
+    cores, sockets = set(), set()
+    base = "/sys/devices/system/cpu"
+    try:
+        names = [d for d in os.listdir(base) if d.startswith("cpu") and d[3:].isdigit()]
+    except OSError:
+        names = []
+    for d in names:
+        try:
+            with open(f"{base}/{d}/topology/physical_package_id") as f1, open(f"{base}/{d}/topology/core_id") as f2:
+                pkg, core = int(f1.read()), int(f2.read())
+        except (OSError, ValueError):
+            continue
+        sockets.add(pkg)
+        cores.add((pkg, core))
+    return dict(sockets=len(sockets) or None, physical_cores=len(cores) or None, logical_cpus=len(names) or None)
+
+
 def _steady(run_rep, min_reps=5, min_s=3.0, max_s=20.0, tol=0.10):
     """repeat run_rep() (-> GiB/s of one rep) until the last min_reps agree within tol of their median, or max_s;
     "noisy" says the spread bar was not met (a shared host: the GPU box grants a CPU share of a larger machine)"""
@@ -235,7 +255,7 @@ def _steady(run_rep, min_reps=5, min_s=3.0, max_s=20.0, tol=0.10):
                         spread=round(spread, 4), reps=len(rates), reps_used=len(last), noisy=bool(spread > tol))
 
 
-def cpu_baseline(cfg_name, cfg, dev=0):
+def cpu_baseline(cfg_name, cfg, dev=0, sample_bytes=1 << 30):
     """The reference's CPU engines (oracle/_ref, built unmodified from lib/fusion.c) on this host's cores: distinct record
     buffers of the config's shape (about 1 GiB, larger than the CPU caches, like the GPU's HBM-resident batch), the
     config's AAD form, one ptls_aead_context_t per pinned thread.  Two engines, the same bytes:
@@ -249,7 +269,7 @@ def cpu_baseline(cfg_name, cfg, dev=0):
     import ctypes
     from oracle_lib import Ref, ORACLE_SO
     L = cfg["L"] or 8224
-    nrec = max(64, (1 << 30) // L)
+    nrec = max(64, sample_bytes // L)
     stride = (L + 16 + 63) // 64 * 64
     aad_len = 5 if cfg["aad"] == "tls" else 13
     if not Ref.available:
@@ -331,6 +351,16 @@ def cpu_baseline(cfg_name, cfg, dev=0):
                       f"({on_node} of {threads} on the GPU's NUMA node {node}); median of 5 reps within "
                       f"{best['spread'] * 100:.1f} %, {threads} threads"
                       + (f" (the host's cgroup grants {quota:g} CPUs of the {n_aff} in the affinity mask)" if quota else ""))
+    topo = host_topology()
+    if topo["physical_cores"]:
+        # the measured value is the box's CPU share; what the whole host could do is only estimated here
+        res["full_host_extrapolation"] = dict(
+            gibps=round(res["single_core"] * topo["physical_cores"], 1), single_core=res["single_core"],
+            physical_cores=topo["physical_cores"], sockets=topo["sockets"], logical_cpus=topo["logical_cpus"],
+            kind="extrapolation, not a measurement",
+            note="one NUMA-local core's rate x every physical core of the host's sockets (sysfs topology); linear in the "
+                 "cores, so it ignores the host DRAM bandwidth the records stream through (every byte read once and "
+                 "written once per pass) and the clock drop with all cores busy: an upper estimate")
     if conf1 is not None:
         res["config1_ptlsbench_aad"] = dict(
             sample=f"BASELINE configs[0]: 4096 x 16384 B, 32-B AAD h[4] with h[0] = seq (t/ptlsbench.c:129-141), {best_name}",
@@ -435,23 +465,31 @@ def golden_check(cfg_name, idx, recs, d_ct):
     return checked
 
 
-def device_copy_gbs(nbytes=4 << 30, reps=5):
-    """achievable HBM bandwidth in this session: device-to-device copy of nbytes (read + write counted),
-    HIP events, median of reps (report against the measured device-copy bandwidth too)"""
+def device_copy_gbs(eng, nbytes=4 << 30, reps=5):
+    """achievable HBM bandwidth in this session (report against the measured device-copy bandwidth too):
+    ptls_hip_device_copy, a streaming copy kernel with 16 bytes per lane per access (the shape MI355X_MICROARCH.md
+    measures 6.29 TB/s with), of nbytes, read + write counted, HIP events on the launch stream, median of reps.  The torch
+    uint8 copy_ this used until round 4 read ~4.9 TB/s and overstated frac_of_measured_copy; it is kept beside it."""
     import torch
     src = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
     dst = torch.empty_like(src)
+    stream = torch.cuda.current_stream()
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
-    dst.copy_(src)
-    ts = []
-    for _ in range(reps):
-        ev[0].record()
-        dst.copy_(src)
-        ev[1].record()
-        torch.cuda.synchronize()
-        ts.append(ev[0].elapsed_time(ev[1]))
+
+    def timed(fn):
+        fn()
+        ts = []
+        for _ in range(reps):
+            ev[0].record(stream)
+            fn()
+            ev[1].record(stream)
+            torch.cuda.synchronize()
+            ts.append(ev[0].elapsed_time(ev[1]))
+        return round(2 * nbytes / (float(np.median(ts)) * 1e-3) / 1e9, 1)
+    kernel = timed(lambda: eng.copy(dst, src, nbytes, stream))
+    torch_copy = timed(lambda: dst.copy_(src))
     del src, dst
-    return round(2 * nbytes / (float(np.median(ts)) * 1e-3) / 1e9, 1)
+    return kernel, torch_copy
 
 
 def lds_issue_ceiling(key_len, clock_ghz):
@@ -681,6 +719,7 @@ def main():
     ap.add_argument("--lanes", type=int, default=0)
     ap.add_argument("--records", type=int, default=0, help="override records per GPU (smaller runs)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-sample-mib", type=int, default=1024, help="records in the CPU baseline's sample (default 1 GiB)")
     ap.add_argument("--no-e2e", action="store_true", help="skip the host-resident (pinned H2D/D2H) measurement")
     ap.add_argument("--no-plugin", action="store_true", help="skip the ptlsbench-shape plugin timing")
     ap.add_argument("--e2e-records", type=int, default=0, help="records in the host-resident sample (default: 1 GiB)")
@@ -880,8 +919,11 @@ def main():
                    "golden_records_checked_per_rank": [int(r[6]) for r in per_rank]},
     }
     report_ranks(result, per_rank, world, args.steps, elapsed)
-    copy_gbs = device_copy_gbs()
+    copy_gbs, torch_copy_gbs = device_copy_gbs(eng)
     result["roofline"]["measured_copy_gbs"] = copy_gbs
+    result["roofline"]["measured_copy_source"] = ("ptls_hip_device_copy: 16 B per lane per access, 4 GiB, read + write "
+                                                  "counted, HIP events, median of 5")
+    result["roofline"]["torch_uint8_copy_gbs"] = torch_copy_gbs
     result["roofline"]["frac_of_measured_copy"] = round(achieved / copy_gbs, 4)
     if batch_kernel:  # the batch kernel's LDS model (the sparse-key kernel is latency-bound)
         ceil = lds_issue_ceiling(cfg["key_len"], seal_ghz)
@@ -918,8 +960,15 @@ def main():
         dist.barrier()
     if rank == 0 and world == 1 and not args.no_plugin:
         result["plugin_ptlsbench"] = plugin_ptlsbench()
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        result["cpu_baseline"] = cpu_baseline(args.config, cfg, dev)
+    if not args.no_cpu_baseline:
+        # on rank 0 with every GPU idle: at N > 1 the other ranks wait at the barrier (an N > 1 line carries
+        # its own CPU baseline)
+        if world > 1:
+            dist.barrier()
+        if rank == 0:
+            result["cpu_baseline"] = cpu_baseline(args.config, cfg, dev, args.cpu_sample_mib << 20)
+        if world > 1:
+            dist.barrier()
     if rank == 0:
         print(json.dumps(result), flush=True)
     for o in (ks, eng):

@@ -108,9 +108,7 @@ __global__ void __launch_bounds__(64) aesecb_one_kernel(uint4 blk, const KeySlot
     }
 }
 
-#ifndef KEYSETUP_WIDE_MAX
-#define KEYSETUP_WIDE_MAX 4096 /* slots up to which key setup runs one wave per slot (keysetup_wide_kernel) */
-#endif
+constexpr uint32_t KEYSETUP_WIDE_MAX = 4096; /* slots up to which key setup runs one wave per slot (keysetup_wide_kernel) */
 
 /* ======================================================================================= *
  *  key setup: one thread per key slot (setup_crypto, lib/fusion.c:1184-1206, :984-1010)    *
@@ -244,10 +242,6 @@ __global__ void keysetup_kernel(KeySlot *slots, uint32_t *basis, const uint8_t *
         bs[NPOW * 128 + q] = make_uint4(pr.w0, pr.w1, pr.w2, pr.w3);
         pk = gf_mul_bitserial(pk, hh);
     }
-#if HYBRID
-    /* round keys 1..rounds in the bit-sliced form of the batch kernel's hybrid waves (bs8_aes.h) */
-    bs8::slice_key(w, rounds, reinterpret_cast<uint32_t *>(bs + BS_KEY_OFF));
-#endif
 }
 
 /* The same outputs with one 64-lane wave per key slot, for a few slots at a time (picotls's setup_crypto keys ONE
@@ -285,9 +279,6 @@ __global__ void __launch_bounds__(64) keysetup_wide_kernel(KeySlot *slots, uint3
             slot->hpow[t][2] = r.w2;
             slot->hpow[t][3] = r.w3;
         }
-#if HYBRID
-        bs8::slice_key(w, rounds, reinterpret_cast<uint32_t *>(bs + BS_KEY_OFF));
-#endif
     }
     for (int t = 0; t < NPOW; ++t) {
         const U128 v0 = gf_mul_xpow(pw[t], j), v1 = gf_mul_xpow(v0, 64);
@@ -370,6 +361,28 @@ __global__ void fill_records_kernel(const ptls_hip_record_t *recs, uint32_t n, u
     }
 }
 
+/* The achievable-HBM reference of bench.py's roofline (ptls_hip_device_copy): a plain streaming copy, 16 bytes per lane
+ * per access, four independent 16-byte loads in flight per lane before their stores (a grid-stride loop over 4 KiB
+ * per workgroup and step; MI355X_MICROARCH.md measures 6.29 TB/s with this shape, "float4 copy").  n16 = 16-byte units. */
+__global__ void __launch_bounds__(256) copy16_kernel(const uint4 *__restrict__ src, uint4 *__restrict__ dst, size_t n16)
+{
+    constexpr size_t U = 4;
+    const size_t stride = (size_t)gridDim.x * 256 * U;
+    size_t i = (size_t)blockIdx.x * 256 * U + threadIdx.x;
+    for (; i + (U - 1) * 256 < n16; i += stride) {
+        uint4 v[U];
+#pragma unroll
+        for (size_t k = 0; k < U; ++k)
+            v[k] = src[i + k * 256];
+#pragma unroll
+        for (size_t k = 0; k < U; ++k)
+            dst[i + k * 256] = v[k];
+    }
+    for (size_t k = 0; k < U; ++k) /* the last, partial step (one workgroup) */
+        if (i + k * 256 < n16)
+            dst[i + k * 256] = src[i + k * 256];
+}
+
 } // namespace ptls_hip
 
 /* ======================================================================================= *
@@ -421,6 +434,13 @@ int launch_fill(const ptls_hip_record_t *recs, uint32_t n, uint8_t *buf, uint64_
 {
     hipLaunchKernelGGL(fill_records_kernel, dim3(grid), dim3(256), 0, static_cast<hipStream_t>(stream), recs, n, buf, seed,
                        index_base, index);
+    return (int)hipGetLastError();
+}
+
+int launch_copy16(void *dst, const void *src, size_t n16, unsigned grid, void *stream)
+{
+    hipLaunchKernelGGL(copy16_kernel, dim3(grid), dim3(256), 0, static_cast<hipStream_t>(stream), static_cast<const uint4 *>(src),
+                       static_cast<uint4 *>(dst), n16);
     return (int)hipGetLastError();
 }
 

@@ -17,88 +17,40 @@
  *           p; lane l looks up byte p = (k + l) % 16 at step k, so the 16 lanes of every ds_read_b128
  *           lane group touch 16 distinct slots -> conflict-free; X is pre-rotated per lane so the
  *           byte for step k sits at a fixed position and the address is again one v_perm_b32.
- *   Record parallelism: G lanes share one record (Horner with stride G inside a lane, then a
- *           log2(G)-level shuffle tree with nibble tables for H, H^2, H^4), 64/G records per wave,
- *           8 waves per workgroup, workgroups persist over key-homogeneous chunks of records.
+ *   Record parallelism: G lanes share one record (Horner with stride G inside a lane, then every lane multiplies its
+ *           sum by its own power H^(q+1) from per-key 4-bit window tables in LDS and the record's lanes XOR their
+ *           products; G = 1 multiplies by H with a nibble table), 64/G records per wave task, 12 waves per workgroup drawing
+ *           tasks from an LDS counter, workgroups persist over key-homogeneous chunks taken from a device-wide queue.
+ * Rejected variants (bit-sliced waves, split records, the shuffle-tree combination, probes) are measured in EXPERIMENTS.md
+ * and are not in this source; the only build switches left are the TEST-ONLY dealing mutants and a diagnostic stamp.
  */
 #ifndef PTLS_HIP_BATCH_KERNEL_H
 #define PTLS_HIP_BATCH_KERNEL_H
 
 #include <hip/hip_runtime.h>
 #include "internal.h"
-#include "bs8_aes.h"
 
 namespace ptls_hip {
 
 /* ---------------- LDS map (bytes) ---------------- */
 constexpr uint32_t LDS_GMAIN = 0;            /* 64 KiB: row v (256 B) = 16 positions x 16 B, P = H^G       */
 constexpr uint32_t LDS_AES = 65536;          /* 64 KiB: row v = [T0 x32 lane slots | T2 x32 lane slots]  */
-constexpr uint32_t LDS_GTREE = 131072;       /* 3 x 8 KiB nibble tables for H^1, H^2, H^4: [p(32)][v(16)] */
+constexpr uint32_t LDS_GTREE = 131072;       /* the lane combination's tables: G = 1 the nibble table of H ([p(32)][v(16)],
+                                                8 KiB), G >= 2 the window tables of H^1 .. H^G (build_ghash_tables) */
 constexpr uint32_t LDS_TREE_STRIDE = 8192;
-constexpr int TREE_TABLES = 3; /* G = 16's level for H^8 multiplies by H^4 twice, so every G fits in 152 KiB */
+constexpr int TREE_TABLES = 3;
 __host__ __device__ constexpr uint32_t lds_bytes(int log2g)
 {
     return (void)log2g, LDS_GTREE + TREE_TABLES * LDS_TREE_STRIDE;
 }
 
-/* Tuning switches (defaults are the measured best):
- *   SKEWED       full-block loop with the lane's KP blocks 1/KP of a round apart (0: round-phased)
- *   SETPRIO      wave priority while a wave issues a segment's lookups;  PFPRIO  ... and its prefetch loads
- *   PURE_BLOCKS  KP, data blocks per lane per full-block iteration */
-#ifndef CTRHI_PROBE
-#define CTRHI_PROBE 0 /* timing probe only (wrong output): rounds 1-2 of the skewed loop as if the counter's high byte were fixed */
-#endif
-#ifndef SETPRIO
-#define SETPRIO 1 /* wave priority while issuing a segment's lookups: c2 +6 % measured */
-#endif
-#ifndef PFPRIO
-#define PFPRIO 0 /* priority for the prefetch loads too: measured no gain */
-#endif
-#ifndef GEN_SKEWED
-#define GEN_SKEWED 1 /* generic elements through ctr_ghash (counter-mode shortcut, skewed, prioritised): c3 +2 %, c4 +4 % */
-#endif
-#ifndef SKEWED
-#define SKEWED 1 /* ctr_ghash_skewed (the lane's KP blocks 1/KP of a round apart) */
-#endif
-#ifndef SPLIT_PROBE
-#define SPLIT_PROBE 0 /* timing ablation only: 1 = AES-CTR part alone, 2 = GHASH part alone (wrong output) */
-#endif
-#ifndef DYN_DEAL
-#define DYN_DEAL 1 /* waves draw tasks from a workgroup counter in LDS instead of a fixed per-chunk deal: c2 +3 %, c3 +5 %, c4 +5 % */
-#endif
-#ifndef WIN_ALL
-#define WIN_ALL 1 /* 1: every G >= 2 combines its record's partial sums like G = 32 (one windowed multiply per lane by H^(q+1)
-                     from shared per-key window tables, then an XOR over the record's lanes) instead of the log2(G)-level
-                     nibble-table tree and its final multiply by H (0): 32 table lookups + ~500 VALU per lane instead of
-                     (log2 G + 1) x 32 lookups in a dependent chain.  Same box (profiles/r04_win_all_ab.log): c3 seal
-                     1 118-1 135 -> 1 140-1 151, c2 +0.3-0.5 %, c4's lengths at ~105 records per key (G = 16) 858 -> 883 */
-#endif
-#ifndef G32_WIN
-#define G32_WIN 1 /* G = 32 lane combination: 1 = shared per-key window tables (gf_win4_mul), 0 = gf_mul_valu */
-#endif
-#ifndef VALU_TREE
-#define VALU_TREE 0 /* 1: combine a record's G partial sums by one VALU multiply per lane (H^(q+1) from the key slot's
-                       power table) and an XOR butterfly instead of the log2(G)-level LDS nibble-table tree.
-                       Parity-green, measured c2 / c4 equal and c3 -4 %; the sparse kernel uses it. */
-#endif
-#ifndef GEN_MASK
-#define GEN_MASK 0 /* 1: a generic element's AES runs under the exec mask of the lanes whose element is in the record */
-#endif
-#ifndef PURE_BLOCKS
-#define PURE_BLOCKS 2 /* data blocks per lane per iteration of the branch-free loop */
-#endif
-#ifndef KEYSWITCH_PROBE
-#define KEYSWITCH_PROBE 0 /* timing ablation only (wrong output): 1 = key switches keep their barriers but skip the table build;
-                           * 2 (with DYN_DEAL=0) = key switches after the first neither wait nor rebuild; 3 = the same with
-                           * dynamic dealing running on across keys */
-#endif
+/* measured constants (EXPERIMENTS.md) */
+constexpr int SETPRIO = 1;     /* wave priority while a wave issues a segment's lookups: c2 +6 % */
+constexpr int PURE_BLOCKS = 2; /* data blocks per lane per iteration of the branch-free loop */
 #ifndef DEAL_MUTANT
-#define DEAL_MUTANT 0 /* TEST-ONLY broken builds (tools/build_mutants.sh, tests/test_gpu_dealing.py): 1 = the task a wave
-                         drew past one chunk is dropped at the next chunk of the key run, 2 = cbase is not advanced */
-#endif
-#ifndef CHUNK_QUEUE
-#define CHUNK_QUEUE 1 /* workgroups take their chunks after the first from a device-wide queue (one returning atomic add per
-                         chunk) instead of the static grid stride blockIdx.x + k * gridDim.x */
+#define DEAL_MUTANT 0 /* TEST-ONLY broken builds (Makefile `mutants`, tests/test_gpu_dealing.py, tests/test_gpu_c4_keyruns.py):
+                         1 = the task a wave drew past one chunk is dropped at the next chunk of the key run, 2 = cbase is not
+                         advanced, 3 = the workgroup's task counter is not reset at a key switch (only at its first key) */
 #endif
 #ifndef KS_STAMPS
 #define KS_STAMPS 0 /* DIAGNOSTIC builds only (tools/keyswitch_stamps.py): every wave sums the shader cycles it spends at key
@@ -256,56 +208,11 @@ __device__ __forceinline__ CtrConst ctr_const(const uint8_t *lds, uint32_t lb, c
     return c;
 }
 
-/* AES of K counter blocks (n0, n1, n2, bswap(ctr_b)) with ctr_b < 2^16, using the per-record constants */
-template <int ROUNDS, int K>
-__device__ __forceinline__ void aes_ctr_n(const uint8_t *lds, uint32_t lb, const uint32_t *__restrict__ rk, const CtrConst &cc,
-                                          const uint32_t (&ctrw)[K], V4 (&s)[K])
-{
-#pragma unroll
-    for (int b = 0; b < K; ++b) {
-        const uint32_t x3 = ctrw[b] ^ cc.r03;                                     /* state column 3 after round 0 */
-        const uint32_t t0 = cc.k10 ^ rotl8(lT2<3>(lds, x3, lb));                  /* + T3[x3.b3] */
-        const uint32_t t1 = cc.k11 ^ lT2<2>(lds, x3, lb);                         /* + T2[x3.b2] */
-        s[b].w0 = xor3(cc.k20, lT0<0>(lds, t0, lb), rotl8(lT0<1>(lds, t1, lb)));  /* T0[t0.b0] ^ T1[t1.b1] */
-        s[b].w1 = xor3(cc.k21, lT0<0>(lds, t1, lb), rotl8(lT2<3>(lds, t0, lb)));  /* T0[t1.b0] ^ T3[t0.b3] */
-        s[b].w2 = xor3(cc.k22, lT2<2>(lds, t0, lb), rotl8(lT2<3>(lds, t1, lb)));  /* T2[t0.b2] ^ T3[t1.b3] */
-        s[b].w3 = xor3(cc.k23, rotl8(lT0<1>(lds, t0, lb)), lT2<2>(lds, t1, lb));  /* T1[t0.b1] ^ T2[t1.b2] */
-    }
-#pragma unroll
-    for (int r = 3; r < ROUNDS; ++r) {
-        const uint32_t k0 = rk[4 * r + 0], k1 = rk[4 * r + 1], k2 = rk[4 * r + 2], k3 = rk[4 * r + 3];
-        V4 t[K];
-#pragma unroll
-        for (int b = 0; b < K; ++b) {
-            t[b].w0 = aes_col(lds, lb, s[b].w0, s[b].w1, s[b].w2, s[b].w3, k0);
-            t[b].w1 = aes_col(lds, lb, s[b].w1, s[b].w2, s[b].w3, s[b].w0, k1);
-            t[b].w2 = aes_col(lds, lb, s[b].w2, s[b].w3, s[b].w0, s[b].w1, k2);
-            t[b].w3 = aes_col(lds, lb, s[b].w3, s[b].w0, s[b].w1, s[b].w2, k3);
-        }
-#pragma unroll
-        for (int b = 0; b < K; ++b)
-            s[b] = t[b];
-    }
-    const uint32_t k0 = rk[4 * ROUNDS + 0], k1 = rk[4 * ROUNDS + 1], k2 = rk[4 * ROUNDS + 2], k3 = rk[4 * ROUNDS + 3];
-    V4 t[K];
-#pragma unroll
-    for (int b = 0; b < K; ++b) {
-        t[b].w0 = aes_col_last(lds, lb, s[b].w0, s[b].w1, s[b].w2, s[b].w3, k0);
-        t[b].w1 = aes_col_last(lds, lb, s[b].w1, s[b].w2, s[b].w3, s[b].w0, k1);
-        t[b].w2 = aes_col_last(lds, lb, s[b].w2, s[b].w3, s[b].w0, s[b].w1, k2);
-        t[b].w3 = aes_col_last(lds, lb, s[b].w3, s[b].w0, s[b].w1, s[b].w2, k3);
-    }
-#pragma unroll
-    for (int b = 0; b < K; ++b)
-        s[b] = t[b];
-}
-
-/* ---------------- round-phased full-block iteration ----------------
- * The compiler, left alone, consumes each T-table lookup a few instructions after issuing it
- * (lgkmcnt(0..4) waits), so a wave keeps only a handful of LDS reads in flight and the LDS array idles
- * while the 12 waves of a CU wait on latency.  Here every AES round is one "phase": all lookups of the
- * round for the KP blocks of the lane (+ a quarter of one GHASH multiply) are issued first, then a
- * scheduling barrier, then all the XORs: 32-36 reads in flight per wave at every round boundary. */
+/* ---------------- the pieces of one round, issue and finish apart ----------------
+ * The compiler, left alone, consumes each T-table lookup a few instructions after issuing it (lgkmcnt(0..4) waits), so a
+ * wave keeps only a handful of LDS reads in flight and the LDS array idles while the 12 waves of a CU wait on latency.
+ * ctr_ghash_skewed issues a round's lookups (round_issue / last_issue), then XORs them (round_finish / last_finish) a
+ * segment later. */
 struct RoundLoads {
     uint32_t L[16];
 };
@@ -357,104 +264,8 @@ __device__ __forceinline__ V4 last_finish(const RoundLoads &r, const uint32_t *_
     return V4{t[0], t[1], t[2], t[3]};
 }
 
-/* forward declarations of the GHASH pieces (defined below) */
-struct GhLane;
-__device__ __forceinline__ V4 gh_rot(const GhLane &g, V4 y);
-template <int T0, int NT, int NG>
-__device__ __forceinline__ void gh_issue(const uint8_t *lds, const GhLane &g, const V4 &xr, V4 (&G)[NG]);
-
-/* Keystream of KP counter blocks (counter-mode shortcut for rounds 1-2, as aes_ctr_n) and, when HASH,
- * y <- (...(y * P ^ hx[0]) * P ^ ...) ^ hx[KP-1]: multiply j spread over phases 4j+1 .. 4j+4. */
-template <int ROUNDS, int KP, bool HASH>
-__device__ __forceinline__ void ctr_ghash_phased(const uint8_t *lds, uint32_t lb, const uint32_t *__restrict__ rk, const CtrConst &cc,
-                                                 const uint32_t (&cw)[KP], V4 (&ks)[KP], V4 &y, const V4 (&hx)[KP], const GhLane &g)
-{
-    /* phases per GHASH multiply (16 lookups each): as many as the rounds allow, a power of two */
-    constexpr int MPR = ROUNDS / KP;
-    constexpr int MP = MPR >= 8 ? 8 : MPR >= 4 ? 4 : MPR >= 2 ? 2 : 1;
-    constexpr int NT = 16 / MP; /* GHASH lookups per phase */
-    static_assert(MP * KP <= ROUNDS, "GHASH multiplies must fit in the AES phases");
-    V4 s[KP];
-    uint32_t t0[KP], t1[KP];
-    V4 acc = V4{0, 0, 0, 0}, xr = V4{0, 0, 0, 0};
-#pragma unroll
-    for (int p = 1; p <= ROUNDS; ++p) {
-        const bool gh = HASH && p <= MP * KP;
-        const int j = (p - 1) / MP, q = (p - 1) % MP;
-        RoundLoads R[KP];
-        uint32_t M[KP][8];
-        V4 G[8];
-        /* ---- issue ---- */
-        if (gh && q == 0) {
-            xr = gh_rot(g, y);
-            acc = hx[j];
-        }
-#pragma unroll
-        for (int b = 0; b < KP; ++b) {
-            if (p == 1) {
-                const uint32_t x3 = cw[b] ^ cc.r03;
-                M[b][0] = lT2<3>(lds, x3, lb);
-                M[b][1] = lT2<2>(lds, x3, lb);
-            } else if (p == 2) {
-                M[b][0] = lT0<0>(lds, t0[b], lb);
-                M[b][1] = lT0<1>(lds, t1[b], lb);
-                M[b][2] = lT0<0>(lds, t1[b], lb);
-                M[b][3] = lT2<3>(lds, t0[b], lb);
-                M[b][4] = lT2<2>(lds, t0[b], lb);
-                M[b][5] = lT2<3>(lds, t1[b], lb);
-                M[b][6] = lT0<1>(lds, t0[b], lb);
-                M[b][7] = lT2<2>(lds, t1[b], lb);
-            } else if (p < ROUNDS) {
-                round_issue(lds, lb, s[b], R[b]);
-            } else {
-                last_issue(lds, lb, s[b], R[b]);
-            }
-        }
-        if (gh) {
-            /* q is a constant once the phase loop is unrolled: the switch folds to one call */
-            switch (q) {
-            case 0: gh_issue<(0 * NT) & 15, NT>(lds, g, xr, G); break;
-            case 1: gh_issue<(1 * NT) & 15, NT>(lds, g, xr, G); break;
-            case 2: gh_issue<(2 * NT) & 15, NT>(lds, g, xr, G); break;
-            case 3: gh_issue<(3 * NT) & 15, NT>(lds, g, xr, G); break;
-            case 4: gh_issue<(4 * NT) & 15, NT>(lds, g, xr, G); break;
-            case 5: gh_issue<(5 * NT) & 15, NT>(lds, g, xr, G); break;
-            case 6: gh_issue<(6 * NT) & 15, NT>(lds, g, xr, G); break;
-            default: gh_issue<(7 * NT) & 15, NT>(lds, g, xr, G); break;
-            }
-        }
-        __builtin_amdgcn_sched_barrier(0);
-        /* ---- finish ---- */
-#pragma unroll
-        for (int b = 0; b < KP; ++b) {
-            if (p == 1) {
-                t0[b] = cc.k10 ^ rotl8(M[b][0]);
-                t1[b] = cc.k11 ^ M[b][1];
-            } else if (p == 2) {
-                s[b].w0 = xor3(cc.k20, M[b][0], rotl8(M[b][1]));
-                s[b].w1 = xor3(cc.k21, M[b][2], rotl8(M[b][3]));
-                s[b].w2 = xor3(cc.k22, M[b][4], rotl8(M[b][5]));
-                s[b].w3 = xor3(cc.k23, rotl8(M[b][6]), M[b][7]);
-            } else if (p < ROUNDS) {
-                s[b] = round_finish(R[b], rk + 4 * p);
-            } else {
-                ks[b] = last_finish(R[b], rk + 4 * p);
-            }
-        }
-        if (gh) {
-#pragma unroll
-            for (int i = 0; i + 1 < NT; i += 2)
-                acc = v4xor3(acc, G[i], G[i + 1]);
-            if (NT & 1)
-                acc = v4xor(acc, G[NT - 1]);
-            if (q == MP - 1)
-                y = acc;
-        }
-        __builtin_amdgcn_sched_barrier(0);
-    }
-}
-
-/* SKEWED=1 variant of ctr_ghash_phased: the lane's KP blocks run 1/KP of a round apart, so a wave always
+/* Keystream of KP counter blocks (the counter-mode shortcut for rounds 1-2, CtrConst) and, when HASH,
+ * y <- (...(y * P ^ hx[0]) * P ^ ...) ^ hx[KP-1].  The lane's KP blocks run 1/KP of a round apart, so a wave always
  * has lookups in flight while it XORs.  Segment s issues a quarter GHASH multiply (s < 4 KP) and round
  * s/KP+1 of block s%KP, then finishes the round that block (s-KP+1)%KP issued KP-1 segments earlier and
  * folds in the quarter multiply (its lookups go out first, so the fold does not wait for the AES ones).
@@ -477,9 +288,7 @@ __device__ __forceinline__ void ctr_ghash_skewed(const uint8_t *lds, uint32_t lb
     for (int seg = 0; seg < NSEG; ++seg) {
         const int gj = seg / P, gq = seg % P;
         const bool gh = HASH && gj < KP;
-#if SETPRIO
         __builtin_amdgcn_s_setprio(SETPRIO); /* a wave about to issue lookups goes first */
-#endif
         /* ---- issue: GHASH quarter first, then the AES lookups (so the fold below need not wait for them) ---- */
         if (gh) {
             if (gq == 0) {
@@ -503,13 +312,7 @@ __device__ __forceinline__ void ctr_ghash_skewed(const uint8_t *lds, uint32_t lb
             if (r == 1) {
                 const uint32_t x3 = cw[b] ^ cc.r03;
                 M[b][0] = lT2<3>(lds, x3, lb);
-                if (!CTRHI_PROBE)
-                    M[b][1] = lT2<2>(lds, x3, lb);
-            } else if (r == 2 && CTRHI_PROBE) {
-                M[b][0] = lT0<0>(lds, t0[b], lb);
-                M[b][3] = lT2<3>(lds, t0[b], lb);
-                M[b][4] = lT2<2>(lds, t0[b], lb);
-                M[b][6] = lT0<1>(lds, t0[b], lb);
+                M[b][1] = lT2<2>(lds, x3, lb);
             } else if (r == 2) {
                 M[b][0] = lT0<0>(lds, t0[b], lb);
                 M[b][1] = lT0<1>(lds, t1[b], lb);
@@ -526,22 +329,14 @@ __device__ __forceinline__ void ctr_ghash_skewed(const uint8_t *lds, uint32_t lb
             }
         }
         __builtin_amdgcn_sched_barrier(0);
-#if SETPRIO
         __builtin_amdgcn_s_setprio(0);
-#endif
         /* ---- finish ---- */
         if (seg >= KP - 1) {
             const int fs = seg - (KP - 1); /* the segment that issued the lookups finished here */
             const int b = fs % KP, r = fs / KP + 1;
             if (r == 1) {
                 t0[b] = cc.k10 ^ rotl8(M[b][0]);
-                if (!CTRHI_PROBE)
-                    t1[b] = cc.k11 ^ M[b][1];
-            } else if (r == 2 && CTRHI_PROBE) {
-                s[b].w0 = cc.k20 ^ M[b][0];
-                s[b].w1 = cc.k21 ^ rotl8(M[b][3]);
-                s[b].w2 = cc.k22 ^ M[b][4];
-                s[b].w3 = cc.k23 ^ rotl8(M[b][6]);
+                t1[b] = cc.k11 ^ M[b][1];
             } else if (r == 2) {
                 s[b].w0 = xor3(cc.k20, M[b][0], rotl8(M[b][1]));
                 s[b].w1 = xor3(cc.k21, M[b][2], rotl8(M[b][3]));
@@ -662,21 +457,7 @@ __device__ __forceinline__ V4 gh_mul_main(const uint8_t *lds, const GhLane &g, V
     return acc;
 }
 
-/* gh_mul_main with its 16 lookups in two halves of 8 (32 VGPRs in flight instead of 64) */
-__device__ __forceinline__ V4 gh_mul_main_halves(const uint8_t *lds, const GhLane &g, V4 y, V4 x)
-{
-    const V4 xr = gh_rot(g, y);
-    V4 acc = x, G[8];
-    gh_issue<0, 8>(lds, g, xr, G);
-    acc = v4xor3(acc, G[0], G[1]), acc = v4xor3(acc, G[2], G[3]), acc = v4xor3(acc, G[4], G[5]), acc = v4xor3(acc, G[6], G[7]);
-    __builtin_amdgcn_sched_barrier(0);
-    gh_issue<8, 8>(lds, g, xr, G);
-    acc = v4xor3(acc, G[0], G[1]), acc = v4xor3(acc, G[2], G[3]), acc = v4xor3(acc, G[4], G[5]), acc = v4xor3(acc, G[6], G[7]);
-    __builtin_amdgcn_sched_barrier(0);
-    return acc;
-}
-
-/* gh_mul_main in pieces for the phased loop: the lane rotation of y, then the 4 lookups of word Q */
+/* gh_mul_main in pieces for ctr_ghash_skewed (GhMain): the lane rotation of y, then the lookups of words T0 / 4 .. */
 __device__ __forceinline__ V4 gh_rot(const GhLane &g, V4 y)
 {
     const uint32_t s0 = g.rot1 ? y.w1 : y.w0, s1 = g.rot1 ? y.w2 : y.w1, s2 = g.rot1 ? y.w3 : y.w2, s3 = g.rot1 ? y.w0 : y.w3;
@@ -731,13 +512,10 @@ template <int ROUNDS, int KP, bool HASH>
 __device__ __forceinline__ void ctr_ghash(const uint8_t *lds, uint32_t lb, const uint32_t *__restrict__ rk, const CtrConst &cc,
                                           const uint32_t (&cw)[KP], V4 (&ks)[KP], V4 &y, const V4 (&hx)[KP], const GhLane &g)
 {
-    if constexpr (SKEWED)
-        ctr_ghash_skewed<ROUNDS, KP, HASH>(lds, lb, rk, cc, cw, ks, y, hx, GhMain{g});
-    else
-        ctr_ghash_phased<ROUNDS, KP, HASH>(lds, lb, rk, cc, cw, ks, y, hx, g);
+    ctr_ghash_skewed<ROUNDS, KP, HASH>(lds, lb, rk, cc, cw, ks, y, hx, GhMain{g});
 }
 
-/* y * P with a nibble table [p = 8w + j][v] (used only in the per-record reduction tree).  One word
+/* y * P with a nibble table [p = 8w + j][v] (the G = 1 multiply by H, the sparse kernel's Horner steps).  One word
  * (8 lookups) at a time: sched barriers keep the compiler from hoisting all 32 ds_read_b128 (128 VGPRs). */
 __device__ __forceinline__ V4 gh_mul_nibble(const uint8_t *lds, uint32_t table, V4 y)
 {
@@ -758,29 +536,6 @@ __device__ __forceinline__ V4 gh_mul_nibble(const uint8_t *lds, uint32_t table, 
     return acc;
 }
 
-/* x * y in GF(2^128), GCM bit order (SP 800-38D Algorithm 1), both operands per lane, on the VALU: 128 steps
- * of "Z ^= V if bit i of x; V = V * x^1" with 32-bit big-endian words (11 VALU per step) */
-__device__ __forceinline__ V4 gf_mul_valu(V4 xr, V4 yr)
-{
-    const uint32_t x[4] = {bswap32(xr.w0), bswap32(xr.w1), bswap32(xr.w2), bswap32(xr.w3)};
-    uint32_t v0 = bswap32(yr.w0), v1 = bswap32(yr.w1), v2 = bswap32(yr.w2), v3 = bswap32(yr.w3);
-    uint32_t z0 = 0, z1 = 0, z2 = 0, z3 = 0;
-#pragma unroll
-    for (int i = 0; i < 128; ++i) {
-        const uint32_t m = (uint32_t)__builtin_amdgcn_sbfe((int)x[i >> 5], 31u - (uint32_t)(i & 31), 1u); /* 0 or ~0 */
-        z0 = __builtin_amdgcn_bitop3_b32(z0, m, v0, 0x78); /* z ^ (m & v) */
-        z1 = __builtin_amdgcn_bitop3_b32(z1, m, v1, 0x78);
-        z2 = __builtin_amdgcn_bitop3_b32(z2, m, v2, 0x78);
-        z3 = __builtin_amdgcn_bitop3_b32(z3, m, v3, 0x78);
-        const uint32_t c = (uint32_t)__builtin_amdgcn_sbfe((int)v3, 0u, 1u); /* the bit shifted out */
-        v3 = __builtin_amdgcn_alignbit(v2, v3, 1);
-        v2 = __builtin_amdgcn_alignbit(v1, v2, 1);
-        v1 = __builtin_amdgcn_alignbit(v0, v1, 1);
-        v0 = (v0 >> 1) ^ (c & 0xe1000000u); /* R = 11100001 || 0^120 */
-    }
-    return V4{bswap32(z0), bswap32(z1), bswap32(z2), bswap32(z3)};
-}
-
 /* v * x in GF(2^128) on big-endian words (bit 0 of the GCM string = bit 31 of v[0]) */
 __device__ __forceinline__ void mulx_be(uint32_t (&v)[4])
 {
@@ -791,8 +546,8 @@ __device__ __forceinline__ void mulx_be(uint32_t (&v)[4])
     v[0] = (v[0] >> 1) ^ (c & 0xe1000000u);
 }
 
-/* x * y in GF(2^128), GCM bit order, both operands per lane: gf_mul_valu's product with 4-bit windows over x (Shoup)
- * and a per-lane table of y in LDS instead of 128 single-bit steps.
+/* x * y in GF(2^128), GCM bit order, both operands per lane: SP 800-38D Algorithm 1's product with 4-bit windows over x
+ * (Shoup) and a per-lane table of y in LDS instead of 128 single-bit steps (11 VALU each, 1 408 in all).
  *   T[n] = n3 y + n2 y x + n1 y x^2 + n0 y x^3 (n3 = the nibble's first GCM bit); entry n of lane l at
  *   tab + n * 1024 + l * 16 (STRIDE = 1024: a row of the 64 lanes' entries n), so the 16 lanes of every ds_read_b128 /
  *   ds_write_b128 group touch 16 consecutive 16-B slots, i.e. the 64 banks once, whatever the nibbles.  (Until round 4
@@ -801,7 +556,7 @@ __device__ __forceinline__ void mulx_be(uint32_t (&v)[4])
  *   NT = 8 holds T[0..7] and folds n3 y in on the VALU (8 KiB per wave: the sparse kernel's per-wave table area).
  *   Z = T[nib_31]; Z = Z x^4 + T[nib_j] for j = 30 .. 0.  The 4 bits each shift drops (positions 128..131) are
  *   collected in one overflow word and folded back every 8 shifts with x^128 = 1 + x + x^2 + x^7.
- * About 500 VALU + NT ds_write_b128 + 32 ds_read_b128 against gf_mul_valu's 1 408 VALU.  The caller owns the table
+ * About 500 VALU + NT ds_write_b128 + 32 ds_read_b128 against the bit-serial 1 408 VALU.  The caller owns the table
  * area; the wave's LDS operations complete in order, so no barrier is needed around it.  STRIDE = 512: the batch
  * kernel's shared G = 32 tables ([n][q], build_ghash_tables), base = the record position q's column. */
 template <int NT, int STRIDE = 1024>
@@ -945,7 +700,7 @@ __device__ __forceinline__ void build_aes_tables(uint8_t *lds, uint32_t base, co
 __host__ __device__ constexpr int win_row(int g) { return g > 16 ? g : 16; }
 __host__ __device__ constexpr int win_copies(int g) { return g >= 16 ? 1 : 16 / g; }
 
-__device__ void build_ghash_tables(uint8_t *lds, const uint32_t *__restrict__ basis, int log2g, bool tree = true, bool win = false)
+__device__ void build_ghash_tables(uint8_t *lds, const uint32_t *__restrict__ basis, int log2g)
 {
     const uint32_t *bm = basis + log2g * 128 * 4;
     /* the thread index made opaque: otherwise its addresses (basis vectors, table slots) are hoisted out of the kernel's
@@ -973,30 +728,30 @@ __device__ void build_ghash_tables(uint8_t *lds, const uint32_t *__restrict__ ba
             lds128_store(lds, LDS_GMAIN + (uint32_t)(16 * hv + lv) * 256u + (uint32_t)p * 16u, cur);
         }
     }
-    /* H^(2^d) for the tree levels d < log2 G (at most H^4); d = 0 (H) always */
-    const int ntree = !tree ? 0 : log2g < 1 ? 1 : log2g > TREE_TABLES ? TREE_TABLES : log2g;
     const int t0 = (int)blockDim.x > 256 ? 256 : 0, nt = (int)blockDim.x - t0;
-    for (int e = tid - t0; e >= 0 && e < ntree * 512; e += nt) {
-        const int d = e >> 9, p = (e >> 4) & 31, v = e & 15;
-        const int w = p >> 3, j = p & 7;
-        const uint32_t *bt = basis + d * 128 * 4;
-        V4 acc = V4{0, 0, 0, 0};
+    if (log2g == 0) { /* G = 1: the nibble table of H for the record's final multiply (gh_mul_nibble's layout) */
+        for (int e = tid - t0; e >= 0 && e < 512; e += nt) {
+            const int p = (e >> 4) & 31, v = e & 15;
+            const int w = p >> 3, j = p & 7;
+            V4 acc = V4{0, 0, 0, 0};
 #pragma unroll
-        for (int t = 0; t < 4; ++t) {
-            if ((v >> t) & 1) {
-                const int u = 4 * j + t; /* bit u of little-endian word w = raw byte 4w + u/8, bit u%8 */
-                acc = v4xor(acc, ld_basis(bt, 8 * (4 * w + (u >> 3)) + 7 - (u & 7)));
+            for (int t = 0; t < 4; ++t) {
+                if ((v >> t) & 1) {
+                    const int u = 4 * j + t; /* bit u of little-endian word w = raw byte 4w + u/8, bit u%8 */
+                    acc = v4xor(acc, ld_basis(basis, 8 * (4 * w + (u >> 3)) + 7 - (u & 7)));
+                }
             }
+            lds128_store(lds, LDS_GTREE + p * 256 + v * 16, acc);
         }
-        lds128_store(lds, LDS_GTREE + d * LDS_TREE_STRIDE + p * 256 + v * 16, acc);
+        return;
     }
-    /* win (no tree): the lane combination's shared window tables in the tree area, rows n < 16 of win_row(G) slots, slot
+    /* G >= 2: the lane combination's shared window tables, rows n < 16 of win_row(G) slots, slot
      * q * CP + c = n * H^(q + 1) for q < G (CP = win_copies(G) copies, one per record of a 16-lane group when G < 16), in
      * gf_win4_mul's big-endian words (gf_win4_build's entries, shared by every lane of the workgroup whose record position
      * is q).  A lookup's 16-lane group then reads 16 distinct slots of its row, whatever the nibbles (until round 4, for
      * G = 32 only: [q][slot (n + q) mod 16], data-dependent conflicts) */
     const int wrow = win_row(1 << log2g), wcp = win_copies(1 << log2g);
-    for (int e = tid - t0; win && e >= 0 && e < 16 * wrow; e += nt) {
+    for (int e = tid - t0; e >= 0 && e < 16 * wrow; e += nt) {
         const int sl = e % wrow, q = sl / wcp, n = e / wrow; /* consecutive threads: consecutive slots (conflict-free stores) */
         const uint32_t *hp = basis + (NPOW * 128 + q) * 4; /* H^(q + 1) */
         uint32_t m[4] = {bswap32(hp[0]), bswap32(hp[1]), bswap32(hp[2]), bswap32(hp[3])}, acc[4] = {0, 0, 0, 0};
@@ -1207,67 +962,6 @@ __device__ __forceinline__ int wave_max(int v)
     return (int)group_reduce<64>((uint32_t)v, MaxOp{});
 }
 
-/* Bit-sliced AES-CTR keystream of 8 counter blocks c0 + k * stride of one lane (bs8_aes.h, all on the VALU); the
- * lane's 8 data blocks src + k * src_stride are loaded during the last round, so they are not held through the group */
-template <int ROUNDS>
-__device__ __forceinline__ void bs8_ctr(const uint32_t *__restrict__ rk, const uint32_t *__restrict__ bk, uint32_t n0, uint32_t n1,
-                                        uint32_t n2, uint32_t c0, uint32_t stride, V4 (&ks)[8], const uint8_t *src, size_t src_stride,
-                                        V4 (&d)[8])
-{
-    uint32_t P[32];
-    bs8::ctr_planes(P, rk, n0, n1, n2, c0, stride);
-#pragma unroll
-    for (int r = 1; r <= ROUNDS; ++r) {
-        const uint32_t *Kr = bk + bs8::opaque_off(32 * (r - 1), P[0]);
-        bs8::sub_row<0>(P), bs8::sub_row<1>(P), bs8::sub_row<2>(P), bs8::sub_row<3>(P);
-        if (r == ROUNDS) {
-            asm volatile("" : "+v"(src) : "v"(P[0])); /* the loads go out after the last S-boxes, not earlier */
-#pragma unroll
-            for (int k = 0; k < 8; ++k)
-                d[k] = load_full(src + (size_t)k * src_stride);
-        }
-        bs8::shift_rows(P);
-        if (r < ROUNDS)
-            bs8::mix_columns_ark(P, Kr);
-        else
-            bs8::add_round_key(P, Kr);
-    }
-    uint32_t W[8][4];
-    bs8::from_planes(P, W);
-#pragma unroll
-    for (int k = 0; k < 8; ++k)
-        ks[k] = V4{W[k][0], W[k][1], W[k][2], W[k][3]};
-}
-
-/* y * P for the G lanes of one record group, all holding y: `plane` = basis plane of P (plane[e] = P * x^e, GCM bit e =
- * raw byte e / 8, bit 7 - e % 8); lane r XORs the vectors of bits [r 128 / G, (r + 1) 128 / G) of y (independent
- * loads, one memory latency), an XOR butterfly over the group sums them: every lane of the group gets y * P */
-template <int G>
-__device__ __forceinline__ V4 mul_by_plane(V4 y, const uint4 *__restrict__ plane, int r)
-{
-    constexpr int BPL = 128 / G;
-    const uint32_t w[4] = {y.w0, y.w1, y.w2, y.w3};
-    uint4 v[BPL];
-#pragma unroll
-    for (int k = 0; k < BPL; ++k)
-        v[k] = plane[r * BPL + k];
-    V4 acc = V4{0, 0, 0, 0};
-#pragma unroll
-    for (int k = 0; k < BPL; ++k) {
-        const int e = r * BPL + k, byte = e >> 3;
-        const uint32_t m = 0u - ((w[byte >> 2] >> (8 * (byte & 3) + 7 - (e & 7))) & 1u);
-        acc = V4{acc.w0 ^ (m & v[k].x), acc.w1 ^ (m & v[k].y), acc.w2 ^ (m & v[k].z), acc.w3 ^ (m & v[k].w)};
-    }
-#pragma unroll
-    for (int o = G / 2; o > 0; o >>= 1) {
-        acc.w0 ^= __shfl_xor(acc.w0, o, 64);
-        acc.w1 ^= __shfl_xor(acc.w1, o, 64);
-        acc.w2 ^= __shfl_xor(acc.w2, o, 64);
-        acc.w3 ^= __shfl_xor(acc.w3, o, 64);
-    }
-    return acc;
-}
-
 /* ======================================================================================= *
  *  batch seal / open                                                                       *
  * ======================================================================================= */
@@ -1331,36 +1025,26 @@ __global__ void __launch_bounds__(WGT)
 {
     constexpr int LOG2G = G == 1 ? 0 : G == 2 ? 1 : G == 4 ? 2 : G == 8 ? 3 : G == 16 ? 4 : 5;
     static_assert(G >= 1 && G <= 32 && (G & (G - 1)) == 0, "lanes per record: 1, 2, 4, 8, 16 or 32");
-    /* DYN_DEAL: the task counter sits after the tables; SPLIT (G >= 16): then the split-record slots */
-    constexpr bool DYN = DYN_DEAL != 0 && SPLIT_PROBE != 1; /* the counter is reset at key switches, which SPLIT_PROBE 1 skips */
-    /* G = 32: the lane combination by 4-bit windows over a per-key table of H^1..H^32 in the (unused) tree area instead of
-     * gf_mul_valu's 1 408 VALU per lane (G32_WIN = 0: the VALU multiply) */
-    constexpr bool VCOMB = VALU_TREE != 0 || G >= 32 || (WIN_ALL != 0 && G >= 2);
-    constexpr bool WINCOMB = VCOMB && VALU_TREE == 0 && G32_WIN != 0;
-    constexpr bool SPLIT = SPLIT_TASKS != 0 && G >= 16 && DYN && SPLIT_PROBE == 0 && HYBRID == 0 && KEYSWITCH_PROBE == 0;
-    constexpr uint32_t LDS_SPLIT = lds_bytes(LOG2G) + 16;                 /* partials: [slot][part] 16 B each */
-    constexpr uint32_t LDS_SPLIT_CTR = LDS_SPLIT + SPLIT_SLOTS * 32;      /* arrival counters: [slot] */
-    constexpr uint32_t LDS_QBASE = ((SPLIT ? LDS_SPLIT_CTR + SPLIT_SLOTS * 4 : lds_bytes(LOG2G) + (DYN ? 16 : 0)) + 7u) & ~7u;
-    /* QUEUE: a workgroup takes its chunks from a device-wide counter (queue[0]), one at a time, each claimed by the first
-     * of its waves that needs it; the waves walk the same chunk sequence, so the claimed chunk is left in an LDS ring for
-     * the others.  A workgroup that starts late (a CU still held by another kernel) or runs at a lower clock (the CUs of
-     * one XCD do not all hold the same clock under load) simply takes fewer chunks.  queue[1] counts the workgroups that
-     * have drawn past the end; the last one resets both words for the next launch that gets this slot (engine.cpp
-     * queue_slot). */
-    constexpr bool QUEUE = CHUNK_QUEUE != 0 && DYN && KEYSWITCH_PROBE == 0 && SPLIT_PROBE == 0;
+    /* the workgroup's task counter sits after the tables, then the chunk ring.  The chunks come from a device-wide counter
+     * (queue[0]), one at a time, each claimed by the first of the workgroup's waves that needs it; the waves walk the same
+     * chunk sequence, so the claimed chunk is left in an LDS ring for the others.  A workgroup that starts late (a CU still
+     * held by another kernel) or runs at a lower clock (the CUs of one XCD do not all hold the same clock under load)
+     * simply takes fewer chunks.  queue[1] counts the workgroups that have drawn past the end; the last one resets both
+     * words for the next launch that gets this slot (engine.cpp queue_slot).  queue == nullptr: the static grid stride. */
+    constexpr uint32_t LDS_QBASE = (lds_bytes(LOG2G) + 16 + 7u) & ~7u;
     constexpr int NW = WGT / 64;
     constexpr uint32_t LDS_QRING = LDS_QBASE;              /* uint64 [QRING]: position << 32 | chunk */
     constexpr uint32_t LDS_QCLAIM = LDS_QRING + QRING * 8; /* positions claimed so far */
     constexpr uint32_t LDS_QSEQ = LDS_QCLAIM + 4;          /* uint32 [NW]: positions each wave has entered */
-    constexpr uint32_t LDS_TOTAL = QUEUE ? LDS_QSEQ + NW * 4 : LDS_QBASE;
-    static_assert(LDS_TOTAL <= 163840, "tables + task counter + split slots + chunk ring must fit the CU's 160 KiB");
+    constexpr uint32_t LDS_TOTAL = LDS_QSEQ + NW * 4;
+    static_assert(LDS_TOTAL <= 163840, "tables + task counter + chunk ring must fit the CU's 160 KiB");
     __shared__ __attribute__((aligned(16))) uint8_t lds[LDS_TOTAL];
     uint32_t *const task_ctr = reinterpret_cast<uint32_t *>(lds + lds_bytes(LOG2G));
     constexpr int R = 64 / G; /* records per wave task */
 
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
-    const bool use_q = QUEUE && queue != nullptr;
+    const bool use_q = queue != nullptr;
     if (use_q) {
         for (int k = (int)threadIdx.x; k < QRING; k += WGT)
             reinterpret_cast<uint64_t *>(lds + LDS_QRING)[k] = ~0ull;
@@ -1424,28 +1108,20 @@ __global__ void __launch_bounds__(WGT)
     uint64_t ks_acc[5] = {0, 0, 0, 0, 0}; /* KS_STAMPS: total, barrier 1, build, barrier 2, switches */
     const uint64_t ks_t0 = KS_STAMPS ? __builtin_amdgcn_s_memtime() : 0;
     uint32_t cur_key = 0xffffffffu;
-    /* DYN: g = the wave's next task in the workgroup's same-key run of chunks (drawn, not yet used);
-     * cbase = tasks of the run's chunks before the current one; sbase = split tasks of those chunks (slot numbering) */
-    uint32_t g = 0, cbase = 0, sbase = 0;
+    /* g = the wave's next task in the workgroup's same-key run of chunks (drawn, not yet used); cbase = tasks of the run's
+     * chunks before the current one */
+    uint32_t g = 0, cbase = 0;
     bool have_g = false;
 
     for (uint32_t ci = use_q ? next_chunk() : blockIdx.x; ci < nchunks; ci = use_q ? next_chunk() : ci + gridDim.x) {
         const Chunk ch = chunks[ci];
-        if ((KEYSWITCH_PROBE == 2 || KEYSWITCH_PROBE == 3) && cur_key != 0xffffffffu && ch.key != cur_key) {
-            /* timing bound only: later key switches neither wait nor rebuild; with DYN (3) the workgroup's task counter
-             * and the waves' cursors run on across keys as across the chunks of one key run */
-            cur_key = ch.key;
-        } else if (SPLIT_PROBE != 1 && ch.key != cur_key) {
+        if (ch.key != cur_key) { /* a key switch: every wave is done with the old key's tables before they are rebuilt */
             const uint64_t s0 = KS_STAMPS ? __builtin_amdgcn_s_memtime() : 0;
             __syncthreads();
             const uint64_t s1 = KS_STAMPS ? __builtin_amdgcn_s_memtime() : 0;
-            if (KEYSWITCH_PROBE != 1 || cur_key == 0xffffffffu)
-                build_ghash_tables(lds, basis + (size_t)ch.key * (BASIS_VECS * 4), LOG2G, !VCOMB, WINCOMB);
-            if (DYN && threadIdx.x == 0)
+            build_ghash_tables(lds, basis + (size_t)ch.key * (BASIS_VECS * 4), LOG2G);
+            if (threadIdx.x == 0 && (DEAL_MUTANT != 3 || cur_key == 0xffffffffu))
                 *task_ctr = 0;
-            if (SPLIT)
-                for (int k = (int)threadIdx.x; k < SPLIT_SLOTS; k += WGT)
-                    reinterpret_cast<uint32_t *>(lds + LDS_SPLIT_CTR)[k] = 0;
             if (KS_STAMPS)
                 __builtin_amdgcn_s_waitcnt(0); /* the wave's own table stores are done: what remains is waiting for others */
             const uint64_t s2 = KS_STAMPS ? __builtin_amdgcn_s_memtime() : 0;
@@ -1459,7 +1135,6 @@ __global__ void __launch_bounds__(WGT)
             }
             cur_key = ch.key;
             cbase = 0;
-            sbase = 0;
             have_g = false; /* a task drawn past the old key's run belongs to no chunk */
         }
         if (DEAL_MUTANT == 1)
@@ -1467,39 +1142,24 @@ __global__ void __launch_bounds__(WGT)
 
         const KeySlot *__restrict__ slot = slots + ch.key;
         const uint32_t *__restrict__ rk = slot->rk;
-        /* tasks of the chunk: its first nsplit (longest) tasks are dealt as two part tasks each, part A then part B */
-        const int nsplit = SPLIT ? (int)((ch.flags >> 8) & 0xffu) : 0;
-        const int ntasks = (int)((ch.count + R - 1) / R) + nsplit;
+        const int ntasks = (int)((ch.count + R - 1) / R);
 
-        /* DYN: a wave draws its next task when it finishes one, across the chunks of a same-key run, in order
-         * (records sorted by decreasing length: longest first).  Waves on one SIMD do not progress equally
-         * (issue arbitration favours the older wave), so a fixed deal leaves the slowest wave on the critical
-         * path.  Otherwise: snake order over the chunk's tasks, the waves that drew the longest tasks in one
-         * pass draw the shortest ones in the next. */
-        for (int pass = 0;; ++pass) {
-            int t;
-            if (DYN) {
-                if (!have_g) {
-                    uint32_t v = 0;
-                    if (lane == 0)
-                        v = __hip_atomic_fetch_add(task_ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                    g = __builtin_amdgcn_readfirstlane(v);
-                    have_g = true;
-                }
-                t = (int)(g - cbase);
-                if (t >= ntasks)
-                    break; /* keep g for the next chunk of the run */
-                have_g = false;
-            } else {
-                t = pass * NW + ((pass & 1) ? NW - 1 - wave : wave);
-                if (t >= ntasks)
-                    break;
+        /* A wave draws its next task when it finishes one, across the chunks of a same-key run, in order (records sorted
+         * by decreasing length: longest first).  Waves on one SIMD do not progress equally (issue arbitration favours the
+         * older wave), so a fixed deal would leave the slowest wave on the critical path. */
+        for (;;) {
+            if (!have_g) {
+                uint32_t v = 0;
+                if (lane == 0)
+                    v = __hip_atomic_fetch_add(task_ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                g = __builtin_amdgcn_readfirstlane(v);
+                have_g = true;
             }
-            /* part: -1 = the whole record, 0 / 1 = part A / B of a split record; tt = the task's record group */
-            const bool is_part = SPLIT && t < 2 * nsplit;
-            const int part = is_part ? (t & 1) : -1;
-            const int tt = is_part ? (t >> 1) : t - nsplit;
-            const uint32_t ridx = (uint32_t)tt * R + grp;
+            const int t = (int)(g - cbase);
+            if (t >= ntasks)
+                break; /* keep g for the next chunk of the run */
+            have_g = false;
+            const uint32_t ridx = (uint32_t)t * R + grp;
             const bool valid = ridx < ch.count;
             /* descriptors in chunk order: the record is one load away (its caller index only matters for
              * result[] and supp[] at the end) */
@@ -1511,13 +1171,8 @@ __global__ void __launch_bounds__(WGT)
             const int na = (A + 15) >> 4, nc = (L + 15) >> 4;
             const int N = valid ? na + nc + 1 : 0;
             const int i0 = (r + na) & (G - 1);
-            /* the elements [e_lo, e_hi) this task handles; the lane's are i0 + m G for m in [m_lo, m_hi).  A split task's
-             * part B is the last B elements of every record of the task, B from the task's shortest record (its last
-             * record group: the chunk is sorted longest first), so both parts stay even across the task's records */
-            const int bsplit = is_part ? split_tail(__builtin_amdgcn_readlane(N, 64 - G)) : 0;
-            const int e_lo = is_part && part == 1 ? N - bsplit : 0, e_hi = is_part && part == 0 ? N - bsplit : N;
-            const int m_lo = e_lo > i0 ? ((e_lo - 1 - i0) >> LOG2G) + 1 : 0;
-            const int my_iters = e_hi > i0 ? ((e_hi - 1 - i0) >> LOG2G) + 1 : 0;
+            /* the lane's elements are i0 + m G for m < my_iters */
+            const int my_iters = N > i0 ? ((N - 1 - i0) >> LOG2G) + 1 : 0;
 
             /* seal of a TLS 1.3 record: the last plaintext byte is the content type, not input */
             const bool tflag = !OPEN && (rec.flags & 1u) != 0 && L > 0;
@@ -1532,7 +1187,7 @@ __global__ void __launch_bounds__(WGT)
             /* Iterations handle two Horner elements (i and i + G) of a lane; their AES blocks are independent
              * and run interleaved.  y = y * P ^ x is exact from y = 0 (0 * P = 0), so no first-element case. */
             /* counter-mode shortcut constants of this lane's record (rounds 1-2 of every block with counter < 2^16) */
-            CtrConst cc; /* computed after the stretch's bit-sliced part (not held through it) */
+            CtrConst cc; /* computed after the AAD elements (not held through them) */
 
             /* elements m and m + 1 of the lane (AAD, partial or full data, length block), their two AES blocks
              * interleaved; the counter-mode shortcut unless some lane of the wave has a counter >= 2^16 */
@@ -1543,7 +1198,7 @@ __global__ void __launch_bounds__(WGT)
                 int big = 0;
 #pragma unroll
                 for (int b = 0; b < 2; ++b) {
-                    e[b] = elem_of(i0 + (m + b) * G, N, na, nc, L, e_hi);
+                    e[b] = elem_of(i0 + (m + b) * G, N, na, nc, L, N);
                     in[b] = V4{0, 0, 0, 0};
                     if (e[b].is_c) {
                         const bool tb = tflag && e[b].c == nc - 1; /* the block holding the content-type byte */
@@ -1556,31 +1211,23 @@ __global__ void __launch_bounds__(WGT)
                     ks[b] = V4{n0, n1, n2, cw[b]};
                     big |= (e[b].is_c && e[b].c >= 65534) ? 1 : 0;
                 }
-                const bool bigw = wave_max(big) != 0; /* wave-wide, before any lane branches off */
-                const bool act = !GEN_MASK || e[0].active || e[1].active;
-                if (SPLIT_PROBE == 2 || !act) {
-                } else if (bigw)
+                if (wave_max(big) != 0) { /* wave-wide, before any lane branches off */
                     aes_encrypt_n<ROUNDS, 2>(lds, lb_aes, rk, ks);
-                else
-#if GEN_SKEWED
-                {
+                } else {
                     const V4 nohash[2] = {V4{0, 0, 0, 0}, V4{0, 0, 0, 0}};
                     V4 ydummy = V4{0, 0, 0, 0};
                     ctr_ghash<ROUNDS, 2, false>(lds, lb_aes, rk, cc, cw, ks, ydummy, nohash, gl);
                 }
-#else
-                    aes_ctr_n<ROUNDS, 2>(lds, lb_aes, rk, cc, cw, ks);
-#endif
 #pragma unroll
                 for (int b = 0; b < 2; ++b) {
                     const V4 x = finish_elem<OPEN, ALIGNED>(e[b], in[b], ks[b], aad_p, A, L, out_p, ek0);
-                    if (SPLIT_PROBE != 1 && e[b].active)
+                    if (e[b].active)
                         y = gh_mul_main(lds, gl, y, x);
                 }
             };
 
             auto generic_iter_m = [&](int m) {
-                const Elem e0 = elem_of(i0 + m * G, N, na, nc, L, e_hi);
+                const Elem e0 = elem_of(i0 + m * G, N, na, nc, L, N);
                 V4 in0 = V4{0, 0, 0, 0};
                 if (e0.is_c) {
                     const bool tb = tflag && e0.c == nc - 1; /* the block holding the content-type byte */
@@ -1591,18 +1238,15 @@ __global__ void __launch_bounds__(WGT)
                 /* keystream for data block c (counter inc32(J0) + c), E_K(J0) for the length-block lane */
                 const uint32_t cw0[1] = {e0.is_c ? bswap32((uint32_t)e0.c + 2u) : 0x01000000u};
                 V4 ks0[1] = {V4{n0, n1, n2, cw0[0]}};
-#if GEN_SKEWED
-                const bool big0 = wave_max((e0.is_c && e0.c >= 65534) ? 1 : 0) != 0;
-                if (SPLIT_PROBE == 2 || (GEN_MASK && !e0.active)) {
-                } else if (!big0) {
+                if (wave_max((e0.is_c && e0.c >= 65534) ? 1 : 0) == 0) {
                     const V4 nohash[1] = {V4{0, 0, 0, 0}};
                     V4 ydummy = V4{0, 0, 0, 0};
                     ctr_ghash<ROUNDS, 1, false>(lds, lb_aes, rk, cc, cw0, ks0, ydummy, nohash, gl);
-                } else
-#endif
+                } else {
                     aes_encrypt_n<ROUNDS, 1>(lds, lb_aes, rk, ks0);
+                }
                 const V4 x0 = finish_elem<OPEN, ALIGNED>(e0, in0, ks0[0], aad_p, A, L, out_p, ek0);
-                if (SPLIT_PROBE != 1 && e0.active)
+                if (e0.active)
                     y = gh_mul_main(lds, gl, y, x0);
             };
 
@@ -1611,67 +1255,30 @@ __global__ void __launch_bounds__(WGT)
              * GHASH lookups of the previous iteration's ciphertext can all be in flight together. */
             constexpr int KP = PURE_BLOCKS;
             const int nf = (L - (tflag ? 1 : 0)) >> 4; /* full blocks that are all input bytes */
-            /* the lane's AAD elements (m < my_mlo); a split record's part B has none (the planner splits past the AAD) */
-            const int my_mlo = is_part && part == 1 ? 0 : na > i0 ? (na - i0 + G - 1) >> LOG2G : 0;
+            /* the lane's AAD elements (m < pm0) */
+            const int pm0 = na > i0 ? (na - i0 + G - 1) >> LOG2G : 0;
             /* full blocks only, and (for the counter-mode shortcut) block counters c + 2 < 2^16 */
             const int lastc = min(nf, 65534) - 1; /* last data block index allowed in the pure stretch */
             const int my_mhi = min((valid && na + lastc - i0 >= 0) ? ((na + lastc - i0) >> LOG2G) + 1 : 0, my_iters);
-            /* Each lane starts the stretch at its own first data element (after its AAD elements, or at its first
-             * element of a part B), so the lanes without AAD do not spend a generic step on data block 0; the stretch
-             * length is the shortest lane's. */
-            const int pm0 = max(my_mlo, m_lo);
+            /* Each lane starts the stretch at its own first data element (after its AAD elements), so the lanes without AAD
+             * do not spend a generic step on data block 0; the stretch length is the shortest lane's. */
             const int npure = -wave_max(-max(my_mhi - pm0, 0)) / KP;
             const int pm1 = pm0 + npure * KP; /* per lane: first element after the stretch */
 
             /* AAD elements: GHASH only (no keystream); y = 0 * P ^ x = x for the first one */
-            const int naad = wave_max(my_mlo);
+            const int naad = wave_max(pm0);
             for (int j = 0; j < naad; ++j) {
-                if (SPLIT_PROBE != 1 && j < my_mlo) {
-                    const Elem e = elem_of(i0 + j * G, N, na, nc, L, e_hi);
+                if (j < pm0) {
+                    const Elem e = elem_of(i0 + j * G, N, na, nc, L, N);
                     const V4 x = load_block<ALIGNED>(aad_p + 16 * e.i, min(16, A - 16 * e.i));
                     y = j == 0 ? x : gh_mul_main(lds, gl, y, x);
                 }
             }
-            /* HYBRID: a bit-slicing wave runs the first 8 * (npure * KP / 8) elements of the stretch on the VALU */
-            int vdone = 0;
-#if HYBRID
-            if (wave >= NW - HYBRID && SPLIT_PROBE == 0) {
-                static_assert(8 % KP == 0, "a sliced group covers whole iterations of the table loop");
-                const int ngr = npure * KP / 8;
-                if (ngr > 0) {
-                    const size_t o0 = 16 * (size_t)(i0 - na + pm0 * G);
-                    const uint32_t c0 = (uint32_t)(i0 - na + pm0 * G) + 2u;
-                    const uint32_t *__restrict__ bk = basis + ((size_t)ch.key * BASIS_VECS + BS_KEY_OFF) * 4;
-                    for (int gi = 0; gi < ngr; ++gi) {
-                        const size_t o = o0 + (size_t)(8 * gi * G) * 16;
-                        V4 d[8], ks[8];
-                        bs8_ctr<ROUNDS>(rk, bk, n0, n1, n2, c0 + (uint32_t)(8 * gi * G), (uint32_t)G, ks, in_p + o, 16 * (size_t)G, d);
-                        /* GHASH right away (Horner with the main table): its LDS latency is exposed to this wave, but nothing
-                         * has to be held through the next group's rounds */
-#pragma unroll
-                        for (int k = 0; k < 8; ++k) {
-                            /* (open hashes d, which does not depend on the keystream: keep its multiplies after it) */
-                            asm volatile("" : "+v"(d[k].w0), "+v"(d[k].w1), "+v"(d[k].w2), "+v"(d[k].w3) : "v"(ks[k].w0));
-                            const V4 x = v4xor(d[k], ks[k]);
-                            store_full(out_p + o + 16 * (size_t)(k * G), x);
-                            if (!OPEN)
-                                d[k] = x; /* d = the GHASH input from here on */
-                        }
-#pragma unroll
-                        for (int k = 0; k < 8; ++k)
-                            y = gh_mul_main_halves(lds, gl, y, d[k]);
-                    }
-                    vdone = 8 * ngr;
-                }
-            }
-#endif
             cc = ctr_const(lds, lb_aes, rk, n0, n1, n2);
-            const int ntab = npure - vdone / KP; /* iterations left for the table loop */
-            if (ntab) {
-                const int pst = pm0 + vdone;
-                const uint8_t *src = in_p + 16 * (size_t)(i0 - na + pst * G);
-                uint8_t *dst = out_p + 16 * (size_t)(i0 - na + pst * G);
-                const uint32_t cbase = (uint32_t)(i0 - na + pst * G) + 2u;
+            if (npure) {
+                const uint8_t *src = in_p + 16 * (size_t)(i0 - na + pm0 * G);
+                uint8_t *dst = out_p + 16 * (size_t)(i0 - na + pm0 * G);
+                const uint32_t cbase = (uint32_t)(i0 - na + pm0 * G) + 2u;
                 V4 pend[KP], bufA[KP], bufB[KP];
                 /* ping-pong prefetch: iteration `it` consumes the buffer loaded one iteration earlier and refills
                  * the other one for it + 1 (clamped to the last iteration so the body stays branch-free).  Two
@@ -1682,12 +1289,9 @@ __global__ void __launch_bounds__(WGT)
                 /* one branch-free iteration; `hash_pending` is a literal at every call site */
                 auto pure_iter = [&](int it, bool hash_pending, V4(&d)[KP], V4(&dn)[KP]) {
                     const size_t o = (size_t)(it * KP * G) * 16;
-                    const size_t on = (size_t)(min(it + 1, ntab - 1) * KP * G) * 16;
+                    const size_t on = (size_t)(min(it + 1, npure - 1) * KP * G) * 16;
                     V4 k[KP];
                     uint32_t cw[KP];
-#if PFPRIO
-                    __builtin_amdgcn_s_setprio(PFPRIO); /* the prefetch loads issue with the first lookups */
-#endif
 #pragma unroll
                     for (int b = 0; b < KP; ++b) {
                         dn[b] = load_full(src + on + 16 * b * G);
@@ -1695,16 +1299,7 @@ __global__ void __launch_bounds__(WGT)
                         k[b] = V4{n0, n1, n2, cw[b]};
                     }
                     __builtin_amdgcn_sched_barrier(0); /* keep the prefetch at the top of the iteration */
-                    if (SPLIT_PROBE == 1) {
-                        ctr_ghash<ROUNDS, KP, false>(lds, lb_aes, rk, cc, cw, k, y, d, gl);
-#pragma unroll
-                        for (int b = 0; b < KP; ++b)
-                            store_full(dst + o + 16 * b * G, v4xor(d[b], k[b]));
-                    } else if (SPLIT_PROBE == 2) {
-#pragma unroll
-                        for (int b = 0; b < KP; ++b)
-                            y = gh_mul_main(lds, gl, y, d[b]);
-                    } else if (OPEN) {
+                    if (OPEN) {
                         /* the input is the ciphertext: hash it in the same iteration */
                         ctr_ghash<ROUNDS, KP, true>(lds, lb_aes, rk, cc, cw, k, y, d, gl);
 #pragma unroll
@@ -1725,13 +1320,13 @@ __global__ void __launch_bounds__(WGT)
                 };
                 pure_iter(0, false, bufA, bufB);
                 int it = 1;
-                for (; it + 1 < ntab; it += 2) {
+                for (; it + 1 < npure; it += 2) {
                     pure_iter(it, true, bufB, bufA);
                     pure_iter(it + 1, true, bufA, bufB);
                 }
-                if (it < ntab)
+                if (it < npure)
                     pure_iter(it, true, bufB, bufA);
-                if (!OPEN && SPLIT_PROBE == 0) {
+                if (!OPEN) {
 #pragma unroll
                     for (int b = 0; b < KP; ++b)
                         y = gh_mul_main(lds, gl, y, pend[b]);
@@ -1748,98 +1343,20 @@ __global__ void __launch_bounds__(WGT)
                     generic_iter_m(pm1 + j);
             }
 
-            /* combine the G partial sums of each record: position q = distance of a lane's last element
-             * from the end of the GHASH input; sum_q y_q * H^(q+1).  G <= 16: a log2(G)-level shuffle tree over
-             * nibble tables of H, H^2, H^4 in LDS; G = 32 (or VALU_TREE): one VALU multiply per lane by its own
-             * power H^(q+1) (keysetup's list) and an XOR butterfly over the record's lanes */
-            const int q = (e_hi - 1 - na - r) & (G - 1); /* (nc - r) mod G for a whole record or a part B */
-            V4 s; /* the record's GHASH (VCOMB: in every lane; tree: computed below in lane q == 0) */
-            if constexpr (VCOMB) {
-                s = V4{0, 0, 0, 0};
-                if (SPLIT_PROBE != 1) {
-                    if constexpr (WINCOMB) { /* the key's shared window table of H^(q+1) (build_ghash_tables) */
-                        constexpr int WCP = win_copies(G);
-                        Win4<16, 16 * win_row(G)> wt;
-                        wt.base = LDS_GTREE + (uint32_t)(q * WCP + (grp & (WCP - 1))) * 16u;
-                        s = gf_win4_mul<16, 4>(lds, wt, y);
-                    } else {
-                        const uint4 hp = reinterpret_cast<const uint4 *>(basis)[(size_t)ch.key * BASIS_VECS + NPOW * 128 + q]; /* H^(q+1) */
-                        s = gf_mul_valu(y, V4{hp.x, hp.y, hp.z, hp.w});
-                    }
-                    s = group_xor<G>(s); /* the sum over the record's G lanes (VALU_TREE at G < 32 too) */
-                }
-            } else {
-#pragma unroll
-                for (int lvl = 0; lvl < (SPLIT_PROBE == 1 ? 0 : LOG2G); ++lvl) {
-                    const int d = 1 << lvl;
-                    const int src = (lane & ~(G - 1)) | ((r - d) & (G - 1));
-                    V4 v;
-                    v.w0 = __shfl(y.w0, src, 64);
-                    v.w1 = __shfl(y.w1, src, 64);
-                    v.w2 = __shfl(y.w2, src, 64);
-                    v.w3 = __shfl(y.w3, src, 64);
-                    V4 w;
-                    if (lvl < TREE_TABLES) {
-                        w = gh_mul_nibble(lds, LDS_GTREE + lvl * LDS_TREE_STRIDE, v);
-                    } else { /* H^8 = H^4 * H^4 */
-                        const uint32_t t4 = LDS_GTREE + (TREE_TABLES - 1) * LDS_TREE_STRIDE;
-                        w = gh_mul_nibble(lds, t4, gh_mul_nibble(lds, t4, v));
-                    }
-                    if ((q & (2 * d - 1)) == 0)
-                        y = v4xor(y, w);
-                }
-            }
-            if (is_part) {
-                /* a part of a split record: part A's partial times H^B (N - e_hi = B = 2^t: basis plane t, the record's
-                 * G lanes multiply 128 / G bits each, then XOR-reduce); part B's XOR E_K(J0).  Both go to the record's
-                 * slot; the part arriving second sums them into the tag. */
-                if constexpr (!VCOMB)
-                    s = gh_mul_nibble(lds, LDS_GTREE, y); /* * H (meaningful in the q == 0 lane) */
-                V4 sp = s;
-                if (part == 0) {
-                    if constexpr (!VCOMB) { /* the q == 0 lane's value to the record's G lanes */
-                        const int src = (lane & ~(G - 1)) | ((e_hi - 1 - na) & (G - 1));
-                        sp = V4{__shfl(s.w0, src, 64), __shfl(s.w1, src, 64), __shfl(s.w2, src, 64), __shfl(s.w3, src, 64)};
-                    }
-                    sp = mul_by_plane<G>(sp, reinterpret_cast<const uint4 *>(basis) + (size_t)ch.key * BASIS_VECS +
-                                                 split_plane_of_tail(bsplit) * 128, r);
-                } else {
-                    sp = v4xor(sp, ek0);
-                }
-                if (valid && q == 0) {
-                    const uint32_t sl = (sbase + (uint32_t)tt) * R + (uint32_t)grp;
-                    lds128_store(lds, LDS_SPLIT + sl * 32u + (uint32_t)part * 16u, sp);
-                    /* the other part's ciphertext (header protection samples it) and partial are visible once its
-                     * counter increment is: release / acquire around the LDS atomic, workgroup scope (both parts run in
-                     * this workgroup, on this CU; agent scope would write back and invalidate the XCD's L2) */
-                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-                    const uint32_t arrived = __hip_atomic_fetch_add(reinterpret_cast<uint32_t *>(lds + LDS_SPLIT_CTR) + sl, 1u,
-                                                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                    if (arrived == 1) {
-                        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-                        const V4 tag = v4xor(sp, lds128(lds, LDS_SPLIT + sl * 32u + (uint32_t)(1 - part) * 16u));
-                        if (OPEN) {
-                            const V4 rt = load_full(in_p + L);
-                            const bool ok = rt.w0 == tag.w0 && rt.w1 == tag.w1 && rt.w2 == tag.w2 && rt.w3 == tag.w3;
-                            result[rec_i] = ok ? (uint64_t)L : ~(uint64_t)0;
-                        } else {
-                            store_full(out_p + L, tag);
-                            if (supp != nullptr) { /* header protection after the whole record, tag included */
-                                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-                                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-                                const ptls_hip_supp_t sp2 = supp[rec_i];
-                                if ((sp2.flags & PTLS_HIP_SUPP_ENABLE) && sp2.hp_key < hp_nslots) {
-                                    const V4 sample = load_full(out + sp2.sample_off);
-                                    store_full(mask + sp2.mask_off, aes_encrypt<ROUNDS>(lds, lb_aes, hp_slots[sp2.hp_key].rk, sample));
-                                }
-                            }
-                        }
-                    }
-                }
-                continue;
+            /* combine the G partial sums of each record: position q = distance of a lane's last element from the end of
+             * the GHASH input; sum_q y_q * H^(q+1).  G >= 2: each lane multiplies by its own power from the key's shared
+             * window tables (build_ghash_tables), then an XOR butterfly over the record's G lanes leaves the GHASH in each;
+             * G = 1: the lane's sum times H (the nibble table of H) */
+            const int q = (N - 1 - na - r) & (G - 1); /* (nc - r) mod G */
+            V4 s;
+            if constexpr (G >= 2) {
+                constexpr int WCP = win_copies(G);
+                Win4<16, 16 * win_row(G)> wt;
+                wt.base = LDS_GTREE + (uint32_t)(q * WCP + (grp & (WCP - 1))) * 16u;
+                s = group_xor<G>(gf_win4_mul<16, 4>(lds, wt, y));
             }
             if (valid && q == 0) {
-                if constexpr (!VCOMB)
+                if constexpr (G == 1)
                     s = gh_mul_nibble(lds, LDS_GTREE, y); /* * H */
                 const V4 tag = v4xor(s, ek0);
                 if (OPEN) {
@@ -1869,7 +1386,6 @@ __global__ void __launch_bounds__(WGT)
         }
         if (DEAL_MUTANT != 2)
             cbase += (uint32_t)ntasks;
-        sbase += (uint32_t)nsplit;
     }
     if (KS_STAMPS && clk != nullptr) {
         ks_acc[0] = __builtin_amdgcn_s_memtime() - ks_t0;

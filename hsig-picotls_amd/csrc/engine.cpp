@@ -111,6 +111,7 @@ struct st_ptls_hip_engine_t {
     uint32_t *d_t0;
     uint32_t *d_queue;                /* QUEUE_SLOTS x {next chunk, workgroups done}: the batch kernel's chunk queues */
     std::atomic<uint32_t> queue_next; /* the slot the next batch launch takes */
+    uint32_t queue_slots;             /* slots in the round robin: QUEUE_SLOTS (PTLS_HIP_QUEUE_SLOTS: fewer, for tests) */
     hipStream_t util;                 /* descriptor / keyset allocation, zeroing and release (dev_alloc / dev_free) */
 };
 
@@ -213,7 +214,17 @@ struct Uses {
  * would have to be in flight at once for two to share one */
 static uint32_t *queue_slot(ptls_hip_engine_t *e)
 {
-    return e->d_queue + 2 * (size_t)(e->queue_next.fetch_add(1, std::memory_order_relaxed) % QUEUE_SLOTS);
+    return e->d_queue + 2 * (size_t)(e->queue_next.fetch_add(1, std::memory_order_relaxed) % e->queue_slots);
+}
+
+/* PTLS_HIP_QUEUE_SLOTS (environment, read when an engine is created): a smaller round robin, 1 .. QUEUE_SLOTS, so that a
+ * test reuses every slot within a few launches and checks that each launch leaves its words reset
+ * (tests/test_gpu_queue.py) */
+static uint32_t queue_slots_env(void)
+{
+    const char *v = getenv("PTLS_HIP_QUEUE_SLOTS");
+    const long n = v != nullptr ? atol(v) : 0;
+    return n >= 1 && n <= (long)QUEUE_SLOTS ? (uint32_t)n : QUEUE_SLOTS;
 }
 
 struct st_ptls_hip_keyset_t {
@@ -250,7 +261,6 @@ struct st_ptls_hip_batch_t {
     bool forced;
     uint32_t max_key; /* largest key slot any record names (checked against the keyset at seal/open) */
     unsigned max_wg;  /* 0, or a cap on the workgroups of a launch (planning then sizes chunks for that many) */
-    uint32_t nsplit;  /* wave tasks the plan deals as two part tasks (split records) */
     uint64_t *d_clk;  /* diagnostic clock stamps of the next launches (ptls_hip_batch_set_clock), or nullptr */
     size_t clk_bytes;
     Uses uses;        /* launches that read the descriptors and the plan: re-planning and batch_free wait for them */
@@ -325,6 +335,7 @@ extern "C" ptls_hip_engine_t *ptls_hip_engine_new(int device)
     make_t0(t0);
     e->d_queue = nullptr;
     e->queue_next = 0;
+    e->queue_slots = queue_slots_env();
     e->util = nullptr;
     if (hipMalloc(&e->d_t0, sizeof(t0)) != hipSuccess || hipMemcpy(e->d_t0, t0, sizeof(t0), hipMemcpyHostToDevice) != hipSuccess ||
         hipMalloc(&e->d_queue, 2 * sizeof(uint32_t) * QUEUE_SLOTS) != hipSuccess ||
@@ -623,70 +634,6 @@ static int plan_wg(const std::vector<Chunk> &ch, int lanes)
     return WG_ALT;
 }
 
-/* Split tasks (batch_kernel.h, G >= 16).  A workgroup works through one key run at a time; with few wave tasks per run
- * (configs[3]: 64 records per key = 16 tasks of 4 records at 16 lanes for 12 waves) the run's longest task takes
- * ~1.5x a wave's share and the other waves idle at the key switch (a 7 % bound).  The planner deals a
- * run's longest tasks as two part tasks each (GHASH elements [0, N - B) and [N - B, N) of the task's records, combined
- * through LDS by the part that finishes last) while a task's cost (its first record's GHASH elements: records are
- * sorted longest first) exceeds `pct` % of the run's share per wave.  PTLS_HIP_SPLIT_PCT (environment) overrides the
- * measured default; 0 switches splitting off. */
-static int split_pct(void)
-{
-    static const int pct = [] {
-        const char *e = getenv("PTLS_HIP_SPLIT_PCT");
-        return e != nullptr ? atoi(e) : 75;
-    }();
-    return pct;
-}
-
-static void plan_splits(const ptls_hip_record_t *recs, const std::vector<uint32_t> &order, std::vector<Chunk> &ch, int lanes)
-{
-    const int pct = split_pct();
-    if (pct <= 0)
-        return;
-    const uint32_t R = 64u / (uint32_t)lanes;
-    const int nwaves = WG_ALT / 64;
-    auto elems = [&](uint32_t pos) {
-        const ptls_hip_record_t &r = recs[order[pos]];
-        return (int)((r.aad_len + 15) / 16 + (r.len + 15) / 16 + 1);
-    };
-    for (size_t a = 0; a < ch.size();) {
-        size_t b = a + 1;
-        while (b < ch.size() && ch[b].key == ch[a].key)
-            ++b;
-        /* key run = chunks [a, b): task costs and the share per wave */
-        double total = 0;
-        size_t tasks = 0;
-        for (size_t c = a; c < b; ++c)
-            for (uint32_t t = 0; t * R < ch[c].count; ++t, ++tasks)
-                total += elems(ch[c].first + t * R);
-        if (tasks < (size_t)(4 * nwaves)) { /* many tasks per wave balance by themselves */
-            const double limit = total / nwaves * pct / 100.0;
-            uint32_t slots = 0;
-            for (size_t c = a; c < b; ++c) {
-                uint32_t ns = 0;
-                for (uint32_t t = 0; (t + 1) * R <= ch[c].count && ns < 255; ++t) {
-                    const uint32_t p0 = ch[c].first + t * R;
-                    /* B from the task's shortest (last) record, as the kernel takes it; every record keeps a part A past its AAD */
-                    const int bsplit = split_tail(elems(p0 + R - 1));
-                    bool ok = elems(p0) > limit && slots + R <= (uint32_t)SPLIT_SLOTS;
-                    for (uint32_t k = 0; ok && k < R; ++k) {
-                        const ptls_hip_record_t &r = recs[order[p0 + k]];
-                        const int n = elems(p0 + k), na = (int)((r.aad_len + 15) / 16);
-                        ok = n >= SPLIT_MIN_N && n <= SPLIT_MAX_N && n - bsplit > na;
-                    }
-                    if (!ok)
-                        break;
-                    ++ns;
-                    slots += R;
-                }
-                ch[c].flags = (ch[c].flags & ~0xff00u) | (ns << 8);
-            }
-        }
-        a = b;
-    }
-}
-
 /* Guided chunk sizes at the end of long key runs (batch_kernel.h QUEUE hands chunks out in plan order).  A workgroup's
  * last chunk ends the launch for it, so the chunks dealt last should be small: a chunk that starts when `rem` wave tasks
  * remain in the batch gets at most rem / (2 ncu) tasks (at least one), like guided self-scheduling.  Only chunks of key
@@ -801,8 +748,6 @@ static void build_chunks(const ptls_hip_record_t *recs, size_t n, int lanes, uns
         ch.push_back(c);
     }
     guided_tail(ch, per_task, ncu ? ncu : 1);
-    if (SPLIT_TASKS && lanes >= 16)
-        plan_splits(recs, order, ch, lanes);
 }
 
 static bool identity_order(const std::vector<uint32_t> &order, size_t n);
@@ -824,9 +769,6 @@ static int plan_chunks(ptls_hip_batch_t *b)
     b->d_order = nullptr;
     b->d_recs_ord = nullptr;
     b->nchunks = (uint32_t)ch.size();
-    b->nsplit = 0;
-    for (const Chunk &c : ch)
-        b->nsplit += (c.flags >> 8) & 0xffu;
     if (ch.empty())
         return 0;
     HIP_TRY(dev_alloc(b->eng, reinterpret_cast<void **>(&b->d_chunks), ch.size() * sizeof(Chunk)), PTLS_HIP_ENOMEM);
@@ -943,9 +885,9 @@ extern "C" int ptls_hip_batch_grid(ptls_hip_batch_t *b)
     return (int)plan_grid(b->n, b->nchunks, b->lanes, batch_cus(b));
 }
 
-extern "C" int ptls_hip_batch_split_tasks(ptls_hip_batch_t *b)
+extern "C" int ptls_hip_batch_chunks(ptls_hip_batch_t *b)
 {
-    return b != nullptr ? (int)b->nsplit : fail(PTLS_HIP_EINVAL, "batch_split_tasks: null batch");
+    return b != nullptr ? (int)b->nchunks : fail(PTLS_HIP_EINVAL, "batch_chunks: null batch");
 }
 
 extern "C" int ptls_hip_batch_set_clock(ptls_hip_batch_t *b, void *d_buf, size_t nbytes)
@@ -1177,6 +1119,21 @@ extern "C" int ptls_hip_fill_records(ptls_hip_batch_t *b, void *buf, uint64_t se
  * "hello world\n" x 7 + NUL, seq 0) sealed through the wave-per-record kernel, the batch kernel's table tree (8 lanes
  * per record) and its VALU combination (32 lanes), and opened back, whenever an engine starts: a library that computes
  * anything else (a probe build, a broken device) fails ptls_hip_engine_new instead of serving records. */
+extern "C" int ptls_hip_device_copy(ptls_hip_engine_t *eng, void *dst, const void *src, size_t bytes, void *stream)
+{
+    if (eng == nullptr || dst == nullptr || src == nullptr || (bytes & 15) != 0 ||
+        ((reinterpret_cast<uintptr_t>(dst) | reinterpret_cast<uintptr_t>(src)) & 15) != 0)
+        return fail(PTLS_HIP_EINVAL, "device_copy: 16-byte aligned pointers and a multiple of 16 bytes");
+    if (bytes == 0)
+        return 0;
+    DeviceGuard g(eng->device);
+    const size_t n16 = bytes / 16;
+    /* 4 KiB per workgroup and step; enough workgroups for 8 waves per CU, fewer for a small copy */
+    const unsigned grid = (unsigned)std::max<size_t>(1, std::min<size_t>((n16 + 1023) / 1024, (size_t)eng->ncu * 8));
+    const int e = launch_copy16(dst, src, n16, grid, stream);
+    return e != 0 ? fail(PTLS_HIP_ELAUNCH, "device_copy: launch failed: %s", hipGetErrorString((hipError_t)e)) : 0;
+}
+
 static int engine_self_check(ptls_hip_engine_t *e)
 {
     static const uint8_t key[16] = {0x00, 0x11, 0x22, 0x33, 0x44, 0x55, 0x66, 0x77, 0x88, 0x99, 0xaa, 0xbb, 0xcc, 0xdd, 0xee, 0xff};

@@ -3,8 +3,7 @@
  *
  * HBM layout:
  *   key slots    KeySlot[nslots]             512 B each: round keys, static IV, H powers
- *   GHASH basis  uint4[nslots][BASIS_VECS]   15 KiB per slot: P * x^e for P in {H, H^2, ..., H^64}, then H^1..H^64
- *                                            (HYBRID builds: then the bit-sliced round keys, bs8_aes.h)
+ *   GHASH basis  uint4[nslots][BASIS_VECS]   18 KiB per slot: P * x^e for P in {H, H^2, ..., H^128}, then H^1..H^128
  *   records      ptls_hip_record_t[n]        48 B descriptors (caller's order)
  *   chunks       Chunk[nchunks]              runs of <= CHUNK_RECS records sharing one key slot
  *   payloads     caller's buffers, untouched layout (in / aad / out)
@@ -15,69 +14,30 @@
 #include <stdint.h>
 #include "ptls_hip.h"
 
-/* The product build (Makefile PROD) refuses every switch that makes the kernels compute something else: timing
- * probes and ablations (wrong output by design) and the TEST-ONLY dealing mutants.  The
- * measurement switches that stay bit-exact (VALU_TREE, HYBRID, GEN_MASK, ...) are tested as alternate builds. */
+/* The product build (Makefile PROD) refuses the switches that make the kernels compute something else (the TEST-ONLY
+ * dealing mutants) or carry diagnostics (key-switch stamps): such objects are built only into mutants/ and diag/. */
 #if defined(PTLS_HIP_PRODUCT)
-#if (defined(CTRHI_PROBE) && CTRHI_PROBE) || (defined(SPLIT_PROBE) && SPLIT_PROBE) || (defined(KEYSWITCH_PROBE) && KEYSWITCH_PROBE) || \
-    (defined(DEAL_MUTANT) && DEAL_MUTANT) || (defined(SPARSE_ABLATE) && SPARSE_ABLATE) || (defined(PLUGIN_PROBE) && PLUGIN_PROBE) || \
-    (defined(KS_STAMPS) && KS_STAMPS)
-#error "libptls_hip.so is built with a timing-probe, ablation or test-mutant switch set: such builds compute wrong output"
+#if (defined(DEAL_MUTANT) && DEAL_MUTANT) || (defined(KS_STAMPS) && KS_STAMPS)
+#error "libptls_hip.so is built with a test-mutant or diagnostic switch set"
 #endif
-#endif
-
-/* SPLIT_TASKS (measurement switch, DESIGN.md §4.7 "split records"; off in the product): at 16 and 32 lanes per record the
- * planner deals a key run's longest wave tasks as two part tasks each.  Bit-exact (TEST-ONLY alternate build
- * alt/libptls_hip_split.so, tests/test_gpu_split.py), but configs[3] loses 2-5 % with it, so off. */
-#ifndef SPLIT_TASKS
-#define SPLIT_TASKS 0
 #endif
 
 namespace ptls_hip {
 
-constexpr int NPOW = SPLIT_TASKS ? 10 : 8; /* H^1 .. H^16 (batch kernel main and tree tables), H^32 (batch kernel main table
-                                              at G = 32), H^64 (sparse kernel), H^128 (a single record on two waves, stride
-                                              128); SPLIT_TASKS: H^128 .. H^512 (the shift of a split record's first part) */
-/* GHASH basis slot: NPOW x 128 vectors P * x^e, then H^1 .. H^128 (the sparse kernel's per-lane final powers: H^(q+1),
- * q < 64; a two-wave single record of up to 128 GHASH elements multiplies element i by H^(N - i)) */
+constexpr int NPOW = 8; /* H^1 .. H^16 (batch kernel main tables), H^32 (batch kernel main table at G = 32), H^64 (sparse
+                          kernel), H^128 (a single record on two waves, stride 128) */
+/* GHASH basis slot: NPOW x 128 vectors P * x^e, then H^1 .. H^128 (the lane combinations' per-lane final powers H^(q+1);
+ * a two-wave single record of up to 128 GHASH elements multiplies element i by H^(N - i)) */
 constexpr int LANE_POWS = 128;
-/* HYBRID (measurement switch): this many waves per batch-kernel workgroup (the last ones) run their
- * full-block stretch as bit-sliced AES on the VALU (bs8_aes.h), the others with the LDS T-tables.  Parity-green, but
- * no faster on MI355X (c2: +0-1 % at 4 of 12 waves, -5 % at 8, -20 % at 12), so off. */
-#ifndef HYBRID
-#define HYBRID 0
-#endif
-/* with HYBRID, the slot also holds the bit-sliced round keys 1..rounds (bs8::slice_key: 32 words per round) */
-constexpr int BS_KEY_OFF = NPOW * 128 + LANE_POWS; /* uint4 offset in the slot */
-constexpr int BS_KEY_VECS = HYBRID ? 14 * 32 / 4 : 0;
-constexpr int BASIS_VECS = BS_KEY_OFF + BS_KEY_VECS; /* uint4 per key slot (18 KiB; 19.75 KiB with HYBRID, 22 KiB with SPLIT_TASKS) */
+constexpr int BASIS_VECS = NPOW * 128 + LANE_POWS; /* uint4 per key slot: 18 KiB */
 constexpr int MAX_LANES = 32;    /* lanes per record (G) of the batch kernel: 1, 2, 4, 8, 16, 32 */
 constexpr int SPARSE_LANES = 64; /* "lanes" value of the wave-per-record kernel (sparse_kernel.hip) */
 /* the planner picks that kernel when a batch's key runs hold fewer records than this on average */
-#ifndef SPARSE_MAX_PER_RUN
-#define SPARSE_MAX_PER_RUN 20 /* configs[3]'s lengths, seal GiB/s, sparse kernel / 32 lanes (round 3): 16 records per key 533 / 498,
-                                 24 per key 533 / 680 (tools/calls_r03/r03_call24.sh) */
-#endif
+constexpr int SPARSE_MAX_PER_RUN = 20; /* configs[3]'s lengths, seal GiB/s, sparse kernel / 32 lanes (round 3): 16 records
+                                           per key 533 / 498, 24 per key 533 / 680 (tools/calls_r03/r03_call24.sh) */
 /* one workgroup per CU (LDS-limited); 768 threads (3 waves per SIMD, 168 VGPRs) by default, 512 selectable
  * per batch (engine.cpp:plan_wg).  WG_MAX bounds the chunk size the planner cuts key runs into. */
 constexpr int WG_MAX = 1024;
-
-/* Split records (G >= 16, DESIGN.md §4.1 "split tasks"; planned in engine.cpp plan_splits): the planner may deal a key run's longest tasks as two part
- * tasks each, part A = GHASH elements [0, N - B) of the task's records, part B = [N - B, N), B = split_tail(N) a power
- * of two near N / 2 of the task's shortest record.  Part A multiplies its partial GHASH by H^B (basis plane log2 B), each part leaves its partial in
- * an LDS slot of the workgroup, and the part that finishes second XORs them into the tag.  The slots sit after the
- * tables and the task counter: SPLIT_SLOTS records of {partial A, partial B} (32 B) + a 4-byte arrival counter. */
-constexpr int SPLIT_SLOTS = 192;
-constexpr int SPLIT_MIN_N = 256;  /* records of fewer GHASH elements are never split */
-constexpr int SPLIT_MAX_N = 1536; /* nor records of more (B would be under a third of N) */
-constexpr int split_tail(int N)
-{
-    return N >= 768 ? 512 : N >= 384 ? 256 : 128;
-}
-constexpr int split_plane_of_tail(int B)
-{
-    return B == 512 ? 9 : B == 256 ? 8 : 7;
-}
 
 struct KeySlot {
     uint32_t rk[60];      /* AES round keys, raw byte order as little-endian words (11 or 15 used) */
@@ -89,16 +49,13 @@ struct KeySlot {
 static_assert(sizeof(KeySlot) == 512, "KeySlot must stay 512 bytes");
 
 /* the second compiled workgroup size (the first is 512); tuning builds override it (tools/build_variant.sh) */
-#ifndef WG_ALT
-#define WG_ALT 768
-#endif
+constexpr int WG_ALT = 768;
 
 struct Chunk {
     uint32_t first; /* position of the chunk's first record in the order array */
     uint32_t count; /* records in the chunk, all with the same key slot */
     uint32_t key;   /* key slot */
-    uint32_t flags; /* bit0: every record of the chunk is 16-byte aligned (in/out/aad offsets); bits 8..15: how many of the
-                       chunk's first (longest) wave tasks are dealt as two part tasks each (split records, batch_kernel.h) */
+    uint32_t flags; /* bit0: every record of the chunk is 16-byte aligned (in/out/aad offsets) */
 };
 
 struct KernelArgs {
@@ -211,6 +168,7 @@ int launch_derive_traffic_keys(const uint8_t *secrets_in, uint8_t *secrets_out, 
                                int update, uint8_t *keys, uint8_t *ivs, void *stream);
 int launch_fill(const ptls_hip_record_t *recs, uint32_t n, uint8_t *buf, uint64_t seed, uint64_t index_base,
                 const uint64_t *index, unsigned grid, void *stream);
+int launch_copy16(void *dst, const void *src, size_t n16, unsigned grid, void *stream);
 
 } // namespace ptls_hip
 

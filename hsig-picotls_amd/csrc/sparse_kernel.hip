@@ -13,9 +13,9 @@
  *     times H^64), rebuilt per record from the key's basis H^64 * x^e (keysetup): 4 basis loads and 8
  *     ds_write_b128 per lane, no barrier (a wave's LDS operations complete in order).  A record of at most
  *     64 GHASH elements (one per lane) needs no Horner step and skips the build;
- *   - the combination needs no table: lane l multiplies its sum by its own power H^(q+1),
- *     q = (N - 1 - l) mod 64, read from keysetup's per-key H^1..H^64 list, on the VALU (gf_mul_valu), and an
- *     XOR butterfly over the 64 lanes leaves the GHASH in every lane;
+ *   - the combination: lane l multiplies its sum by its own power H^(q+1), q = (N - 1 - l) mod 64, read from
+ *     keysetup's per-key H^1..H^128 list, with 4-bit windows over a per-lane table in the wave's LDS area
+ *     (gf_mul_win4), and an XOR butterfly over the 64 lanes leaves the GHASH in every lane;
  *   - a Horner multiply is 32 ds_read_b128 (gh_mul_nibble); AES-CTR uses the batch kernel's 32x-replicated
  *     T-tables (64 KiB) and round keys through the scalar unit.  64 KiB + 12 x 8 KiB = the CU's 160 KiB.
  */
@@ -26,59 +26,11 @@
 
 namespace ptls_hip {
 
-#ifndef SPARSE_WG
-#define SPARSE_WG 768 /* 12 waves: 64 KiB AES tables + 12 x 8 KiB wave tables = 160 KiB */
-#endif
-#ifndef SPARSE_ABLATE
-#define SPARSE_ABLATE 0 /* timing ablation only (wrong output): 1 = no final lane combination, 2 = no main-loop multiply, 3 = no H^64 table build */
-#endif
-#ifndef SPARSE_GEN_SKEW
-#define SPARSE_GEN_SKEW 1 /* generic elements through the skewed counter-mode AES (1: c4s seal +1.5 %, open +4 %) or aes_ctr_n (0) */
-#endif
-#ifndef SPARSE_PURE
-#define SPARSE_PURE 1 /* the branch-free skewed stretch over full blocks (0: every element on the generic path) */
-#endif
-#ifndef SPARSE_PURE1
-#define SPARSE_PURE1 1 /* an odd full-block element after the stretch's KP-block iterations takes a single-block step */
-#endif
-#ifndef PLUGIN_PROBE
-#define PLUGIN_PROBE 0 /* timing probe only (wrong output): 1 = no AES table build */
-#endif
-#ifndef SPARSE_AADPF
-#define SPARSE_AADPF 1 /* batch records: the lane's first AAD block is loaded at record setup, before the counter-mode constants
-                        * and the H^64 table (its latency under that work) instead of after them: c4s seal 498-504 -> 513-519,
-                        * open 514-516 -> 520-521 GiB/s (same box, profiles/r04_c4s_prefetch_ab.log) */
-#endif
-#ifndef SPARSE_TAGPF
-#define SPARSE_TAGPF 0 /* batch open: the received tag is loaded at record setup instead of after the lane combination (measured
-                        * no faster: 505-514 against 514-516 GiB/s open) */
-#endif
-#ifndef SPARSE_HPPF
-#define SPARSE_HPPF 0 /* batch records: the lane's power H^(q+1) for the combination is loaded after the stretch, under the tail
-                       * elements, instead of at the combination (measured neutral: 516 / 521 against 517 / 524 GiB/s) */
-#endif
-#ifndef SPARSE_CTR_WAVE
-#define SPARSE_CTR_WAVE 0 /* 1: a record's counter-mode constants by one lookup per lane (ctr_const_wave): 2 LDS instructions instead
-                           * of 22; bit-exact (GPU suite green on it) but no faster: c4s seal 512-516 against 517-519 (same box,
-                           * profiles/r04_c4s_ctr_wave_ab.log) */
-#endif
-#ifndef SPARSE_BASISPF
-#define SPARSE_BASISPF 0 /* batch records: the H^64 basis loads go out before the counter-mode constants (as the single record's;
-                          * measured neutral: 518 / 521 against 517 / 524 GiB/s).  Touching the next record's key slot, basis
-                          * and lane-power lines during the current record was neutral as well (501-504 against 503-511) */
-#endif
-#ifndef SPARSE_QUEUE
-#define SPARSE_QUEUE 3 /* the deal of records to waves (aesgcm_sparse_kernel): 0 static stride, 1 queue, 2 snake, 3 snake + queue tail */
-#endif
-#ifndef SPARSE_TAIL
-#define SPARSE_TAIL 4 /* SPARSE_QUEUE 3: the last nrecs / SPARSE_TAIL records (the shortest) come from the queue */
-#endif
-#ifndef SPARSE_PE
-#define SPARSE_PE 2 /* GHASH elements (AES blocks) per lane per main-loop iteration */
-#endif
-#ifndef BV_PREFETCH
-#define BV_PREFETCH 1 /* the single-record launch reads its first elements and touches its key material before the table build */
-#endif
+constexpr int SPARSE_WG = 768;  /* 12 waves: 64 KiB AES tables + 12 x 8 KiB wave tables = 160 KiB */
+constexpr int SPARSE_PE = 2;    /* GHASH elements (AES blocks) per lane per main-loop iteration */
+constexpr int SPARSE_TAIL = 4;  /* the last nrecs / SPARSE_TAIL records (the shortest) come from the launch's queue word */
+constexpr int SPARSE_WIN_LB = 8; /* lane combination: window lookups in flight per group (c4s seal +0.3 %, open +0.7 % over 4,
+                                    profiles/r04_c4s_win_lb8_ab.log) */
 #ifndef STAMP_PHASES
 #define STAMP_PHASES 0 /* diagnostic build only (Makefile `diag`, tools/plugin_stamps.py): the single-record (plugin) launch
                           stamps the shader clock at its phase boundaries into clk[0 .. 11] (clk[14], clk[15]: the 100 MHz
@@ -145,12 +97,6 @@ __device__ __forceinline__ void wave_lds_sync()
  * laid out as gh_mul_nibble reads it: entry [p = 8w + j][v] = v at bits 4j..4j+3 of raw word w, times P.
  * Lane l writes position l/2, values 8(l&1) .. 8(l&1) + 7: load_wave_basis fetches the lane's four basis
  * vectors (issued early to hide their latency), store_wave_table writes the eight combinations. */
-#ifndef SPARSE_DERIVE
-#define SPARSE_DERIVE 2 /* 2: each lane loads P x^(32 w) (one of four vectors, four cache lines per record), moves it to its
-                           own P x^(e0 - 3) by a 0..28-bit multiply by x^r and derives the other three by multiplying by x
-                           (VALU); 1: loads P x^(e0 - 3) itself (32 vectors over 16 lines); 0: four loads per lane */
-#endif
-
 /* v * x in GF(2^128), GCM bit order, raw byte order words: the 128-bit big-endian string shifted right by one bit,
  * R = 0xE1 || 0^120 folded in when the last bit drops out (SP 800-38D) */
 __device__ __forceinline__ V4 mulx_raw(V4 v)
@@ -179,35 +125,24 @@ __device__ __forceinline__ uint32_t basis_r(int lane)
 __device__ __forceinline__ void load_wave_basis(const uint4 *__restrict__ bp, int lane, V4 (&b)[4])
 {
     asm volatile("" : "+v"(lane)); /* the lane's basis offset computed here, not hoisted out of the record loop (scratch) */
-    const int p = lane >> 1, w = p >> 3, j = p & 7;
     /* the lane's four vectors are P x^(e0), P x^(e0 - 1), P x^(e0 - 2), P x^(e0 - 3) for one e0 (bits 4j .. 4j + 3 of
-     * word w lie in one byte): e0 - 3 = 32 w + basis_r(lane).  SPARSE_DERIVE 1 loads P x^(e0 - 3), 2 loads P x^(32 w);
-     * store_wave_table derives the rest */
-    if (SPARSE_DERIVE == 2) {
-        const uint4 v = bp[32 * w];
-        b[3] = V4{v.x, v.y, v.z, v.w};
-        return;
-    }
-#pragma unroll
-    for (int t = SPARSE_DERIVE ? 3 : 0; t < 4; ++t) {
-        const int u = 4 * j + t; /* bit u of little-endian word w = raw byte 4w + u/8, bit u%8 */
-        const uint4 v = bp[8 * (4 * w + (u >> 3)) + 7 - (u & 7)];
-        b[t] = V4{v.x, v.y, v.z, v.w};
-    }
+     * word w lie in one byte): e0 - 3 = 32 w + basis_r(lane).  The lane loads P x^(32 w), one of four vectors (four cache
+     * lines per record); store_wave_table derives the rest on the VALU (round 4: 32 vectors over 16 lines before) */
+    const int w = (lane >> 1) >> 3;
+    const uint4 v = bp[32 * w];
+    b[3] = V4{v.x, v.y, v.z, v.w};
 }
 
 __device__ __forceinline__ void store_wave_table(uint8_t *lds, uint32_t tab, V4 (&b)[4], int lane)
 {
-    if (SPARSE_DERIVE == 2) {
+    {
         int ln = lane;
         asm volatile("" : "+v"(ln));
         b[3] = mulxpow_raw(b[3], basis_r(ln));
     }
-    if (SPARSE_DERIVE) {
-        b[2] = mulx_raw(b[3]);
-        b[1] = mulx_raw(b[2]);
-        b[0] = mulx_raw(b[1]);
-    }
+    b[2] = mulx_raw(b[3]);
+    b[1] = mulx_raw(b[2]);
+    b[0] = mulx_raw(b[1]);
     asm volatile("" : "+v"(lane)); /* the entries' masks and slots are computed here, not hoisted out of the record loop
                                       (32 lane-invariant values live across the kernel: scratch beside the lane combination) */
     const int p = lane >> 1;
@@ -235,66 +170,6 @@ __device__ __forceinline__ void store_wave_table(uint8_t *lds, uint32_t tab, V4 
     }
 }
 
-#ifndef SPARSE_WIN
-#define SPARSE_WIN 1 /* the lane combination's multiply: 1 = 4-bit windows over a per-lane table in LDS (gf_mul_win4, ~500 VALU
-                        + 8 / 16 stores + 32 lookups), 0 = gf_mul_valu (1 408 VALU) */
-#endif
-#ifndef SPARSE_WIN_LB
-#define SPARSE_WIN_LB 8 /* the batch instantiations' lookups in flight per group (8 spilled at 168 VGPRs until the round-4 spill fix; now
-                          * the same 12 B of scratch as 4, c4s seal +0.3 %, open +0.7 %: profiles/r04_c4s_win_lb8_ab.log) */
-#endif
-
-/* The counter-mode constants of a record the whole wave works on (ctr_const's values, wave-uniform): lane i < 14 makes
- * round 1's lookup i and lane i < 8 round 2's, one ds_read_b32 per round instead of 14 + 8, and the sums are gathered
- * with v_readlane.  ctr_const issues 22 dependent-by-round LDS instructions into a command queue the other waves keep
- * full; this issues 2.  Per lane (bit i of each mask): the state word (two bits), its byte (two bits), T2 instead of T0,
- * and a rotation by 8 (T1 = rotl8 T0, T3 = rotl8 T2).  The sparse kernel's tables sit at LDS offset 0. */
-__device__ __forceinline__ uint32_t ctr_lookup(const uint8_t *lds, uint32_t lb, int ln, uint32_t w0, uint32_t w1, uint32_t w2,
-                                               uint32_t w3, uint32_t mw0, uint32_t mw1, uint32_t mk0, uint32_t mk1, uint32_t mt2,
-                                               uint32_t mrot)
-{
-    const uint32_t b = 1u << (ln & 31); /* lanes 14-31 take a valid dummy lookup, lanes 32-63 repeat 0-31 (not read) */
-    const uint32_t x = (mw1 & b) ? ((mw0 & b) ? w3 : w2) : ((mw0 & b) ? w1 : w0);
-    const uint32_t k = ((mk0 & b) ? 1u : 0u) + ((mk1 & b) ? 2u : 0u);
-    const uint32_t byte = __builtin_amdgcn_ubfe(x, 8u * k, 8u);
-    const uint32_t v = lds32(lds, (byte << 8) | (lb & 0x7fu) | ((mt2 & b) ? 128u : 0u));
-    return (mrot & b) ? rotl8(v) : v;
-}
-
-__device__ __forceinline__ CtrConst ctr_const_wave(const uint8_t *lds, uint32_t lb, const uint32_t *__restrict__ rk,
-                                                   uint32_t n0, uint32_t n1, uint32_t n2)
-{
-    int ln;
-    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(ln));
-    const uint32_t s0 = n0 ^ rk[0], s1 = n1 ^ rk[1], s2 = n2 ^ rk[2], s3 = rk[3]; /* counter bytes 12, 13 = 0 */
-    /* round 1, lanes 0-13: k10 = T0[s0.0] ^ T1[s1.1] ^ T2[s2.2], k11 = T0[s1.0] ^ T1[s2.1] ^ T3[s0.3],
-     * t2 = T0[s2.0] ^ T1[s3.1] ^ T2[s0.2] ^ T3[s1.3], t3 = T0[s3.0] ^ T1[s0.1] ^ T2[s1.2] ^ T3[s2.3] */
-    /* per-lane masks (word bit 0, word bit 1, byte bit 0, byte bit 1, T2, rotl8) for the 14 lookups in the order above */
-    const uint32_t r1 = ctr_lookup(lds, lb, ln & 63, s0, s1, s2, s3, 0x168au, 0x24d4u, 0x2ab2u, 0x3324u, 0x3324u, 0x2ab2u);
-    uint32_t v[14];
-#pragma unroll
-    for (int i = 0; i < 14; ++i)
-        v[i] = (uint32_t)__builtin_amdgcn_readlane((int)r1, i);
-    CtrConst c;
-    c.r03 = rk[3];
-    c.k10 = v[0] ^ v[1] ^ v[2] ^ rk[4];
-    c.k11 = v[3] ^ v[4] ^ v[5] ^ rk[5];
-    const uint32_t t2 = v[6] ^ v[7] ^ v[8] ^ v[9] ^ rk[6];
-    const uint32_t t3 = v[10] ^ v[11] ^ v[12] ^ v[13] ^ rk[7];
-    /* round 2, lanes 0-7 (w 0 = t2, 1 = t3): k20 = T2[t2.2] ^ T3[t3.3], k21 = T1[t2.1] ^ T2[t3.2],
-     * k22 = T0[t2.0] ^ T1[t3.1], k23 = T0[t3.0] ^ T3[t2.3] */
-    const uint32_t r2 = ctr_lookup(lds, lb, ln & 63, t2, t3, t2, t3, 0x6au, 0x0u, 0xa6u, 0x8bu, 0x8bu, 0xa6u);
-    uint32_t u[8];
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-        u[i] = (uint32_t)__builtin_amdgcn_readlane((int)r2, i);
-    c.k20 = u[0] ^ u[1] ^ rk[8];
-    c.k21 = u[2] ^ u[3] ^ rk[9];
-    c.k22 = u[4] ^ u[5] ^ rk[10];
-    c.k23 = u[6] ^ u[7] ^ rk[11];
-    return c;
-}
-
 /* the wave's maximum / XOR sum in every lane: batch_kernel.h's DPP + permlane reduction (no LDS instruction, no partner
  * address; until round 4 a ds_bpermute butterfly whose partner addresses had to come from an opaque lane index, or the
  * compiler hoisted them out of the record loop into scratch) */
@@ -308,19 +183,16 @@ __device__ __forceinline__ V4 wave_xor(V4 z)
     return group_xor<64>(z);
 }
 
-/* sum over the wave of (lane's GHASH sum) * H^(q+1): one multiply by the lane's own power (keysetup's H^1..H^64 table),
- * then the XOR butterfly; every lane ends with the total.  SPARSE_WIN: the multiply's table is the lane's 8 multiples of
- * H^(q+1) in the wave's own 8 KiB table area (the H^64 Horner table is dead by now). */
-__device__ __forceinline__ V4 ghash_combine(uint8_t *lds, uint32_t tab, int lane, const uint4 *__restrict__ bs, int q, V4 y,
-                                          bool have_hp = false, uint4 hp = uint4{0, 0, 0, 0})
+/* sum over the wave of (lane's GHASH sum) * H^(q+1): one multiply by the lane's own power (keysetup's H^1..H^128 list),
+ * then the XOR butterfly; every lane ends with the total.  The multiply's table is the lane's 8 multiples of H^(q+1) in
+ * the wave's own 8 KiB table area (the H^64 Horner table is dead by now). */
+__device__ __forceinline__ V4 ghash_combine(uint8_t *lds, uint32_t tab, int lane, const uint4 *__restrict__ bs, int q, V4 y)
 {
     /* q made opaque here: the power's load and the table arithmetic stay after the record's elements instead of being
      * hoisted above the stretch (where their registers pushed the batch instantiations into scratch) */
     asm volatile("" : "+v"(q));
-    if (!have_hp)
-        hp = bs[NPOW * 128 + q]; /* H^(q+1) */
-    const V4 p = V4{hp.x, hp.y, hp.z, hp.w};
-    return wave_xor(SPARSE_WIN ? gf_mul_win4<8, SPARSE_WIN_LB>(lds, tab, lane, y, p) : gf_mul_valu(y, p));
+    const uint4 hp = bs[NPOW * 128 + q]; /* H^(q+1) */
+    return wave_xor(gf_mul_win4<8, SPARSE_WIN_LB>(lds, tab, lane, y, V4{hp.x, hp.y, hp.z, hp.w}));
 }
 
 /* One record on one wave (the sparse-key kernel's per-record body, also the plugin worker's): its counter-mode
@@ -371,29 +243,28 @@ __device__ __forceinline__ void sparse_record(uint8_t *lds, int lane, uint32_t l
                    n1 = __builtin_amdgcn_readfirstlane((ov ? ivo.y : slot->iv[1]) ^ bswap32((uint32_t)(rec.seq >> 32))),
                    n2 = __builtin_amdgcn_readfirstlane((ov ? ivo.z : slot->iv[2]) ^ bswap32((uint32_t)rec.seq));
     const int iters = (N + S - 1) >> LOG2S;
-    const bool horner = SPARSE_ABLATE != 3 && iters > 1; /* N <= S: one element per lane, no Horner step */
+    const bool horner = iters > 1; /* N <= S: one element per lane, no Horner step */
     V4 b[4];
     /* a single record (the plugin's launch): the H^64 basis loads go out before the counter-mode constants, so their
      * memory latency overlaps that LDS chain (in batches other waves hide it; there the early loads cost c4s open
      * 2.5 %, measured) */
     const int q = (N - 1 - vl) & (S - 1);
-    /* batch records: loads whose latency would otherwise sit after the table build (SPARSE_AADPF, SPARSE_TAGPF) */
-    V4 aad_pf = V4{0, 0, 0, 0}, tag_pf = V4{0, 0, 0, 0};
-    if (SPARSE_AADPF && !BYVAL && vl < na)
+    /* batch records: the lane's first AAD block is loaded here, before the counter-mode constants and the H^64 table, so
+     * its latency runs under that work (c4s seal 498-504 -> 513-519 GiB/s, profiles/r04_c4s_prefetch_ab.log) */
+    V4 aad_pf = V4{0, 0, 0, 0};
+    if (!BYVAL && vl < na)
         aad_pf = load_block<ALIGNED>(aad_p + 16 * vl, min(16, A - 16 * vl));
-    if (SPARSE_TAGPF && OPEN && !BYVAL && q == 0)
-        tag_pf = load_block<false>(in_p + L, 16);
-    (void)aad_pf, (void)tag_pf;
+    (void)aad_pf;
     /* a single record builds its lane-combination table (the 16 multiples of H^(q+1)) early, in an LDS area of its own
      * (ctab), so that only the lookups remain after its last element */
-    constexpr bool early_win = BYVAL && SPARSE_WIN;
+    constexpr bool early_win = BYVAL;
     uint4 hpe = uint4{0, 0, 0, 0};
     if (early_win)
         hpe = bs[NPOW * 128 + q]; /* H^(q+1) */
-    if (horner && (by_value || SPARSE_BASISPF))
+    if (horner && by_value)
         load_wave_basis(bs + LOG2S * 128, lane, b); /* H^S */
     /* the record (and so its counter-mode constants) is the wave's alone: keep them in SGPRs */
-    CtrConst cc = SPARSE_CTR_WAVE ? ctr_const_wave(lds, lb_aes, rk, n0, n1, n2) : ctr_const(lds, lb_aes, rk, n0, n1, n2);
+    CtrConst cc = ctr_const(lds, lb_aes, rk, n0, n1, n2);
     cc.k10 = __builtin_amdgcn_readfirstlane(cc.k10);
     cc.k11 = __builtin_amdgcn_readfirstlane(cc.k11);
     cc.k20 = __builtin_amdgcn_readfirstlane(cc.k20);
@@ -409,7 +280,7 @@ __device__ __forceinline__ void sparse_record(uint8_t *lds, int lane, uint32_t l
     phase_acc(pa, bstamps, 2);
     wave_lds_sync(); /* the previous record's Horner reads of the table are done */
     if (horner) { /* (loading the basis during the previous record's VALU combine measured no faster: other waves hide it) */
-        if (!by_value && !SPARSE_BASISPF)
+        if (!by_value)
             load_wave_basis(bs + LOG2S * 128, lane, b); /* H^S */
         store_wave_table(lds, tab, b, lane);
     }
@@ -451,8 +322,6 @@ __device__ __forceinline__ void sparse_record(uint8_t *lds, int lane, uint32_t l
         }
         if (wave_max_sp(big)) {
             aes_encrypt_n<ROUNDS, NE>(lds, lb_aes, rk, ks);
-        } else if (!SPARSE_GEN_SKEW) {
-            aes_ctr_n<ROUNDS, NE>(lds, lb_aes, rk, cc, cw, ks);
         } else {
             const V4 nohash[NE] = {};
             V4 ydummy = V4{0, 0, 0, 0};
@@ -463,7 +332,7 @@ __device__ __forceinline__ void sparse_record(uint8_t *lds, int lane, uint32_t l
             const V4 x = finish_elem<OPEN, ALIGNED, true>(e[b], inb[b], ks[b], aad_p, A, L, out_p, ek0);
             if (m + b == 0)
                 y = x; /* 0 * P ^ x */
-            else if (SPARSE_ABLATE != 2 && e[b].active)
+            else if (e[b].active)
                 y = v4xor(gh_mul_nibble(lds, tab, y), x); /* y * H^64 ^ x */
         }
     };
@@ -489,10 +358,10 @@ __device__ __forceinline__ void sparse_record(uint8_t *lds, int lane, uint32_t l
     const int ml = vl < na ? (na - vl + S - 1) >> LOG2S : 0;                      /* the lane's first data element */
     const int mhl = lastc + na - vl >= 0 ? ((lastc + na - vl) >> LOG2S) + 1 : 0;  /* its elements m < mhl: full blocks */
     const int fmin = -wave_max_sp(-max(mhl - ml, 0)); /* full-block elements every lane has */
-    const int npure = SPARSE_PURE ? fmin / KP : 0;
-    /* SPARSE_PURE1: an odd full element left over by the KP-block iterations takes one single-block step of the stretch
-     * instead of the generic path */
-    const int npx = SPARSE_PURE1 && npure > 0 && fmin - npure * KP > 0 ? 1 : 0;
+    const int npure = fmin / KP;
+    /* an odd full element left over by the KP-block iterations takes one single-block step of the stretch instead of the
+     * generic path */
+    const int npx = npure > 0 && fmin - npure * KP > 0 ? 1 : 0;
     const int iters_l = vl < N ? ((N - 1 - vl) >> LOG2S) + 1 : 0;                /* the lane's elements */
     const int pm1 = ml + npure * KP + npx;                                        /* the lane's first after the stretch */
     if (!npure) { /* head and tail are one range: elements share one round trip to the record's memory (the plugin) */
@@ -504,7 +373,7 @@ __device__ __forceinline__ void sparse_record(uint8_t *lds, int lane, uint32_t l
                 const int i = vl + S * j;
                 const int nb = min(16, A - 16 * i);
                 const V4 x = (BYVAL && prefetch && j < 2)       ? mask_block(j == 0 ? pre[0] : pre[1], nb)
-                             : (SPARSE_AADPF && !BYVAL && j == 0) ? aad_pf
+                             : (!BYVAL && j == 0)                ? aad_pf
                                                                   : load_block<ALIGNED>(aad_p + 16 * i, nb);
                 y = j == 0 ? x : v4xor(gh_mul_nibble(lds, tab, y), x);
             }
@@ -538,14 +407,7 @@ __device__ __forceinline__ void sparse_record(uint8_t *lds, int lane, uint32_t l
                 k[b] = V4{n0, n1, n2, cw[b]};
             }
             __builtin_amdgcn_sched_barrier(0); /* keep the loads at the top of the iteration */
-            if (SPARSE_ABLATE == 2) {
-                ctr_ghash_skewed<ROUNDS, KP, false>(lds, lb_aes, rk, cc, cw, k, y, d, GhNibble{tab});
-#pragma unroll
-                for (int b = 0; b < KP; ++b) {
-                    pend[b] = v4xor(d[b], k[b]);
-                    store_full(dst + o + 16 * S * b, pend[b]);
-                }
-            } else if (OPEN) {
+            if (OPEN) {
                 ctr_ghash_skewed<ROUNDS, KP, true>(lds, lb_aes, rk, cc, cw, k, y, d, GhNibble{tab});
 #pragma unroll
                 for (int b = 0; b < KP; ++b)
@@ -604,12 +466,6 @@ __device__ __forceinline__ void sparse_record(uint8_t *lds, int lane, uint32_t l
     }
     phase_stamp(clk, stamps, lane, 5);
     phase_acc(pa, bstamps, 5);
-    uint4 hp_pf = uint4{0, 0, 0, 0};
-    if (SPARSE_HPPF && !early_win) { /* the combination's power, under the tail elements */
-        int qo = q;
-        asm volatile("" : "+v"(qo));
-        hp_pf = bs[NPOW * 128 + qo];
-    }
     if (npure) { /* the rest of each lane's elements from its own position (partial, length and leftover blocks) */
         const int rest = wave_max_sp(max(iters_l - pm1, 0));
         int j = 0;
@@ -621,14 +477,12 @@ __device__ __forceinline__ void sparse_record(uint8_t *lds, int lane, uint32_t l
     phase_stamp(clk, stamps, lane, 6);
     phase_acc(pa, bstamps, 6);
 
-    /* lane l's sum times H^(q+1), q = distance of its last element from the end of the GHASH input, on the
-     * VALU; the XOR butterfly then sums the 64 lanes (ghash_combine) */
-    if (SPARSE_ABLATE != 1) {
-        if (early_win)
-            y = wave_xor(gf_win4_mul<16>(lds, w4, y));
-        else
-            y = ghash_combine(lds, tab, lane, bs, q, y, SPARSE_HPPF != 0, hp_pf);
-    }
+    /* lane l's sum times H^(q+1), q = distance of its last element from the end of the GHASH input; the XOR butterfly
+     * then sums the 64 lanes (ghash_combine) */
+    if (early_win)
+        y = wave_xor(gf_win4_mul<16>(lds, w4, y));
+    else
+        y = ghash_combine(lds, tab, lane, bs, q, y);
     /* S = 128: the wave without the length block hands its sum over (and makes its output stores visible at system scope
      * first: the tag wave's caller stores the completion word); both waves pass the barrier */
     const int tagw = ((N - 1) & (S - 1)) >> 6;
@@ -647,7 +501,7 @@ __device__ __forceinline__ void sparse_record(uint8_t *lds, int lane, uint32_t l
     if (q == 0) {
         const V4 tag = v4xor(y, ek0);
         if (OPEN) {
-            const V4 rt = (SPARSE_TAGPF && !BYVAL) ? tag_pf : load_block<false>(in_p + L, 16);
+            const V4 rt = load_block<false>(in_p + L, 16);
             const bool ok = rt.w0 == tag.w0 && rt.w1 == tag.w1 && rt.w2 == tag.w2 && rt.w3 == tag.w3;
             result[rec_i] = ok ? (uint64_t)L : ~(uint64_t)0;
         } else {
@@ -711,7 +565,7 @@ __device__ __forceinline__ void mw_record(uint8_t *lds, int wave, int lane, uint
         const uint32_t n0 = __builtin_amdgcn_readfirstlane(ov ? ivo.x : slot->iv[0]),
                        n1 = __builtin_amdgcn_readfirstlane((ov ? ivo.y : slot->iv[1]) ^ bswap32((uint32_t)(rec.seq >> 32))),
                        n2 = __builtin_amdgcn_readfirstlane((ov ? ivo.z : slot->iv[2]) ^ bswap32((uint32_t)rec.seq));
-        CtrConst cc = SPARSE_CTR_WAVE ? ctr_const_wave(lds, lb_aes, rk, n0, n1, n2) : ctr_const(lds, lb_aes, rk, n0, n1, n2);
+        CtrConst cc = ctr_const(lds, lb_aes, rk, n0, n1, n2);
         cc.k10 = __builtin_amdgcn_readfirstlane(cc.k10);
         cc.k11 = __builtin_amdgcn_readfirstlane(cc.k11);
         cc.k20 = __builtin_amdgcn_readfirstlane(cc.k20);
@@ -815,7 +669,7 @@ __global__ void __launch_bounds__(WG)
      * instead of after it (tools/plugin_stamps.py).  pre[m] = element lane + 64 m. */
     V4 pre[2] = {V4{0, 0, 0, 0}, V4{0, 0, 0, 0}}, pre_hi[2] = {V4{0, 0, 0, 0}, V4{0, 0, 0, 0}};
     V4 touch = V4{0, 0, 0, 0};
-    const bool prefetch = BV_PREFETCH && by_value && blockIdx.x == 0 && threadIdx.x < 64;
+    const bool prefetch = by_value && blockIdx.x == 0 && threadIdx.x < 64;
     /* a single record longer than MW_MAX_N GHASH elements runs on waves 0 and 1 at stride 128 (sparse_record S = 128):
      * wave 0 reads elements lane + 64 m, m < 4; it keeps m = 0, 2 and hands m = 1, 3 to wave 1 through LDS (XCH2) */
     const int n_one = BYVAL ? (((int)one.aad_len + 15) >> 4) + (((int)one.len + 15) >> 4) + 1 : 0;
@@ -843,12 +697,10 @@ __global__ void __launch_bounds__(WG)
     }
     /* the single record's wave 0 leaves the table build to the other waves: its prefetch loads are older than any T0
      * load it would issue, and vmcnt retires loads in order, so it would wait for its PCIe reads before its table stores */
-    if (!PLUGIN_PROBE) {
-        if (!BYVAL)
-            build_aes_tables<WG>(lds, 0, t0); /* the batch kernel's layout at offset 0 */
-        else if (threadIdx.x >= 64)
-            build_aes_tables<WG - 64>(lds, 0, t0, (int)threadIdx.x - 64);
-    }
+    if (!BYVAL)
+        build_aes_tables<WG>(lds, 0, t0); /* the batch kernel's layout at offset 0 */
+    else if (threadIdx.x >= 64)
+        build_aes_tables<WG - 64>(lds, 0, t0, (int)threadIdx.x - 64);
     /* a two-wave record (mw_record): wave 1's element lane + 64 was prefetched by wave 0 (pre[1]); it goes through LDS
      * (wave 3's table area, unused by a single record) */
     const bool mw = BYVAL && STAMP_PHASES == 0 && n_one >= MW_MIN_N && n_one <= MW_MAX_N;
@@ -912,22 +764,15 @@ __global__ void __launch_bounds__(WG)
     }
     const uint32_t waves = gridDim.x * (WG / 64);
     const uint32_t w0 = __builtin_amdgcn_readfirstlane(blockIdx.x * (WG / 64) + (threadIdx.x >> 6));
-    /* The deal of records (sorted by decreasing length) to the launch's waves, SPARSE_QUEUE:
-     *   0  static stride: wave w takes w, w + waves, w + 2 waves, ...; wave 0 takes the longest record of every round;
-     *   1  every record from the launch's queue word (greedy, longest first): ~65 K agent-scope atomics on one word per
-     *      c4s launch, whose return the record's first load wait takes (c4s 446 against 467-475 GiB/s static, one box);
-     *   2  snake: round k goes forward on even k and backward on odd k, so each wave's lengths pair long with short;
-     *   3  snake over the first nrecs - nrecs / SPARSE_TAIL records, the shortest tail from the queue word (a few claims
-     *      per wave, taking up what the waves' different speeds leave: the youngest wave on each SIMD, the slowest XCD).
-     * A queued claim is issued when the record before it starts, so its latency runs under that record; the last wave to
-     * claim past the end resets the words (engine.cpp queue_slot). */
-    const bool dyn = (SPARSE_QUEUE & 1) && !by_value && queue != nullptr;
-    const uint32_t nstat = !dyn ? nrecs : SPARSE_QUEUE == 1 ? 0u : nrecs - nrecs / SPARSE_TAIL;
-    auto stat_pos = [&](uint32_t k) -> uint32_t {
-        if (SPARSE_QUEUE >= 2)
-            return k * waves + ((k & 1u) ? waves - 1u - w0 : w0);
-        return w0 + k * waves;
-    };
+    /* The deal of records (sorted by decreasing length) to the launch's waves: a snake over the first
+     * nrecs - nrecs / SPARSE_TAIL records (round k goes forward on even k and backward on odd k, so each wave's lengths
+     * pair long with short), the shortest tail from the launch's queue word (a few claims per wave, taking up what the
+     * waves' different speeds leave: the youngest wave on each SIMD, the slowest XCD).  A queued claim is issued when the
+     * record before it starts, so its latency runs under that record; the last wave to claim past the end resets the words
+     * (engine.cpp queue_slot).  Measured alternatives (EXPERIMENTS.md): a static stride, every record from the queue. */
+    const bool dyn = !by_value && queue != nullptr;
+    const uint32_t nstat = !dyn ? nrecs : nrecs - nrecs / SPARSE_TAIL;
+    auto stat_pos = [&](uint32_t k) -> uint32_t { return k * waves + ((k & 1u) ? waves - 1u - w0 : w0); };
     auto claim = [&]() -> uint32_t { /* lane 0's returned value; read (readfirstlane) only when it is needed */
         uint32_t v = 0;
         if (lane == 0)
@@ -1015,16 +860,13 @@ __device__ __forceinline__ T *as_global(T *p)
     asm volatile("" : "+v"(v)); /* an opaque integer: the global pointer made from it cannot be folded back to a flat one */
     return (T *)((__attribute__((address_space(1))) T *)v);
 }
-/* WORKER_CONST: the key slot and basis pointers of a request are constant-address-space pointers, so the round keys come
+/* The key slot and basis pointers of a request are constant-address-space pointers (as_const), so the round keys come
  * through the scalar unit (s_load) as in a launched kernel (16 KiB record 28 -> 24 us per call, one ECB block 10.1 ->
  * 9.3 us; tools/calls_r04/r04_call8.sh).  Valid because a slot the resident dispatch may have read never changes while it
  * is resident (engine.cpp slot pool: a freed slot is reused only after that dispatch has left; the IV travels in the
  * request).  The round-3 attempt faulted, and so did this one's first build (r04_call7.sh): both rebuilt the 64-bit
  * pointer from two readfirstlane results, which return int, so an address with bit 31 set sign-extended over the high
  * half (s_bfe_i64 in the disassembly); as_const widens each half through uint32_t. */
-#ifndef WORKER_CONST
-#define WORKER_CONST 1
-#endif
 template <typename T>
 __device__ __forceinline__ const T *as_const(const T *p)
 {
@@ -1147,14 +989,14 @@ __global__ void __launch_bounds__(WORKER_WG)
         const uint4 ivo = (flags & WREQ_IV) ? uint4{rq.iv[0], rq.iv[1], rq.iv[2], 1u} : uint4{0, 0, 0, 0};
         const uint8_t *in = as_global(rq.in), *aad = as_global(rq.aad);
         uint8_t *out = as_global(rq.out);
-        const KeySlot *slots = WORKER_CONST ? as_const(rq.slots) : as_global(rq.slots);
+        const KeySlot *slots = as_const(rq.slots);
         uint32_t *done = as_global(rq.done);
         const uint32_t done_seq = __builtin_amdgcn_readfirstlane(rq.done_seq);
         const ptls_hip_supp_t *supp = rq.supp != nullptr ? as_global(rq.supp) : nullptr;
         const KeySlot *hp_slots = rq.hp_slots != nullptr ? as_global(rq.hp_slots) : nullptr;
         uint8_t *mask = rq.mask != nullptr ? as_global(rq.mask) : nullptr;
         uint64_t *result = as_global(rq.result);
-        const uint32_t *basis = WORKER_CONST ? as_const(rq.basis) : as_global(rq.basis);
+        const uint32_t *basis = as_const(rq.basis);
         const bool open = (flags & WREQ_OPEN) != 0, a256 = (flags & WREQ_AES256) != 0;
         const int na1 = ((int)rec.aad_len + 15) >> 4, nc1 = ((int)rec.len + 15) >> 4;
         const int n1 = na1 + nc1 + 1;

@@ -59,7 +59,7 @@ SIGNATURES = {
     "ptls_hip_batch_workgroup": (_i, [_vp]),
     "ptls_hip_batch_set_max_workgroups": (_i, [_vp, _i]),
     "ptls_hip_batch_grid": (_i, [_vp]),
-    "ptls_hip_batch_split_tasks": (_i, [_vp]),
+    "ptls_hip_batch_chunks": (_i, [_vp]),
     "ptls_hip_batch_set_clock": (_i, [_vp, _vp, _sz]),
     "ptls_hip_aesecb_init": (_i, [_vp, _i, _vp, _sz, _i]),
     "ptls_hip_aesecb_dispose": (None, [_vp]),
@@ -69,6 +69,7 @@ SIGNATURES = {
     "ptls_hip_aesgcm_seal_batch_supp": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "ptls_hip_aesecb_batch": (_i, [_vp, _vp, _vp, _sz, _vp, _vp, _vp]),
     "ptls_hip_fill_records": (_i, [_vp, _vp, _u64, _u64, _vp, _vp]),
+    "ptls_hip_device_copy": (_i, [_vp, _vp, _vp, _sz, _vp]),
     "ptls_hip_tls13_wire_size": (_sz, [_sz]),
     "ptls_hip_tls13_frame": (_sz, [_vp, _sz, _vp, _sz]),
     "ptls_hip_tls13_seal_batch": (_i, [_vp, _vp, _vp, _vp, _vp]),
@@ -185,6 +186,10 @@ class Engine:
         _check(lib().ptls_hip_aesecb_batch(self.ptr, hp_keyset.ptr, _ptr(supp), n, _ptr(src), _ptr(mask), _stream(stream)),
                "aesecb_batch")
 
+    def copy(self, dst, src, nbytes, stream=None):
+        """ptls_hip_device_copy: the 16-byte-per-lane streaming copy (bench.py's achievable-HBM reference)"""
+        _check(lib().ptls_hip_device_copy(self.ptr, _ptr(dst), _ptr(src), nbytes, _stream(stream)), "device_copy")
+
     def close(self):
         if self.ptr:
             lib().ptls_hip_engine_free(self.ptr)
@@ -269,9 +274,9 @@ class Batch:
         _check(lib().ptls_hip_batch_set_max_workgroups(self.ptr, n), "batch_set_max_workgroups")
 
     @property
-    def split_tasks(self):
-        """wave tasks the plan deals as two part tasks (split records)"""
-        return lib().ptls_hip_batch_split_tasks(self.ptr)
+    def chunks(self):
+        """chunks of the launch plan (key-slot runs of at most 32 wave tasks)"""
+        return lib().ptls_hip_batch_chunks(self.ptr)
 
     @property
     def grid(self):

@@ -193,9 +193,8 @@ int ptls_hip_batch_workgroup(ptls_hip_batch_t *batch);
  * count, the default).  For tests of the work distribution (a workgroup then takes several chunks of one
  * key run) and for sharing a device with other work. */
 int ptls_hip_batch_set_max_workgroups(ptls_hip_batch_t *batch, int n);
-/* wave tasks the launch plan deals as two part tasks each (split records: a key run's longest records when its tasks
- * are few for the workgroup's waves; lanes per record 16 and 32) */
-int ptls_hip_batch_split_tasks(ptls_hip_batch_t *batch);
+/* chunks of the launch plan (runs of one key slot, at most 32 wave tasks each; the sparse kernel's plan: one) */
+int ptls_hip_batch_chunks(ptls_hip_batch_t *batch);
 /* workgroups one seal/open launch of the batch uses (for sizing the clock-stamp buffer below) */
 int ptls_hip_batch_grid(ptls_hip_batch_t *batch);
 /* Diagnostic: the following launches of the batch write, per workgroup w, the shader-cycle counter and the constant
@@ -379,6 +378,9 @@ size_t ptls_hip_host_page_nodes(const void *ptr, size_t bytes, size_t stride, in
  * ------------------------------------------------------------------------------------------ */
 int ptls_hip_fill_records(ptls_hip_batch_t *batch, void *buf, uint64_t seed, uint64_t index_base, const uint64_t *index,
                           void *stream);
+/* The achievable-HBM reference of the roofline (bench.py): copy `bytes` (a multiple of 16; 16-byte aligned device
+ * pointers) from src to dst on the engine's device, 16 bytes per lane per access, asynchronously on `stream`. */
+int ptls_hip_device_copy(ptls_hip_engine_t *engine, void *dst, const void *src, size_t bytes, void *stream);
 
 #ifdef __cplusplus
 }

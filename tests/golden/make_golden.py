@@ -12,8 +12,12 @@ Outputs (data only -- inputs are re-derivable from the documented splitmix64 gen
                 full output for L <= 97.
   configs.json  per-BASELINE-config sample records (first/last 64 and shard seams, §8(c)(iii)):
                 SHA-256 of ct||tag per record.
+  c4_keyruns.npy  configs[3]'s WHOLE key runs of keys 0..255 (64 records each, 16 384 records, AES-256, mixed
+                lengths): SHA-256 of ct||tag per record, uint8[16384][32] in key-run order (key j's records
+                i = j + 65536 s, s = 0..63).  The config samples above hold <= 8 records per key, which the planner
+                sends to the sparse kernel; these runs take the 32-lane batch kernel the full configs[3] runs.
 
-Run:  make -C oracle && python3 tests/golden/make_golden.py
+Run:  make -C oracle && python3 tests/golden/make_golden.py [c4_keyruns]
 """
 import hashlib
 import json
@@ -70,9 +74,34 @@ def config_samples(cfg):
     return sorted(set(idx))
 
 
+C4_KEYRUN_KEYS = 256
+C4_KEYRUN_LEN = 64  # records per key in configs[3]: 4M records over 64K keys
+
+
+def c4_keyrun_index():
+    """record indices of configs[3]'s key runs 0..C4_KEYRUN_KEYS-1, in key-run order"""
+    keys = CONFIGS["c4_mixed_aes256_64k"]["keys"]
+    return [j + keys * s for j in range(C4_KEYRUN_KEYS) for s in range(C4_KEYRUN_LEN)]
+
+
+def make_c4_keyruns(o, r):
+    import numpy as np
+    cfg = CONFIGS["c4_mixed_aes256_64k"]
+    idx = c4_keyrun_index()
+    dig = np.zeros((len(idx), 32), dtype=np.uint8)
+    for k, i in enumerate(idx):
+        out = r.seal(*config_record(o, cfg, i))
+        dig[k] = np.frombuffer(hashlib.sha256(out).digest(), np.uint8)
+    np.save(os.path.join(HERE, "c4_keyruns.npy"), dig, allow_pickle=False)
+    print("c4_keyruns.npy written:", len(idx), "records")
+
+
 def main():
     o, r = Oracle(), Ref()
     assert Ref.available, "build oracle/_ref first (make -C oracle)"
+    if sys.argv[1:] == ["c4_keyruns"]:
+        make_c4_keyruns(o, r)
+        return
     zero = bytes(16384)
 
     # ---- KATs from t/fusion.c (data), re-run through the reference build ----
@@ -172,6 +201,7 @@ def main():
     with open(os.path.join(HERE, "configs.json"), "w") as f:
         json.dump(cfgs, f, indent=0)
     print("golden fixtures written:", len(sweep["vectors"]), "sweep vectors")
+    make_c4_keyruns(o, r)
 
 
 if __name__ == "__main__":

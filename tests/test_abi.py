@@ -226,13 +226,32 @@ def test_node_fails_loudly_without_device():
 
 
 @pytest.mark.skipif(shutil.which("/opt/rocm/bin/hipcc") is None, reason="hipcc missing")
-@pytest.mark.parametrize("switch", ["CTRHI_PROBE=1", "SPARSE_ABLATE=1", "DEAL_MUTANT=1"])
+@pytest.mark.parametrize("switch", ["DEAL_MUTANT=1", "DEAL_MUTANT=3", "KS_STAMPS=1"])
 def test_product_build_refuses_wrong_output_switches(switch, tmp_path):
-    """the product objects are compiled with PTLS_HIP_PRODUCT (hsig-picotls_amd/Makefile PROD): any timing-probe /
-    ablation / mutant switch (wrong output by design) is then a compile error, not a library"""
+    """the product objects are compiled with PTLS_HIP_PRODUCT (hsig-picotls_amd/Makefile PROD): a test-mutant switch
+    (wrong output by design) or a diagnostic one is then a compile error, not a library"""
     src = os.path.join(ROOT, "hsig-picotls_amd", "csrc", "sparse_kernel.hip")
     inc = ["-I" + os.path.join(ROOT, "include"), "-I" + os.path.join(ROOT, "hsig-picotls_amd", "csrc")]
     cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-std=c++17", "-fsyntax-only", "-DPTLS_HIP_PRODUCT=1", "-D" + switch,
            *inc, src]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
-    assert r.returncode != 0 and "timing-probe, ablation or test-mutant switch" in r.stderr
+    assert r.returncode != 0 and "test-mutant or diagnostic switch" in r.stderr
+
+
+def test_product_sources_carry_no_experiment_switches():
+    """the product sources hold the shipping design only.  Every preprocessor conditional in them is
+    an include guard, the x86 host pause, or one of the switches the builds use: the TEST-ONLY dealing mutants
+    (DEAL_MUTANT), the diagnostic stamp builds (KS_STAMPS, STAMP_PHASES, WORKER_STAMPS) and the product guard; the
+    rejected variants are measured in EXPERIMENTS.md, not kept in the code"""
+    import re
+    allowed = {"PTLS_HIP_BATCH_KERNEL_H", "PTLS_HIP_INTERNAL_H", "PTLS_HIP_GF128_H", "PTLS_HIP_H", "PTLS_HIP_PRODUCT", "DEAL_MUTANT",
+               "KS_STAMPS", "STAMP_PHASES", "WORKER_STAMPS", "__x86_64__", "__i386__", "GF128_FN"}
+    csrc = os.path.join(ROOT, "hsig-picotls_amd", "csrc")
+    seen = set()
+    for name in sorted(os.listdir(csrc)):
+        with open(os.path.join(csrc, name)) as f:
+            for ln in f:
+                m = re.match(r"\s*#\s*(if|ifdef|ifndef|elif)\b(.*)", ln)
+                if m:
+                    seen |= set(re.findall(r"[A-Za-z_][A-Za-z0-9_]*", m.group(2))) - {"defined"}
+    assert seen <= allowed, sorted(seen - allowed)

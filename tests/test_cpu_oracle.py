@@ -82,6 +82,26 @@ def test_config_samples(oracle, golden, name):
         assert hashlib.sha256(out).hexdigest() == rec["sha256"], rec["i"]
 
 
+def test_c4_keyruns_fixture(oracle, golden):
+    """tests/golden/c4_keyruns.npy (configs[3]'s whole key runs 0..255, lib/fusion.c digests): the oracle matches every
+    record of key runs 0, 1 and 255 and the first record of every run; the runs' records that configs.json also holds
+    (record i < 64: the first record of key run i) carry the same digest there"""
+    from make_golden import C4_KEYRUN_LEN, c4_keyrun_index
+    dig = np.load(os.path.join(HERE, "golden", "c4_keyruns.npy"), allow_pickle=False)
+    idx = c4_keyrun_index()
+    assert dig.shape == (len(idx), 32) and len(idx) == 256 * C4_KEYRUN_LEN
+    cfg = CONFIGS["c4_mixed_aes256_64k"]
+    check = set(range(0, len(idx), C4_KEYRUN_LEN)) | set(range(2 * C4_KEYRUN_LEN)) | set(range(len(idx) - C4_KEYRUN_LEN, len(idx)))
+    for k in sorted(check):
+        out = oracle.seal(*config_record(oracle, cfg, idx[k]))
+        assert hashlib.sha256(out).digest() == dig[k].tobytes(), idx[k]
+    sample = {r["i"]: r["sha256"] for r in golden["configs"]["configs"]["c4_mixed_aes256_64k"]["records"]}
+    shared = [k for k, i in enumerate(idx) if i in sample]
+    assert len(shared) == 64
+    for k in shared:
+        assert dig[k].tobytes().hex() == sample[idx[k]]
+
+
 def test_generator_matches_bench(oracle):
     """bench.py's vectorised splitmix64 workload generator == the oracle's scalar one"""
     sys.path.insert(0, os.path.dirname(HERE))

@@ -1,7 +1,8 @@
 """The multi-rank bench path on hardware (never run on a GPU before round 3): `bench.py --gpus 2` starts
 its own two ranks (torch.distributed.run, gloo for the barriers and the timing summary, no RCCL), here both on device 0
 (--device 0), each sealing / opening its own shard of configs[4] and checking its sealed records against the
-lib/fusion.c digests of tests/golden/configs.json."""
+lib/fusion.c digests of tests/golden/configs.json; rank 0 then times the reference's CPU engines with the GPUs idle, so
+the N > 1 line carries its cpu_baseline too."""
 import json
 import os
 import subprocess
@@ -26,7 +27,7 @@ def _bench(*args, timeout=300):
 
 def test_bench_two_ranks_on_one_device():
     rc, lines, err = _bench("--gpus", "2", "--device", "0", "--config", "c5", "--records", "65536", "--steps", "2",
-                            "--warmup", "1", "--no-cpu-baseline", "--e2e-records", "20000", "--no-plugin")
+                            "--warmup", "1", "--cpu-sample-mib", "64", "--e2e-records", "20000", "--no-plugin")
     assert rc == 0, err[-4000:]
     assert len(lines) == 1
     r = lines[0]
@@ -41,6 +42,11 @@ def test_bench_two_ranks_on_one_device():
     e = r["host_e2e_node"]
     assert e["devices"] == [0, 0] and len(e["per_device"]) == 2 and e["seal_open_gibps"] > 0
     assert e["parity"]["open_all_ok"] and e["parity"]["roundtrip_bytes_equal"] and e["parity"]["golden_records_checked"] >= 64
+    # an N > 1 line carries its own CPU baseline (rank 0, GPUs idle), with the labelled whole-host extrapolation
+    c = r["cpu_baseline"]
+    assert c["kind"] == "reference" and c["cores"] >= 1 and c["value"] > 0, c
+    x = c["full_host_extrapolation"]
+    assert x["kind"].startswith("extrapolation") and x["physical_cores"] >= c["cores"] and x["gibps"] > c["single_core"]
 
 
 def test_bench_node_e2e_device_listed_twice():

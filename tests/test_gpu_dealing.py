@@ -27,7 +27,7 @@ def test_cross_chunk_dealing_parity(engine, oracle, lanes, key_len):
     assert dealing_case.mismatches(engine, oracle, key_len, lanes) == (0, 0)
 
 
-@pytest.mark.parametrize("lanes", [8, 16])
+@pytest.mark.parametrize("lanes", [8, 16, 32])
 @pytest.mark.parametrize("mutant", [1, 2])
 def test_dealing_mutants_are_caught(mutant, lanes):
     lib = os.path.join(MUTANTS, f"libptls_hip_deal{mutant}.so")

@@ -1,5 +1,5 @@
-/* host check of csrc/bs8_aes.h against the oracle's FIPS-197 AES:
- *   g++ -O2 -std=c++17 -I hsig-picotls_amd/csrc -I oracle tools/bs_probe/bs8_check.cpp oracle/aesgcm_oracle.c -o /tmp/bs8_check
+/* host check of tools/bs_probe/bs8_aes.h against the oracle's FIPS-197 AES:
+ *   g++ -O2 -std=c++17 -I tools/bs_probe -I oracle tools/bs_probe/bs8_check.cpp oracle/aesgcm_oracle.c -o /tmp/bs8_check
  * (tests/test_bs8.py builds and runs it) */
 #include <stdio.h>
 #include <stdlib.h>

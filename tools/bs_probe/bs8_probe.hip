@@ -1,7 +1,7 @@
-/* bs8_probe.hip -- throughput probe of the 8-blocks-per-lane bit-sliced AES-CTR keystream (csrc/bs8_aes.h) on
+/* bs8_probe.hip -- throughput probe of the 8-blocks-per-lane bit-sliced AES-CTR keystream (tools/bs_probe/bs8_aes.h) on
  * gfx950: every lane XORs the keystream of 8 counter blocks into 8 consecutive-by-stride buffer blocks, in place.
  * Prints GiB/s per (rounds, waves per SIMD) and checks the first blocks against a host run of the same header.
- * Tool, not product:  hipcc --offload-arch=gfx950 -O3 -std=c++17 -I hsig-picotls_amd/csrc tools/bs_probe/bs8_probe.hip */
+ * Tool, not product:  hipcc --offload-arch=gfx950 -O3 -std=c++17 -I tools/bs_probe tools/bs_probe/bs8_probe.hip */
 #include <hip/hip_runtime.h>
 #pragma clang diagnostic ignored "-Wunused-result"
 #include <stdio.h>

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Map the Boyar-Peralta AES S-box circuit (eprint 2009/191: 32 AND + 81 XOR/XNOR) onto 3-input lookup gates --
 gfx950's v_bitop3_b32 computes any boolean function of three 32-bit operands in one VALU instruction -- and emit
-the mapped circuit as C (hsig-picotls_amd/csrc/bs8_sbox.h).
+the mapped circuit as C (tools/bs_probe/bs8_sbox.h).
 
 Cut-based technology mapping: every node's 3-feasible cuts are enumerated, a cover is chosen by area flow and
 then improved by exact-area recovery passes with randomised tie-breaks; the best cover found is emitted.  Every
@@ -314,7 +314,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=400)
     ap.add_argument("--seed", type=int, default=1)
-    ap.add_argument("--out", default=os.path.join(os.path.dirname(__file__), "..", "..", "hsig-picotls_amd", "csrc", "bs8_sbox.h"))
+    ap.add_argument("--out", default=os.path.join(os.path.dirname(__file__), "bs8_sbox.h"))
     args = ap.parse_args()
     nodes, order = parse()
     S = aes_sbox()

@@ -1,6 +1,6 @@
 #!/bin/bash
 # build a tuning / ablation variant of the engine with extra defines:
-#   EXTRA="-DWG_ALT=768 -DPURE_BLOCKS=2" tools/build_variant.sh <name>  ->  hsig-picotls_amd/variants/libptls_hip_<name>.so
+#   EXTRA="-DKS_STAMPS=1" tools/build_variant.sh <name>  ->  hsig-picotls_amd/variants/libptls_hip_<name>.so
 # SRCS (optional) = the kernel sources that get EXTRA (default: all); the others reuse the product build's objects.
 set -e
 cd "$(dirname "$0")/../hsig-picotls_amd"
