@@ -467,8 +467,9 @@ def golden_check(cfg_name, idx, recs, d_ct):
 
 def device_copy_gbs(eng, nbytes=4 << 30, reps=5):
     """achievable HBM bandwidth in this session (report against the measured device-copy bandwidth too):
-    ptls_hip_device_copy, a streaming copy kernel with 16 bytes per lane per access (the shape MI355X_MICROARCH.md
-    measures 6.29 TB/s with), of nbytes, read + write counted, HIP events on the launch stream, median of reps.  The torch
+    ptls_hip_device_copy, a flat copy kernel with one 16-byte load and store per thread (the shape MI355X_MICROARCH.md
+    measures 6.29 TB/s with; tools/copy_probe: 6.19 TB/s, the best of 40 shapes), of nbytes, read + write counted, HIP
+    events on the launch stream, median of reps.  The torch
     uint8 copy_ this used until round 4 read ~4.9 TB/s and overstated frac_of_measured_copy; it is kept beside it."""
     import torch
     src = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
@@ -921,8 +922,8 @@ def main():
     report_ranks(result, per_rank, world, args.steps, elapsed)
     copy_gbs, torch_copy_gbs = device_copy_gbs(eng)
     result["roofline"]["measured_copy_gbs"] = copy_gbs
-    result["roofline"]["measured_copy_source"] = ("ptls_hip_device_copy: 16 B per lane per access, 4 GiB, read + write "
-                                                  "counted, HIP events, median of 5")
+    result["roofline"]["measured_copy_source"] = ("ptls_hip_device_copy: one 16-B load + store per thread, 4 GiB, read + "
+                                                  "write counted, HIP events, median of 5")
     result["roofline"]["torch_uint8_copy_gbs"] = torch_copy_gbs
     result["roofline"]["frac_of_measured_copy"] = round(achieved / copy_gbs, 4)
     if batch_kernel:  # the batch kernel's LDS model (the sparse-key kernel is latency-bound)

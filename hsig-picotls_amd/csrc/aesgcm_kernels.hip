@@ -361,26 +361,16 @@ __global__ void fill_records_kernel(const ptls_hip_record_t *recs, uint32_t n, u
     }
 }
 
-/* The achievable-HBM reference of bench.py's roofline (ptls_hip_device_copy): a plain streaming copy, 16 bytes per lane
- * per access, four independent 16-byte loads in flight per lane before their stores (a grid-stride loop over 4 KiB
- * per workgroup and step; MI355X_MICROARCH.md measures 6.29 TB/s with this shape, "float4 copy").  n16 = 16-byte units. */
+/* The achievable-HBM reference of bench.py's roofline (ptls_hip_device_copy): one 16-byte load and store per thread, a
+ * workgroup per 4 KiB, no loop.  Measured against grid-stride forms on one MI355X (tools/copy_probe, 4 GiB, read + write
+ * counted): this flat launch 6 190 GB/s (MI355X_MICROARCH.md: 6.29 TB/s for a float4 copy); 1-8 accesses per lane in
+ * a grid-stride loop over 2-64 workgroups per CU 4 460-5 400, nontemporal 4 730-5 540, one slice per workgroup
+ * 5 160-5 330, hipMemcpyAsync device to device 4 980 (profiles/r05_copy_probe.log). */
 __global__ void __launch_bounds__(256) copy16_kernel(const uint4 *__restrict__ src, uint4 *__restrict__ dst, size_t n16)
 {
-    constexpr size_t U = 4;
-    const size_t stride = (size_t)gridDim.x * 256 * U;
-    size_t i = (size_t)blockIdx.x * 256 * U + threadIdx.x;
-    for (; i + (U - 1) * 256 < n16; i += stride) {
-        uint4 v[U];
-#pragma unroll
-        for (size_t k = 0; k < U; ++k)
-            v[k] = src[i + k * 256];
-#pragma unroll
-        for (size_t k = 0; k < U; ++k)
-            dst[i + k * 256] = v[k];
-    }
-    for (size_t k = 0; k < U; ++k) /* the last, partial step (one workgroup) */
-        if (i + k * 256 < n16)
-            dst[i + k * 256] = src[i + k * 256];
+    const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+    if (i < n16)
+        dst[i] = src[i];
 }
 
 } // namespace ptls_hip
@@ -437,8 +427,9 @@ int launch_fill(const ptls_hip_record_t *recs, uint32_t n, uint8_t *buf, uint64_
     return (int)hipGetLastError();
 }
 
-int launch_copy16(void *dst, const void *src, size_t n16, unsigned grid, void *stream)
+int launch_copy16(void *dst, const void *src, size_t n16, void *stream)
 {
+    const unsigned grid = (unsigned)((n16 + 255) / 256);
     hipLaunchKernelGGL(copy16_kernel, dim3(grid), dim3(256), 0, static_cast<hipStream_t>(stream), static_cast<const uint4 *>(src),
                        static_cast<uint4 *>(dst), n16);
     return (int)hipGetLastError();

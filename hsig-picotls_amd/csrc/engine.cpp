@@ -113,42 +113,45 @@ struct st_ptls_hip_engine_t {
     std::atomic<uint32_t> queue_next; /* the slot the next batch launch takes */
     uint32_t queue_slots;             /* slots in the round robin: QUEUE_SLOTS (PTLS_HIP_QUEUE_SLOTS: fewer, for tests) */
     hipStream_t util;                 /* descriptor / keyset allocation, zeroing and release (dev_alloc / dev_free) */
+    hipMemPool_t pool;                /* the engine's own device memory pool (dev_alloc), or nullptr: hipMalloc */
 };
 
 /* Device memory of keysets and batches.  hipFree synchronizes the whole device, so it would wait for a resident plugin
  * worker (up to its lifetime) and for other threads' work; stream-ordered allocation on the engine's own stream does
- * not (the objects' users are waited for through their launch events, Uses below).  hipMalloc where the runtime has no
- * stream-ordered allocator. */
-static bool async_alloc_ok(void)
+ * not (the objects' users are waited for through their launch events, Uses below).  The allocations come from the
+ * engine's OWN memory pool (the device's default pool belongs to the whole process: ADVICE r04), which keeps what is freed
+ * into it (release threshold: never), since otherwise every stream-ordered free returns memory to the driver at the next
+ * synchronization and the next allocation maps it again, which waits for the device like hipMalloc / hipFree do.
+ * hipMalloc / hipFree where the runtime has no memory pools. */
+static hipMemPool_t engine_pool_new(int device)
 {
-    static const bool ok = [] {
-        int dev = 0, v = 0;
-        return hipGetDevice(&dev) == hipSuccess && hipDeviceGetAttribute(&v, hipDeviceAttributeMemoryPoolsSupported, dev) == hipSuccess &&
-               v != 0;
-    }();
-    return ok;
-}
-
-/* the device's default pool keeps what is freed into it (release threshold: never): otherwise every stream-ordered free
- * returns memory to the driver at the next synchronization and the next allocation maps it again, which waits for the
- * device like hipMalloc / hipFree do */
-static void pool_keep_memory(int device)
-{
-    if (!async_alloc_ok())
-        return;
+    int v = 0;
+    if (hipDeviceGetAttribute(&v, hipDeviceAttributeMemoryPoolsSupported, device) != hipSuccess || v == 0) {
+        (void)hipGetLastError();
+        return nullptr;
+    }
+    hipMemPoolProps props{};
+    props.allocType = hipMemAllocationTypePinned;
+    props.handleTypes = hipMemHandleTypeNone;
+    props.location.type = hipMemLocationTypeDevice;
+    props.location.id = device;
     hipMemPool_t pool = nullptr;
+    if (hipMemPoolCreate(&pool, &props) != hipSuccess) {
+        (void)hipGetLastError();
+        return nullptr;
+    }
     uint64_t keep = UINT64_MAX;
-    if (hipDeviceGetDefaultMemPool(&pool, device) == hipSuccess)
-        (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep);
+    (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep);
     (void)hipGetLastError();
+    return pool;
 }
 
 static hipError_t dev_alloc(ptls_hip_engine_t *e, void **p, size_t bytes)
 {
     *p = nullptr;
-    if (!async_alloc_ok())
+    if (e->pool == nullptr)
         return hipMalloc(p, bytes);
-    hipError_t r = hipMallocAsync(p, bytes, e->util);
+    hipError_t r = hipMallocFromPoolAsync(p, bytes, e->pool, e->util);
     if (r == hipSuccess)
         r = hipStreamSynchronize(e->util); /* usable from any stream once the call returns */
     return r;
@@ -158,7 +161,7 @@ static void dev_free(ptls_hip_engine_t *e, void *p)
 {
     if (p == nullptr)
         return;
-    if (!async_alloc_ok())
+    if (e->pool == nullptr)
         (void)hipFree(p);
     else
         (void)hipFreeAsync(p, e->util);
@@ -337,6 +340,7 @@ extern "C" ptls_hip_engine_t *ptls_hip_engine_new(int device)
     e->queue_next = 0;
     e->queue_slots = queue_slots_env();
     e->util = nullptr;
+    e->pool = nullptr;
     if (hipMalloc(&e->d_t0, sizeof(t0)) != hipSuccess || hipMemcpy(e->d_t0, t0, sizeof(t0), hipMemcpyHostToDevice) != hipSuccess ||
         hipMalloc(&e->d_queue, 2 * sizeof(uint32_t) * QUEUE_SLOTS) != hipSuccess ||
         hipMemset(e->d_queue, 0, 2 * sizeof(uint32_t) * QUEUE_SLOTS) != hipSuccess ||
@@ -349,7 +353,7 @@ extern "C" ptls_hip_engine_t *ptls_hip_engine_new(int device)
         delete e;
         return nullptr;
     }
-    pool_keep_memory(device);
+    e->pool = engine_pool_new(device);
     if (engine_self_check(e) != 0) {
         const std::string why = g_err;
         ptls_hip_engine_free(e);
@@ -368,6 +372,8 @@ extern "C" void ptls_hip_engine_free(ptls_hip_engine_t *e)
     (void)hipStreamDestroy(e->util);
     (void)hipFree(e->d_t0);
     (void)hipFree(e->d_queue);
+    if (e->pool != nullptr) /* keysets and batches are freed before their engine (their frees are stream-ordered on util) */
+        (void)hipMemPoolDestroy(e->pool);
     delete e;
 }
 
@@ -461,7 +467,9 @@ extern "C" int ptls_hip_keyset_set(ptls_hip_keyset_t *ks, size_t first, size_t c
     hipStream_t s = static_cast<hipStream_t>(stream);
     uint8_t *d_tmp = nullptr;
     const size_t kbytes = count * ks->key_size, ibytes = count * 12;
-    HIP_TRY(hipMalloc(&d_tmp, kbytes + ibytes), PTLS_HIP_ENOMEM);
+    /* stream-ordered (dev_alloc): a hipMalloc / hipFree pair would wait for all device work, a resident plugin worker
+     * included */
+    HIP_TRY(dev_alloc(ks->eng, reinterpret_cast<void **>(&d_tmp), kbytes + ibytes), PTLS_HIP_ENOMEM);
     int rc = 0;
     if (hipMemcpyAsync(d_tmp, keys, kbytes, hipMemcpyHostToDevice, s) != hipSuccess ||
         hipMemcpyAsync(d_tmp + kbytes, ivs, ibytes, hipMemcpyHostToDevice, s) != hipSuccess) {
@@ -478,7 +486,7 @@ extern "C" int ptls_hip_keyset_set(ptls_hip_keyset_t *ks, size_t first, size_t c
      * uploads and the key setup on the same stream, whatever path got here */
     (void)hipMemsetAsync(d_tmp, 0, kbytes + ibytes, s);
     (void)hipStreamSynchronize(s);
-    (void)hipFree(d_tmp);
+    dev_free(ks->eng, d_tmp); /* after the scrub: the stream was synchronized */
     if (rc == 0)
         std::memcpy(&ks->ivs[first * 12], ivs, ibytes);
     return rc;
@@ -497,7 +505,7 @@ static int keyset_from_secrets(ptls_hip_keyset_t *ks, size_t first, size_t count
     hipStream_t s = static_cast<hipStream_t>(stream);
     const size_t sbytes = count * hash_size, kbytes = count * ks->key_size, ibytes = count * 12;
     uint8_t *d = nullptr;
-    HIP_TRY(hipMalloc(&d, 2 * sbytes + kbytes + ibytes), PTLS_HIP_ENOMEM);
+    HIP_TRY(dev_alloc(ks->eng, reinterpret_cast<void **>(&d), 2 * sbytes + kbytes + ibytes), PTLS_HIP_ENOMEM);
     uint8_t *d_sec = d, *d_next = d + sbytes, *d_keys = d + 2 * sbytes, *d_ivs = d + 2 * sbytes + kbytes;
     std::vector<uint8_t> h_ivs(ibytes);
     int rc = 0;
@@ -517,7 +525,7 @@ static int keyset_from_secrets(ptls_hip_keyset_t *ks, size_t first, size_t count
     /* secrets and raw keys do not stay in device memory outside the expanded slots */
     (void)hipMemsetAsync(d, 0, 2 * sbytes + kbytes + ibytes, s);
     (void)hipStreamSynchronize(s);
-    (void)hipFree(d);
+    dev_free(ks->eng, d); /* after the scrub: the stream was synchronized */
     if (rc == 0)
         std::memcpy(&ks->ivs[first * 12], h_ivs.data(), ibytes);
     std::fill(h_ivs.begin(), h_ivs.end(), 0);
@@ -1127,10 +1135,9 @@ extern "C" int ptls_hip_device_copy(ptls_hip_engine_t *eng, void *dst, const voi
     if (bytes == 0)
         return 0;
     DeviceGuard g(eng->device);
-    const size_t n16 = bytes / 16;
-    /* 4 KiB per workgroup and step; enough workgroups for 8 waves per CU, fewer for a small copy */
-    const unsigned grid = (unsigned)std::max<size_t>(1, std::min<size_t>((n16 + 1023) / 1024, (size_t)eng->ncu * 8));
-    const int e = launch_copy16(dst, src, n16, grid, stream);
+    if (bytes / 16 > (size_t)0xffffffffu * 256)
+        return fail(PTLS_HIP_EINVAL, "device_copy: at most 2^32 - 1 workgroups of 4 KiB");
+    const int e = launch_copy16(dst, src, bytes / 16, stream);
     return e != 0 ? fail(PTLS_HIP_ELAUNCH, "device_copy: launch failed: %s", hipGetErrorString((hipError_t)e)) : 0;
 }
 
@@ -2255,6 +2262,9 @@ struct PluginWorker {
     hipStream_t stream = nullptr;
     unsigned n = 0;
     WorkerSlot *h_mb = nullptr, *d_mb = nullptr;
+    /* set (release) once worker_init has filled every field above; the unlocked fast paths test it (acquire) before they
+     * read h_mb, n, d_mb or eng (a plain pointer store published nothing) */
+    std::atomic<bool> ready{false};
     uint64_t *d_activity = nullptr;   /* the last time any workgroup served a request (100 MHz ticks) */
     std::atomic<uint32_t> epoch{0};   /* of the last dispatch launched; h_mb[j].exited == epoch: workgroup j has left */
     std::atomic<bool> launched{false};
@@ -2312,7 +2322,7 @@ static bool worker_drained(const PluginWorker &w, uint32_t epoch)
 static void worker_atexit(void)
 {
     PluginWorker &w = g_worker;
-    if (w.h_mb == nullptr || !w.launched.load())
+    if (!w.ready.load(std::memory_order_acquire) || !w.launched.load())
         return;
     for (unsigned j = 0; j < w.n; ++j)
         __atomic_store_n(&w.h_mb[j].quit, 1u, __ATOMIC_RELEASE);
@@ -2325,7 +2335,7 @@ static void worker_atexit(void)
  * engine's device */
 static void worker_init(PluginWorker &w, ptls_hip_engine_t *eng)
 {
-    if (w.h_mb != nullptr)
+    if (w.ready.load(std::memory_order_acquire))
         return;
     DeviceGuard g(eng->device);
     const unsigned n = worker_count();
@@ -2348,8 +2358,9 @@ static void worker_init(PluginWorker &w, ptls_hip_engine_t *eng)
     w.eng = eng;
     w.n = n;
     w.d_mb = static_cast<WorkerSlot *>(d);
-    w.h_mb = h; /* published last: readers test h_mb first */
+    w.h_mb = h;
     atexit(worker_atexit);
+    w.ready.store(true, std::memory_order_release); /* published last: the fast paths test `ready` first */
 }
 
 /* With mailbox j's lock held: a dispatch whose workgroup j has not left.  A dispatch in which it has left is drained first
@@ -2424,7 +2435,7 @@ static unsigned worker_acquire(PluginWorker &w)
 static double g_worker_call_us = 0;
 extern "C" int ptls_hip_diag_worker_stamps(uint64_t *out, double *call_us)
 {
-    if (g_worker.h_mb == nullptr)
+    if (!g_worker.ready.load(std::memory_order_acquire))
         return -1;
     for (int i = 0; i < 5; ++i)
         out[i] = __atomic_load_n(&g_worker.h_mb->stamps[i], __ATOMIC_ACQUIRE);
@@ -2669,7 +2680,7 @@ static void pool_release(ptls_hip_keyset_t *ks)
     plugin_check(hipEventRecord(ev, s), "hipEventRecord(pool)");
     pool_stream_put(s);
     const PluginWorker &w = g_worker;
-    const uint32_t ep = w.h_mb != nullptr && w.launched.load() ? w.epoch.load() : 0;
+    const uint32_t ep = w.ready.load(std::memory_order_acquire) && w.launched.load() ? w.epoch.load() : 0;
     std::lock_guard<std::mutex> lk(g_pool.mu);
     g_pool.retired[c].push_back(SlotPool::Retired{id, ep, ev});
 }
@@ -2721,7 +2732,7 @@ static void ecb_block(hip_ctr_state *st, const void *src, uint8_t dst[16])
     if (worker_enabled() && !ecb_by_launch()) {
         /* through the worker: the block travels in the mailbox with the request (WREQ_ECB) */
         PluginWorker &w = g_worker;
-        if (w.h_mb == nullptr) {
+        if (!w.ready.load(std::memory_order_acquire)) {
             std::lock_guard<std::mutex> lk(w.launch_mu);
             worker_init(w, st->eng);
         }
@@ -2982,7 +2993,7 @@ static uint64_t plugin_run(hip_aead_state *st, bool open, void *output, const vo
     uint64_t result = len;
     if (worker_enabled() && !STAMP_PHASES) {
         PluginWorker &w = g_worker;
-        if (w.h_mb == nullptr) {
+        if (!w.ready.load(std::memory_order_acquire)) {
             std::lock_guard<std::mutex> lk(w.launch_mu);
             worker_init(w, st->eng);
         }

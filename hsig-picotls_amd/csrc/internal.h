@@ -168,7 +168,7 @@ int launch_derive_traffic_keys(const uint8_t *secrets_in, uint8_t *secrets_out, 
                                int update, uint8_t *keys, uint8_t *ivs, void *stream);
 int launch_fill(const ptls_hip_record_t *recs, uint32_t n, uint8_t *buf, uint64_t seed, uint64_t index_base,
                 const uint64_t *index, unsigned grid, void *stream);
-int launch_copy16(void *dst, const void *src, size_t n16, unsigned grid, void *stream);
+int launch_copy16(void *dst, const void *src, size_t n16, void *stream);
 
 } // namespace ptls_hip
 

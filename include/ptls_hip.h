@@ -379,7 +379,7 @@ size_t ptls_hip_host_page_nodes(const void *ptr, size_t bytes, size_t stride, in
 int ptls_hip_fill_records(ptls_hip_batch_t *batch, void *buf, uint64_t seed, uint64_t index_base, const uint64_t *index,
                           void *stream);
 /* The achievable-HBM reference of the roofline (bench.py): copy `bytes` (a multiple of 16; 16-byte aligned device
- * pointers) from src to dst on the engine's device, 16 bytes per lane per access, asynchronously on `stream`. */
+ * pointers) from src to dst on the engine's device, one 16-byte load and store per thread, asynchronously on `stream`. */
 int ptls_hip_device_copy(ptls_hip_engine_t *engine, void *dst, const void *src, size_t bytes, void *stream);
 
 #ifdef __cplusplus

@@ -3,9 +3,11 @@ serve plugin calls from pinned mailboxes (one per calling thread) instead of one
 reference's own picotls lifecycle code (tests/plugin_driver.py) and every output is compared with lib/fusion.c
 (oracle/_ref): calls separated by gaps longer than the worker's idle timeout (it leaves, the next call relaunches it),
 IV changes (ptls_aead_xor_iv: the IV travels in the request), contexts created and freed between calls (a freed pooled
-key slot comes back with other keys once no resident workgroup can hold it), header-protection ECB blocks (one launch each) and
-fused header protection interleaved with AEAD calls on the worker, and two threads sharing it.  Each case runs in its
-own process, with the worker on (the default) and off (PTLS_HIP_PLUGIN_WORKER=0: one launch per call).
+key slot comes back with other keys once no resident workgroup can hold it), header-protection ECB blocks (through the
+worker's mailbox, WREQ_ECB, by default; one launch each with PTLS_HIP_ECB_LAUNCH=1) and fused header protection
+interleaved with AEAD calls on the worker, and two threads sharing it.  Each case runs in its own process: worker on
+(the default) with ECB blocks through the worker or launched, and worker off (PTLS_HIP_PLUGIN_WORKER=0: one launch per
+call).
 test_plugin_worker_threads: eight threads with their own contexts at once over 1, 4 and 8 mailboxes (shared homes, the
 try-lock hand-off, a workgroup leaving while the others serve), with IV changes, context churn on every thread (pooled
 slots recycled while other threads' requests run), records too long for a mailbox (the context's own staging) and gaps
@@ -263,13 +265,13 @@ def test_plugin_worker_threads(workers):
     assert r.returncode == 0 and r.stdout.strip().endswith("ok"), (r.returncode, r.stdout[-2000:], r.stderr[-3000:])
 
 
-@pytest.mark.parametrize("worker", ["1", "0"])
-def test_plugin_worker_lifecycle(worker):
+@pytest.mark.parametrize("worker,ecb_launch", [("1", "0"), ("1", "1"), ("0", "0")])
+def test_plugin_worker_lifecycle(worker, ecb_launch):
     from oracle_lib import Ref
     if not Ref.available:
         pytest.skip("oracle/_ref not built")
     paths = [os.path.join(ROOT, "tests"), os.path.join(ROOT, "hsig-picotls_amd"), ROOT]
-    env = dict(os.environ, PTLS_HIP_PLUGIN_WORKER=worker)
+    env = dict(os.environ, PTLS_HIP_PLUGIN_WORKER=worker, PTLS_HIP_ECB_LAUNCH=ecb_launch)
     r = subprocess.run([sys.executable, "-c", _CASE.format(paths=paths)], env=env, capture_output=True, text=True,
                        timeout=240)
     assert r.returncode == 0 and r.stdout.strip().endswith("ok"), (r.returncode, r.stdout[-2000:], r.stderr[-3000:])
