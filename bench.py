@@ -108,8 +108,14 @@ def rank_range(cfg, rank, world, scaling, n_total=None):
     return b[rank], b[rank + 1]
 
 
-def make_workload(cfg, rank, world=1, scaling="weak", n_full=None):
-    """per-rank record descriptors, in key-major order (records of one key adjacent)"""
+def record_align(align=None):
+    """the byte alignment of each record's offsets: --align, else PTLS_BENCH_ALIGN (environment, the tools' knob), else 128"""
+    return int(align or os.environ.get("PTLS_BENCH_ALIGN", "128"))
+
+
+def make_workload(cfg, rank, world=1, scaling="weak", n_full=None, align=None):
+    """per-rank record descriptors, in key-major order (records of one key adjacent), each record's input and output at
+    a multiple of `align` bytes (record_align)"""
     import ptls_hip
     lo, hi = rank_range(cfg, rank, world, scaling, n_full)
     n = hi - lo
@@ -126,10 +132,10 @@ def make_workload(cfg, rank, world=1, scaling="weak", n_full=None):
         seq = (idx // K).astype(np.uint64)
     lens = record_lengths(cfg, idx)
     aad_len = 5 if cfg["aad"] == "tls" else 13
-    # records at 128-byte (L2 line) aligned offsets: no line holds the end of one record and the start of the next, which
-    # different waves would write at different times (c3 at 16-byte alignment: 1.21x the algorithmic HBM bytes, at 128:
-    # 1.05x, seal 5.15 -> 4.97 ms; profiles/r03_traffic_c3_align*.json).  PTLS_BENCH_ALIGN (environment) overrides it.
-    align = int(os.environ.get("PTLS_BENCH_ALIGN", "128"))
+    # records at 128-byte (L2 line) aligned offsets by default: no line holds the end of one record and the start of the
+    # next, which different waves write at different times.  --align 16 packs them as a QUIC stack's datagram buffers
+    # would (c3: 1.11x the algorithmic HBM bytes against 1.05x at 128, profiles/traffic_c3_packed.json)
+    align = record_align(align)
     recs, in_total, out_total, _ = ptls_hip.layout_records(lens, np.full(n, aad_len), keyslot, seq, align=align)
     recs["aad_off"] = np.arange(n, dtype=np.uint64) * np.uint64(16)
     return idx, recs, in_total, out_total, lens
@@ -573,7 +579,7 @@ def node_e2e(args, cfg, devices):
     records that have a lib/fusion.c digest in tests/golden/configs.json are compared with it."""
     import torch
     import ptls_hip
-    idx, recs, in_total, out_total, lens = make_workload(cfg, 0, 1, "weak", CONFIGS[args.config]["n"])
+    idx, recs, in_total, out_total, lens = make_workload(cfg, 0, 1, "weak", CONFIGS[args.config]["n"], args.align)
     L_mean = float(lens.mean())
     n = args.e2e_records or max(1, min(len(recs), int((1 << 30) / L_mean)))
     sub, idx, lens = recs[:n].copy(), idx[:n], lens[:n]
@@ -687,7 +693,7 @@ def dry_run(args, cfg, world, rank):
     if world > 1:
         dist.init_process_group("gloo")
     lo, hi = rank_range(cfg, rank, world, args.scaling, CONFIGS[args.config]["n"])
-    idx, recs, in_total, out_total, lens = make_workload(cfg, rank, world, args.scaling, CONFIGS[args.config]["n"])
+    idx, recs, in_total, out_total, lens = make_workload(cfg, rank, world, args.scaling, CONFIGS[args.config]["n"], args.align)
     sum_L = int(lens.sum())
     if world > 1:
         dist.barrier()
@@ -718,6 +724,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--config", default="c2", choices=list(CONFIGS))
     ap.add_argument("--lanes", type=int, default=0)
+    ap.add_argument("--align", type=int, default=0, choices=[0, 16, 32, 64, 128, 256],
+                    help="byte alignment of every record's input and output (default 128, or PTLS_BENCH_ALIGN); 16 packs "
+                         "them back to back")
     ap.add_argument("--records", type=int, default=0, help="override records per GPU (smaller runs)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-mib", type=int, default=1024, help="records in the CPU baseline's sample (default 1 GiB)")
@@ -762,7 +771,7 @@ def main():
 
     eng = ptls_hip.Engine(dev)
     lo, hi = rank_range(cfg, rank, world, args.scaling, CONFIGS[args.config]["n"])
-    idx, recs, in_total, out_total, lens = make_workload(cfg, rank, world, args.scaling, CONFIGS[args.config]["n"])
+    idx, recs, in_total, out_total, lens = make_workload(cfg, rank, world, args.scaling, CONFIGS[args.config]["n"], args.align)
     n = len(recs)
     sum_L = int(lens.sum())
     aad = build_aad(cfg, idx, lens)
@@ -882,7 +891,7 @@ def main():
         "data": "synthetic (splitmix64 records, SURVEY.md §8(d)), generated in HBM",
         "config": {"workload": cfg["desc"], "records_per_gpu": n, "record_bytes": cfg["L"] or "mixed 64-16384",
                    "aad_bytes": aad_len, "keys": cfg["keys"], "key_bits": cfg["key_len"] * 8,
-                   "lanes_per_record": seal_b.lanes,
+                   "lanes_per_record": seal_b.lanes, "record_align": record_align(args.align),
                    "parallelism": (f"records sharded by range over {world} GPU(s), no collective" if args.scaling == "weak" else
                                    f"one batch of {cfg['n']} records split over {world} GPU(s) in byte-balanced contiguous "
                                    f"ranges, no collective")},

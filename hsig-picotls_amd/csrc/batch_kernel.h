@@ -28,6 +28,7 @@
 #define PTLS_HIP_BATCH_KERNEL_H
 
 #include <hip/hip_runtime.h>
+#include <type_traits>
 #include "internal.h"
 
 namespace ptls_hip {
@@ -1280,52 +1281,102 @@ __global__ void __launch_bounds__(WGT)
                 uint8_t *dst = out_p + 16 * (size_t)(i0 - na + pm0 * G);
                 const uint32_t cbase = (uint32_t)(i0 - na + pm0 * G) + 2u;
                 V4 pend[KP], bufA[KP], bufB[KP];
+                /* Deferred stores (seal of 16-byte aligned records whose output does not start on a 128-byte line).  An
+                 * iteration writes KP G blocks of each record; with the record at block offset lo != 0 of a line, its last
+                 * lo blocks fall into a line whose first 8 - lo blocks the NEXT iteration writes, a few microseconds later,
+                 * and L2 wrote such lines back as two partial lines (16-byte packed QUIC records: seal 1.21x the
+                 * algorithmic bytes).  Those lanes store the block one iteration late instead, with the rest of its line:
+                 * the value is `pend`, the ciphertext the next iteration hashes, so no register is added.  A task whose
+                 * records all start on a line (bench.py's layout) runs the plain loop: the choice is wave-uniform, taken
+                 * once per task, and each loop is its own copy of the code.  Open is not deferred: holding its plaintext
+                 * one iteration spills at 768 threads (EXPERIMENTS.md). */
+                constexpr bool DEFER_OK = !OPEN && ALIGNED && KP * G >= 8;
+                bool spill[KP];
+                int defer_any = 0;
+                {
+                    const int lo = DEFER_OK ? (int)(((uint32_t)(uintptr_t)out_p >> 4) & 7u) : 0; /* the record's line offset */
+                    const int jr = (i0 - na) & (G - 1); /* the lane's block position in an iteration's G-block group */
+#pragma unroll
+                    for (int b = 0; b < KP; ++b) {
+                        spill[b] = DEFER_OK && lo != 0 && jr + b * G >= KP * G - lo;
+                        defer_any |= spill[b] ? 1 : 0;
+                    }
+                }
                 /* ping-pong prefetch: iteration `it` consumes the buffer loaded one iteration earlier and refills
                  * the other one for it + 1 (clamped to the last iteration so the body stays branch-free).  Two
                  * named buffers instead of a copy keep the compiler from waiting on the fresh loads. */
 #pragma unroll
                 for (int b = 0; b < KP; ++b)
                     bufA[b] = load_full(src + 16 * b * G);
-                /* one branch-free iteration; `hash_pending` is a literal at every call site */
-                auto pure_iter = [&](int it, bool hash_pending, V4(&d)[KP], V4(&dn)[KP]) {
+                /* seal's store of output block b of iteration it (c): deferred by one iteration on spilling lanes (held:
+                 * the previous iteration's block) */
+                auto put = [&](auto defer_tag, int it, bool first, int b, const V4 &c, const V4 &held) __attribute__((always_inline)) {
+                    constexpr bool DEFER = decltype(defer_tag)::value;
                     const size_t o = (size_t)(it * KP * G) * 16;
-                    const size_t on = (size_t)(min(it + 1, npure - 1) * KP * G) * 16;
-                    V4 k[KP];
-                    uint32_t cw[KP];
-#pragma unroll
-                    for (int b = 0; b < KP; ++b) {
-                        dn[b] = load_full(src + on + 16 * b * G);
-                        cw[b] = bswap32(cbase + (uint32_t)((it * KP + b) * G));
-                        k[b] = V4{n0, n1, n2, cw[b]};
-                    }
-                    __builtin_amdgcn_sched_barrier(0); /* keep the prefetch at the top of the iteration */
-                    if (OPEN) {
-                        /* the input is the ciphertext: hash it in the same iteration */
-                        ctr_ghash<ROUNDS, KP, true>(lds, lb_aes, rk, cc, cw, k, y, d, gl);
-#pragma unroll
-                        for (int b = 0; b < KP; ++b)
-                            store_full(dst + o + 16 * b * G, v4xor(d[b], k[b]));
-                    } else {
-                        /* software pipelined: the ciphertext of iteration it is hashed during iteration it + 1 */
-                        if (hash_pending)
-                            ctr_ghash<ROUNDS, KP, true>(lds, lb_aes, rk, cc, cw, k, y, pend, gl);
-                        else
-                            ctr_ghash<ROUNDS, KP, false>(lds, lb_aes, rk, cc, cw, k, y, pend, gl);
-#pragma unroll
-                        for (int b = 0; b < KP; ++b) {
-                            pend[b] = v4xor(d[b], k[b]);
-                            store_full(dst + o + 16 * b * G, pend[b]);
-                        }
+                    if (!DEFER) {
+                        store_full(dst + o + 16 * b * G, c);
+                    } else if (first) { /* iteration 0: a spilling block waits for the next iteration */
+                        if (!spill[b])
+                            store_full(dst + o + 16 * b * G, c);
+                    } else { /* a spilling lane stores the previous iteration's block, the others this one's */
+                        const size_t op = (size_t)((it - 1) * KP * G) * 16;
+                        store_full(dst + (spill[b] ? op : o) + 16 * b * G, spill[b] ? held : c);
                     }
                 };
-                pure_iter(0, false, bufA, bufB);
-                int it = 1;
-                for (; it + 1 < npure; it += 2) {
-                    pure_iter(it, true, bufB, bufA);
-                    pure_iter(it + 1, true, bufA, bufB);
-                }
-                if (it < npure)
-                    pure_iter(it, true, bufB, bufA);
+                auto stretch = [&](auto defer_tag) __attribute__((always_inline)) {
+                    constexpr bool DEFER = decltype(defer_tag)::value;
+                    /* one branch-free iteration; `hash_pending` (false: iteration 0) is a literal at every call site */
+                    auto pure_iter = [&](int it, bool hash_pending, V4(&d)[KP], V4(&dn)[KP]) __attribute__((always_inline)) {
+                        const size_t on = (size_t)(min(it + 1, npure - 1) * KP * G) * 16;
+                        V4 k[KP];
+                        uint32_t cw[KP];
+#pragma unroll
+                        for (int b = 0; b < KP; ++b) {
+                            dn[b] = load_full(src + on + 16 * b * G);
+                            cw[b] = bswap32(cbase + (uint32_t)((it * KP + b) * G));
+                            k[b] = V4{n0, n1, n2, cw[b]};
+                        }
+                        __builtin_amdgcn_sched_barrier(0); /* keep the prefetch at the top of the iteration */
+                        if (OPEN) {
+                            /* the input is the ciphertext: hash it in the same iteration */
+                            ctr_ghash<ROUNDS, KP, true>(lds, lb_aes, rk, cc, cw, k, y, d, gl);
+#pragma unroll
+                            for (int b = 0; b < KP; ++b) {
+                                store_full(dst + (size_t)(it * KP * G) * 16 + 16 * b * G, v4xor(d[b], k[b]));
+                            }
+                        } else {
+                            /* software pipelined: the ciphertext of iteration it is hashed during iteration it + 1 */
+                            if (hash_pending)
+                                ctr_ghash<ROUNDS, KP, true>(lds, lb_aes, rk, cc, cw, k, y, pend, gl);
+                            else
+                                ctr_ghash<ROUNDS, KP, false>(lds, lb_aes, rk, cc, cw, k, y, pend, gl);
+#pragma unroll
+                            for (int b = 0; b < KP; ++b) {
+                                const V4 c = v4xor(d[b], k[b]);
+                                put(defer_tag, it, !hash_pending, b, c, pend[b]);
+                                pend[b] = c;
+                            }
+                        }
+                    };
+                    pure_iter(0, false, bufA, bufB);
+                    int it = 1;
+                    for (; it + 1 < npure; it += 2) {
+                        pure_iter(it, true, bufB, bufA);
+                        pure_iter(it + 1, true, bufA, bufB);
+                    }
+                    if (it < npure)
+                        pure_iter(it, true, bufB, bufA);
+                    if (DEFER) { /* the last iteration's deferred blocks */
+#pragma unroll
+                        for (int b = 0; b < KP; ++b)
+                            if (spill[b])
+                                store_full(dst + (size_t)((npure - 1) * KP * G) * 16 + 16 * b * G, pend[b]);
+                    }
+                };
+                if (DEFER_OK && wave_max(defer_any) != 0)
+                    stretch(std::true_type{});
+                else
+                    stretch(std::false_type{});
                 if (!OPEN) {
 #pragma unroll
                     for (int b = 0; b < KP; ++b)

@@ -4,7 +4,7 @@
 # then HBM traffic (FETCH_SIZE / WRITE_SIZE passes) of c3 at 16-byte packing on the new build
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}" || exit 1
 export HSA_ENABLE_IPC_MODE_LEGACY=0 TMPDIR=/tmp
-R=$PWD; O=$R/gpurun_out/r05c6; mkdir -p "$O"
+R=$PWD; O=$R/gpurun_out/r05c7; mkdir -p "$O"
 B=$R/hsig-picotls_amd/variants/libptls_hip_base.so; N=$R/hsig-picotls_amd/libptls_hip.so
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > "$O/gpu_tests.log" 2>&1
 rc=$?; tail -2 "$O/gpu_tests.log"; [ $rc -eq 0 ] || { grep -E "Error|assert|FAIL" "$O/gpu_tests.log" | head -20; exit $rc; }

@@ -1,10 +1,10 @@
 #!/bin/bash
-# round 5, call 6/7: the line-aligned stretch start (call 6) / the deferred spill stores (call 7, batch_kernel.h): GPU suite on it, then c3 at 16-byte packing and at
+# round 5, call 8: the deferred spill stores restricted to seal and to tasks with a record off a 128-byte line (batch_kernel.h, two loop copies): GPU suite on it, then c3 at 16-byte packing and at
 # 128-byte alignment, base (variants/libptls_hip_base.so, the previous product) vs new, alternating; c2 / c4 guard rows;
 # then HBM traffic (FETCH_SIZE / WRITE_SIZE passes) of c3 at 16-byte packing on the new build
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}" || exit 1
 export HSA_ENABLE_IPC_MODE_LEGACY=0 TMPDIR=/tmp
-R=$PWD; O=$R/gpurun_out/r05c6; mkdir -p "$O"
+R=$PWD; O=$R/gpurun_out/r05c8; mkdir -p "$O"
 B=$R/hsig-picotls_amd/variants/libptls_hip_base.so; N=$R/hsig-picotls_amd/libptls_hip.so
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > "$O/gpu_tests.log" 2>&1
 rc=$?; tail -2 "$O/gpu_tests.log"; [ $rc -eq 0 ] || { grep -E "Error|assert|FAIL" "$O/gpu_tests.log" | head -20; exit $rc; }
