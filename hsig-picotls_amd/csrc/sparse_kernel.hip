@@ -866,7 +866,7 @@ __device__ __forceinline__ T *as_global(T *p)
  * is resident (engine.cpp slot pool: a freed slot is reused only after that dispatch has left; the IV travels in the
  * request).  The round-3 attempt faulted, and so did this one's first build (r04_call7.sh): both rebuilt the 64-bit
  * pointer from two readfirstlane results, which return int, so an address with bit 31 set sign-extended over the high
- * half (s_bfe_i64 in the disassembly); as_const widens each half through uint32_t. */
+ * half (s_bfe_i64 in the disassembly); as_const widens each half through uint32_t (EXPERIMENTS.md E3, "worker requests with key material through the scalar unit"). */
 template <typename T>
 __device__ __forceinline__ const T *as_const(const T *p)
 {

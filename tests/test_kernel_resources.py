@@ -1,7 +1,7 @@
 """Register-budget guards read from the built gfx950 code objects (hsig-picotls_amd/build/*.o, no GPU needed): the kernel
 descriptors' private segment (scratch) sizes.
   - plugin_worker_kernel: none.  A resident kernel with scratch is the first suspect of the one GPU fault of round 3
-    (constant-space key pointers), and the worker must not touch memory it does not own.
+    (EXPERIMENTS.md E3: constant-space key pointers), and the worker must not touch memory it does not own.
   - the single-record launch (aesgcm_sparse_kernel, 256 threads): none (the plugin's latency path).
   - the sparse batch kernel (768 threads): at most 16 bytes per lane.  Scratch that lives across its record loop is
     evicted to HBM by the streaming records (c4s: 84 B per lane cost +4.9 KB of HBM traffic per record in round 3; round 4's

@@ -1,6 +1,6 @@
 /*
  * bitslice_aes.h -- EXPERIMENT (not linked into the engine): bit-sliced AES for gfx950, 32 blocks per
- * lane, computed on the VALU.  Measured and rejected, see DESIGN.md §4.7 and tools/bs_probe/README.md.
+ * lane, computed on the VALU.  Measured and rejected, see EXPERIMENTS.md E3 and tools/bs_probe/README.md.
  *
  * Why it was tried: the T-table path spends 138 ds_read_b32 per AES-128 block and is bound by the
  * LDS array (128 B/clk/CU), while the VALU (4 SIMD-32 = 128 lane-ops/clk/CU, v_bitop3 for any 3-input

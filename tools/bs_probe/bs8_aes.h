@@ -1,6 +1,6 @@
 /*
  * bs8_aes.h -- bit-sliced AES-CTR keystream, 8 blocks per lane, on the VALU (gfx950), for the batch kernel's
- * hybrid waves.
+ * hybrid waves (EXPERIMENTS.md E3, "hybrid waves").
  *
  * Why: the T-table path (batch_kernel.h) is bound by the LDS array (138 ds_read_b32 + 16 ds_read_b128 per
  * AES-128 block, 89 % busy on c2) while the VALU idles ~55 % of the time.  Bit-sliced AES needs no tables at
