@@ -584,7 +584,7 @@ extern "C" int ptls_hip_keyset_xor_iv(ptls_hip_keyset_t *ks, size_t slot, const 
  * records each (a server's connections): a workgroup works on one key at a time (its GHASH tables fill
  * the LDS), so with 8 lanes a 64-record key run gives only 8 wave tasks to 12 waves; 16 lanes per
  * record doubles the tasks per key run (measured on the 64K-key BASELINE shape). */
-static int choose_lanes(const ptls_hip_record_t *recs, size_t n)
+static int choose_lanes(const ptls_hip_record_t *recs, size_t n, unsigned ncu)
 {
     if (n == 0)
         return 1;
@@ -620,7 +620,18 @@ static int choose_lanes(const ptls_hip_record_t *recs, size_t n)
      * key 898 / 869 / -, one key 932 / 927 / - */
     if (mean >= 256 && per_run <= 320)
         return 8;
-    return g;
+    /* Small batches: a launch gives each CU 12 waves that draw wave tasks of 64/G records, so a batch of fewer than
+     * about two tasks per wave leaves most waves idle or waiting for one long last task.  More lanes per record make
+     * more, shorter tasks, as long as each lane keeps >= 8 GHASH elements.  Round 5, same box, seal GiB/s at G = 4 / 8 /
+     * 16 / 32 (tools/calls_r05/r05_call11.sh): c2's 16 KiB records, 4 096 records (64 MiB) 206 / 321 / 457 / 542,
+     * 16 384 573-590 / 682-693 / 872-973 / 885-900, 65 536 981-997 / 983-989 / 974-990 / 938-966, 262 144 1 172-1 176 /
+     * 1 179 / 1 173-1 176 / 1 144-1 149; c3's 1 350 B records at G = 2 / 4 / 8: 65 536 records 575 / 655-669 / 700-707,
+     * 786 432 893-904 / 906-910 / 860-864. */
+    int gs = g;
+    const double waves = 12.0 * (double)(ncu ? ncu : 256);
+    while (gs < 32 && (double)n * gs / 64.0 < 2.0 * waves && mean / (2.0 * gs) >= 8.0)
+        gs *= 2;
+    return gs;
 }
 
 /* grid of a launch: one workgroup per CU at most (both kernels fill the LDS); the batch kernel takes one
@@ -808,7 +819,7 @@ extern "C" ptls_hip_batch_t *ptls_hip_batch_new(ptls_hip_engine_t *eng, const pt
     b->max_key = 0;
     for (size_t i = 0; i < n; ++i)
         b->max_key = std::max(b->max_key, recs[i].key);
-    b->auto_lanes = b->lanes = choose_lanes(b->h_recs.data(), b->h_recs.size());
+    b->auto_lanes = b->lanes = choose_lanes(b->h_recs.data(), b->h_recs.size(), (unsigned)eng->ncu);
     if (n != 0) {
         if (dev_alloc(eng, reinterpret_cast<void **>(&b->d_recs), n * sizeof(ptls_hip_record_t)) != hipSuccess ||
             hipMemcpy(b->d_recs, recs, n * sizeof(ptls_hip_record_t), hipMemcpyHostToDevice) != hipSuccess) {
@@ -1406,9 +1417,9 @@ static void *mapped_span(const void *h, uint64_t need, bool *partial)
  * Records of >= 64 GHASH elements go to the wave-per-record kernel (one 1-KiB run per wave instruction): 16 / 32 / 64
  * lanes 1350-B records 36.5 / 39.2 / 40.4, 16-KiB records 40.1 / 41.5 / 42.7 (one 1-GiB batch each).
  * Batches for the sparse-key kernel keep it. */
-static int mapped_lanes(const ptls_hip_record_t *recs, size_t n)
+static int mapped_lanes(const ptls_hip_record_t *recs, size_t n, unsigned ncu)
 {
-    const int lanes = choose_lanes(recs, n);
+    const int lanes = choose_lanes(recs, n, ncu);
     if (lanes == SPARSE_LANES || n == 0)
         return lanes;
     double sum = 0;
@@ -1458,7 +1469,7 @@ static int pipeline_run_mapped(ptls_hip_pipeline_t *p, ptls_hip_keyset_t *ks, co
         if (s.busy)
             HIP_TRY(hipEventSynchronize(s.done), PTLS_HIP_ENODEV);
         std::memcpy(s.h_recs, recs + i, cnt * sizeof(ptls_hip_record_t));
-        const int lanes = mapped_lanes(s.h_recs, cnt);
+        const int lanes = mapped_lanes(s.h_recs, cnt, (unsigned)p->eng->ncu);
         bool aligned;
         build_chunks(s.h_recs, cnt, lanes, (unsigned)p->eng->ncu, ch, order, aligned);
         std::memcpy(s.h_chunks, ch.data(), ch.size() * sizeof(Chunk));
@@ -1683,7 +1694,7 @@ static int pipeline_run_copy(ptls_hip_pipeline_t *p, ptls_hip_keyset_t *ks, cons
             s.h_recs[t].out_off -= out_base;
             s.h_recs[t].aad_off -= aad_in_out ? out_base : aad_in_in ? in_base : aad_base;
         }
-        const int lanes = choose_lanes(s.h_recs, cnt);
+        const int lanes = choose_lanes(s.h_recs, cnt, (unsigned)p->eng->ncu);
         bool aligned;
         build_chunks(s.h_recs, cnt, lanes, (unsigned)p->eng->ncu, ch, order, aligned);
         const uint64_t mask_base = mk.lo & ~(uint64_t)15;
