@@ -55,8 +55,10 @@ constexpr int PURE_BLOCKS = 2; /* data blocks per lane per iteration of the bran
 #endif
 #ifndef KS_STAMPS
 #define KS_STAMPS 0 /* DIAGNOSTIC builds only (tools/keyswitch_stamps.py): every wave sums the shader cycles it spends at key
-                       switches (first barrier, table build, second barrier) and in total, into clk after the 4 x grid
-                       workgroup stamps: [workgroup][wave][total, barrier 1, build, barrier 2, switches] */
+                       switches (first barrier, table build, second barrier) and in total, and within its tasks (drawing
+                       the task, descriptors + AAD elements + counter-mode constants, the stretch, the generic rest, the
+                       combination + tag), into clk after the 4 x grid workgroup stamps: [workgroup][wave][total,
+                       barrier 1, build, barrier 2, switches, draw, setup, stretch, rest, combine] */
 #endif
 /* the chunk sequence a workgroup's waves walk: a ring in LDS of {sequence number, chunk} entries */
 constexpr int QRING = 32;
@@ -801,14 +803,19 @@ __device__ __forceinline__ V4 shl8_in(V4 v, uint8_t b)
               __builtin_amdgcn_alignbit(v.w3, v.w2, 24)};
 }
 
-/* exact byte-granular access (n in 0..16): compact loops, used for unaligned layouts and partial stores */
+/* exact byte-granular access (n in 0..16), used for unaligned layouts: the n byte loads are independent and all issued
+ * before the first use (one memory latency, where a loop carrying the block through its shifts waited n times) */
 __device__ __forceinline__ V4 load_bytes(const uint8_t *p, int n)
 {
-    V4 v = V4{0, 0, 0, 0};
-#pragma unroll 1
-    for (int k = n - 1; k >= 0; --k)
-        v = shl8_in(v, p[k]);
-    return v;
+    uint32_t b[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k)
+        b[k] = k < n ? (uint32_t)p[k] : 0u;
+    uint32_t w[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+        w[i] = b[4 * i] | (b[4 * i + 1] << 8) | (b[4 * i + 2] << 16) | (b[4 * i + 3] << 24);
+    return V4{w[0], w[1], w[2], w[3]};
 }
 
 __device__ __forceinline__ void store_bytes(uint8_t *p, int n, V4 v)
@@ -822,9 +829,10 @@ __device__ __forceinline__ void store_bytes(uint8_t *p, int n, V4 v)
 
 __device__ __forceinline__ V4 mask_block(V4 v, int n);
 
-/* n (0..15) bytes at a 16-byte aligned p as dword loads of the whole dwords, then single bytes: nothing past
- * p + n is read (fusion over-reads within the page, lib/fusion.c:345-388; a caller's allocation may end at
- * the record's last byte) */
+/* n (0..15) bytes at a 16-byte aligned p: the whole dwords as dword loads, the last 1..3 bytes as a 16-bit and / or an
+ * 8-bit load, all independent (one memory latency; a byte loop carrying the word waited once per byte).  Nothing past
+ * p + n is read (fusion over-reads within the page, lib/fusion.c:345-388; a caller's allocation may end at the record's
+ * last byte, SURVEY.md §5, tests/test_gpu_guard.py) */
 __device__ __forceinline__ V4 load_partial_aligned(const uint8_t *p, int n)
 {
     const uint32_t *q = reinterpret_cast<const uint32_t *>(p);
@@ -832,15 +840,10 @@ __device__ __forceinline__ V4 load_partial_aligned(const uint8_t *p, int n)
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         const int k = n - 4 * i;
-        uint32_t v = 0;
-        if (k >= 4) {
-            v = q[i];
-        } else if (k > 0) {
-#pragma unroll 1
-            for (int j = k - 1; j >= 0; --j)
-                v = (v << 8) | p[4 * i + j];
-        }
-        w[i] = v;
+        const uint32_t lo = k >= 4 ? q[i] : k >= 2 ? (uint32_t)*reinterpret_cast<const uint16_t *>(p + 4 * i)
+                                          : k == 1 ? (uint32_t)p[4 * i] : 0u;
+        const uint32_t hi = k == 3 ? (uint32_t)p[4 * i + 2] << 16 : 0u;
+        w[i] = lo | hi;
     }
     return V4{w[0], w[1], w[2], w[3]};
 }
@@ -855,6 +858,25 @@ __device__ __forceinline__ V4 load_block(const uint8_t *p, int n)
     return ALIGNED ? load_partial_aligned(p, n) : load_bytes(p, n);
 }
 
+/* n (0..15) bytes of v to a 16-byte aligned p: whole dwords, then a 16-bit and / or an 8-bit store (nothing past p + n) */
+__device__ __forceinline__ void store_partial_aligned(uint8_t *p, int n, V4 v)
+{
+    uint32_t *q = reinterpret_cast<uint32_t *>(p);
+    const uint32_t w[4] = {v.w0, v.w1, v.w2, v.w3};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int k = n - 4 * i;
+        if (k >= 4) {
+            q[i] = w[i];
+        } else if (k > 0) {
+            if (k >= 2)
+                *reinterpret_cast<uint16_t *>(p + 4 * i) = (uint16_t)w[i];
+            if (k != 2)
+                p[4 * i + k - 1] = (uint8_t)(w[i] >> (8 * (k - 1)));
+        }
+    }
+}
+
 template <bool ALIGNED>
 __device__ __forceinline__ void store_block(uint8_t *p, int n, V4 v)
 {
@@ -862,7 +884,10 @@ __device__ __forceinline__ void store_block(uint8_t *p, int n, V4 v)
         store_full(p, v);
         return;
     }
-    store_bytes(p, n, v);
+    if (ALIGNED)
+        store_partial_aligned(p, n, v);
+    else
+        store_bytes(p, n, v);
 }
 
 __device__ __forceinline__ V4 mask_block(V4 v, int n)
@@ -988,8 +1013,9 @@ __device__ __forceinline__ Elem elem_of(int i, int N, int na, int nc, int L, int
     return e;
 }
 
-/* AAD_IN: an AAD element's block is already in in_blk (loaded before the AES, sparse kernel) */
-template <bool OPEN, bool ALIGNED, bool AAD_IN = false>
+/* AAD_IN: an AAD element's block is already in in_blk (loaded before the AES, sparse kernel); WIDE_PARTIAL = false: a
+ * partial block is stored byte by byte even when aligned (the plugin worker, whose registers the wider form spills) */
+template <bool OPEN, bool ALIGNED, bool AAD_IN = false, bool WIDE_PARTIAL = true>
 __device__ __forceinline__ V4 finish_elem(const Elem &e, V4 in_blk, V4 ks, const uint8_t *aad_p, int A, int L, uint8_t *out_p,
                                           V4 &ek0)
 {
@@ -999,11 +1025,11 @@ __device__ __forceinline__ V4 finish_elem(const Elem &e, V4 in_blk, V4 ks, const
     } else if (e.is_c) {
         const V4 o = v4xor(in_blk, ks);
         if (OPEN) {
-            store_block<ALIGNED>(out_p + 16 * (size_t)e.c, e.nbytes, o);
+            store_block<ALIGNED && WIDE_PARTIAL>(out_p + 16 * (size_t)e.c, e.nbytes, o);
             x = in_blk;
         } else {
             x = mask_block(o, e.nbytes);
-            store_block<ALIGNED>(out_p + 16 * (size_t)e.c, e.nbytes, x);
+            store_block<ALIGNED && WIDE_PARTIAL>(out_p + 16 * (size_t)e.c, e.nbytes, x);
         }
     } else if (e.is_len) { /* [len(A)]64 || [len(C)]64 in bits, big-endian (lib/fusion.c:468) */
         x = V4{0, bswap32((uint32_t)A << 3), 0, bswap32((uint32_t)L << 3)};
@@ -1106,8 +1132,16 @@ __global__ void __launch_bounds__(WGT)
 
     clock_stamp(clk, 0);
     build_aes_tables<WGT>(lds, LDS_AES, t0);
-    uint64_t ks_acc[5] = {0, 0, 0, 0, 0}; /* KS_STAMPS: total, barrier 1, build, barrier 2, switches */
+    uint64_t ks_acc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0}; /* KS_STAMPS: see its definition */
     const uint64_t ks_t0 = KS_STAMPS ? __builtin_amdgcn_s_memtime() : 0;
+    uint64_t ks_last = ks_t0;
+    auto ks_phase = [&](int k) __attribute__((always_inline)) { /* the cycles since the previous mark go to phase k */
+        if (KS_STAMPS) {
+            const uint64_t t = __builtin_amdgcn_s_memtime();
+            ks_acc[k] += t - ks_last;
+            ks_last = t;
+        }
+    };
     uint32_t cur_key = 0xffffffffu;
     /* g = the wave's next task in the workgroup's same-key run of chunks (drawn, not yet used); cbase = tasks of the run's
      * chunks before the current one */
@@ -1133,6 +1167,7 @@ __global__ void __launch_bounds__(WGT)
                 ks_acc[2] += s2 - s1;
                 ks_acc[3] += s3 - s2;
                 ks_acc[4] += 1;
+                ks_last = s3;
             }
             cur_key = ch.key;
             cbase = 0;
@@ -1160,6 +1195,7 @@ __global__ void __launch_bounds__(WGT)
             if (t >= ntasks)
                 break; /* keep g for the next chunk of the run */
             have_g = false;
+            ks_phase(5);
             const uint32_t ridx = (uint32_t)t * R + grp;
             const bool valid = ridx < ch.count;
             /* descriptors in chunk order: the record is one load away (its caller index only matters for
@@ -1276,6 +1312,7 @@ __global__ void __launch_bounds__(WGT)
                 }
             }
             cc = ctr_const(lds, lb_aes, rk, n0, n1, n2);
+            ks_phase(6);
             if (npure) {
                 const uint8_t *src = in_p + 16 * (size_t)(i0 - na + pm0 * G);
                 uint8_t *dst = out_p + 16 * (size_t)(i0 - na + pm0 * G);
@@ -1383,6 +1420,7 @@ __global__ void __launch_bounds__(WGT)
                         y = gh_mul_main(lds, gl, y, pend[b]);
                 }
             }
+            ks_phase(7);
             /* the rest of each lane's elements from its own position (full blocks past the shortest lane's
              * stretch, the partial block, the length block); an element past the record is inactive */
             {
@@ -1398,6 +1436,7 @@ __global__ void __launch_bounds__(WGT)
              * the GHASH input; sum_q y_q * H^(q+1).  G >= 2: each lane multiplies by its own power from the key's shared
              * window tables (build_ghash_tables), then an XOR butterfly over the record's G lanes leaves the GHASH in each;
              * G = 1: the lane's sum times H (the nibble table of H) */
+            ks_phase(8);
             const int q = (N - 1 - na - r) & (G - 1); /* (nc - r) mod G */
             V4 s;
             if constexpr (G >= 2) {
@@ -1434,15 +1473,18 @@ __global__ void __launch_bounds__(WGT)
                     }
                 }
             }
+            ks_phase(9);
         }
         if (DEAL_MUTANT != 2)
             cbase += (uint32_t)ntasks;
     }
     if (KS_STAMPS && clk != nullptr) {
         ks_acc[0] = __builtin_amdgcn_s_memtime() - ks_t0;
-        uint64_t *o = clk + 4 * (size_t)gridDim.x + 5 * ((size_t)blockIdx.x * NW + (size_t)wave);
-        if (lane < 5)
-            o[lane] = lane == 0 ? ks_acc[0] : lane == 1 ? ks_acc[1] : lane == 2 ? ks_acc[2] : lane == 3 ? ks_acc[3] : ks_acc[4];
+        uint64_t *o = clk + 4 * (size_t)gridDim.x + 10 * ((size_t)blockIdx.x * NW + (size_t)wave);
+#pragma unroll
+        for (int k = 0; k < 10; ++k)
+            if (lane == k)
+                o[k] = ks_acc[k];
     }
     if (clk != nullptr) { /* the workgroup's end: after its last wave */
         __syncthreads();

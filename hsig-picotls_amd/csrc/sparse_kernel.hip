@@ -329,7 +329,7 @@ __device__ __forceinline__ void sparse_record(uint8_t *lds, int lane, uint32_t l
         }
 #pragma unroll
         for (int b = 0; b < NE; ++b) {
-            const V4 x = finish_elem<OPEN, ALIGNED, true>(e[b], inb[b], ks[b], aad_p, A, L, out_p, ek0);
+            const V4 x = finish_elem<OPEN, ALIGNED, true, !BYVAL>(e[b], inb[b], ks[b], aad_p, A, L, out_p, ek0);
             if (m + b == 0)
                 y = x; /* 0 * P ^ x */
             else if (e[b].active)
@@ -589,7 +589,7 @@ __device__ __forceinline__ void mw_record(uint8_t *lds, int wave, int lane, uint
         const V4 nohash[1] = {};
         V4 ydummy = V4{0, 0, 0, 0};
         ctr_ghash_skewed<ROUNDS, 1, false>(lds, lb_aes, rk, cc, cw, ks, ydummy, nohash, GhNibble{ctab});
-        const V4 x = finish_elem<OPEN, ALIGNED, true>(e, inb, ks[0], aad_p, A, L, out_p, ek0); /* 0 past the record */
+        const V4 x = finish_elem<OPEN, ALIGNED, true, false>(e, inb, ks[0], aad_p, A, L, out_p, ek0); /* 0 past the record */
         z = wave_xor(gf_win4_mul<16>(lds, w4, x));
         if (wave == 0) {
             if (lane == 0)
