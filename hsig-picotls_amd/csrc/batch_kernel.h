@@ -829,33 +829,40 @@ __device__ __forceinline__ void store_bytes(uint8_t *p, int n, V4 v)
 
 __device__ __forceinline__ V4 mask_block(V4 v, int n);
 
-/* n (0..15) bytes at a 16-byte aligned p: the whole dwords as dword loads, the last 1..3 bytes as a 16-bit and / or an
- * 8-bit load, all independent (one memory latency; a byte loop carrying the word waited once per byte).  Nothing past
+/* A (possibly partial) block of n bytes: a whole block as one 16-byte load; a partial one at a 16-byte aligned p as its
+ * whole dwords, then a 16-bit and / or an 8-bit load for the last 1..3 bytes; unaligned, byte by byte.  Nothing past
  * p + n is read (fusion over-reads within the page, lib/fusion.c:345-388; a caller's allocation may end at the record's
- * last byte, SURVEY.md §5, tests/test_gpu_guard.py) */
-__device__ __forceinline__ V4 load_partial_aligned(const uint8_t *p, int n)
-{
-    const uint32_t *q = reinterpret_cast<const uint32_t *>(p);
-    uint32_t w[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const int k = n - 4 * i;
-        const uint32_t lo = k >= 4 ? q[i] : k >= 2 ? (uint32_t)*reinterpret_cast<const uint16_t *>(p + 4 * i)
-                                          : k == 1 ? (uint32_t)p[4 * i] : 0u;
-        const uint32_t hi = k == 3 ? (uint32_t)p[4 * i + 2] << 16 : 0u;
-        w[i] = lo | hi;
-    }
-    return V4{w[0], w[1], w[2], w[3]};
-}
-
-/* a (possibly partial) block of n bytes: whole blocks as one 16-byte load; partial ones exactly n bytes
- * (ALIGNED: whole dwords + bytes, otherwise byte by byte) */
+ * last byte, SURVEY.md §5, tests/test_gpu_guard.py).  Every load writes a register of its own inside its (divergent)
+ * branch and the pieces are combined after all of them are issued: combining inside a branch made the compiler wait for
+ * each load there, up to 4 memory latencies per partial block (one per dword) before the element's AES could start. */
 template <bool ALIGNED>
 __device__ __forceinline__ V4 load_block(const uint8_t *p, int n)
 {
+    if (!ALIGNED) {
+        if (n == 16)
+            return load_full(p);
+        return load_bytes(p, n);
+    }
+    V4 f = V4{0, 0, 0, 0};
     if (n == 16)
-        return load_full(p);
-    return ALIGNED ? load_partial_aligned(p, n) : load_bytes(p, n);
+        f = load_full(p);
+    const uint32_t *q = reinterpret_cast<const uint32_t *>(p);
+    uint32_t d[4] = {0, 0, 0, 0}, h[4] = {0, 0, 0, 0}, b[4] = {0, 0, 0, 0};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int k = n - 4 * i;
+        if (n < 16 && k >= 4)
+            d[i] = q[i];
+        if (k == 2 || k == 3)
+            h[i] = *reinterpret_cast<const uint16_t *>(p + 4 * i);
+        if (k == 1 || k == 3)
+            b[i] = p[4 * i + k - 1];
+    }
+    uint32_t w[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+        w[i] = d[i] | h[i] | (b[i] << ((n - 4 * i) == 3 ? 16 : 0));
+    return V4{f.w0 | w[0], f.w1 | w[1], f.w2 | w[2], f.w3 | w[3]};
 }
 
 /* n (0..15) bytes of v to a 16-byte aligned p: whole dwords, then a 16-bit and / or an 8-bit store (nothing past p + n) */
@@ -909,6 +916,61 @@ __device__ __forceinline__ V4 put_byte(V4 v, int pos, uint32_t b)
     const uint32_t x = b << (8 * (pos & 3));
     const int w = pos >> 2;
     return V4{v.w0 | (w == 0 ? x : 0u), v.w1 | (w == 1 ? x : 0u), v.w2 | (w == 2 ? x : 0u), v.w3 | (w == 3 ? x : 0u)};
+}
+
+/* n (0..16) bytes at a 16-byte aligned p with no branch: 4 dword loads, a 16-bit and an 8-bit load, each from its place
+ * in the block when it holds record bytes and from `safe` (any readable, 4-byte aligned address, e.g. the AES table's
+ * global copy) when not, the unwanted results masked off.  Nothing outside [p, p + n) is read of the caller's buffers;
+ * since no branch holds a load's result, the loads go out together and the wave waits once (the branchy form waited up
+ * to 4 times per block: the batch kernel's AAD element at every task start). */
+__device__ __forceinline__ V4 load_block_nb(const uint8_t *p, int n, const uint8_t *safe)
+{
+    const int nd = n >> 2, t = n & 3;
+    uint32_t d[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+        d[i] = *reinterpret_cast<const uint32_t *>(i < nd ? p + 4 * i : safe);
+    const uint32_t h = *reinterpret_cast<const uint16_t *>(t >= 2 ? p + 4 * nd : safe);
+    const uint32_t b = *(t & 1 ? p + n - 1 : safe);
+    const uint32_t tail = (t >= 2 ? h : 0u) | (t & 1 ? b << (t == 3 ? 16 : 0) : 0u);
+    uint32_t w[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+        w[i] = i < nd ? d[i] : i == nd ? tail : 0u;
+    return V4{w[0], w[1], w[2], w[3]};
+}
+
+/* byte k of the result = byte k + s of v (s in 0..15), zeros above byte 15 - s */
+__device__ __forceinline__ V4 shr_bytes(V4 v, int s)
+{
+    const uint64_t lo = (uint64_t)v.w1 << 32 | v.w0, hi = (uint64_t)v.w3 << 32 | v.w2;
+    const uint32_t sh = 8u * (uint32_t)s;
+    const uint64_t a = sh < 64 ? lo : hi, b = sh < 64 ? hi : 0;
+    const uint32_t r = sh & 63u;
+    const uint64_t rlo = r ? (a >> r) | (b << (64u - r)) : a, rhi = r ? b >> r : b;
+    return V4{(uint32_t)rlo, (uint32_t)(rlo >> 32), (uint32_t)rhi, (uint32_t)(rhi >> 32)};
+}
+
+/* Data block c of a record, its first nb (0..16) bytes, for the generic elements: issued as ONE 16-byte load of the 16
+ * bytes that END at the block's last byte (inside the record whenever 16 c + nb >= 16), brought down by tail_shift()
+ * after the AES; only the first block of a record shorter than 16 bytes is read piecewise.  No branch uses the loaded
+ * value, so the loads of an element pair are all in flight during its AES (loading the partial block piecewise inside
+ * divergent branches made the compiler wait there: 3.7 % of c3's wave cycles before the AES could start). */
+__device__ __forceinline__ V4 tail_load(const uint8_t *blk, int c, int nb, int &shift)
+{
+    shift = 0;
+    if (nb <= 0)
+        return V4{0, 0, 0, 0};
+    if (16 * c + nb >= 16) {
+        shift = 16 - nb;
+        return load_full(blk + nb - 16);
+    }
+    return load_bytes(blk, nb); /* the first block of a record of fewer than 16 bytes */
+}
+
+__device__ __forceinline__ V4 tail_shift(V4 raw, int shift)
+{
+    return shift ? shr_bytes(raw, shift) : raw;
 }
 
 /* Diagnostic clock stamps (ptls_hip_batch_set_clock; nothing runs unless a buffer is given): thread 0 of a workgroup
@@ -1132,7 +1194,7 @@ __global__ void __launch_bounds__(WGT)
 
     clock_stamp(clk, 0);
     build_aes_tables<WGT>(lds, LDS_AES, t0);
-    uint64_t ks_acc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0}; /* KS_STAMPS: see its definition */
+    uint64_t ks_acc[16] = {}; /* KS_STAMPS: see its definition */
     const uint64_t ks_t0 = KS_STAMPS ? __builtin_amdgcn_s_memtime() : 0;
     uint64_t ks_last = ks_t0;
     auto ks_phase = [&](int k) __attribute__((always_inline)) { /* the cycles since the previous mark go to phase k */
@@ -1233,45 +1295,60 @@ __global__ void __launch_bounds__(WGT)
                 V4 in[2], ks[2];
                 uint32_t cw[2];
                 int big = 0;
+                int sft[2];
 #pragma unroll
                 for (int b = 0; b < 2; ++b) {
                     e[b] = elem_of(i0 + (m + b) * G, N, na, nc, L, N);
                     in[b] = V4{0, 0, 0, 0};
+                    sft[b] = 0;
                     if (e[b].is_c) {
                         const bool tb = tflag && e[b].c == nc - 1; /* the block holding the content-type byte */
-                        in[b] = load_block<ALIGNED>(in_p + 16 * (size_t)e[b].c, e[b].nbytes - (tb ? 1 : 0));
-                        if (tb)
-                            in[b] = put_byte(in[b], e[b].nbytes - 1, ttype);
+                        in[b] = tail_load(in_p + 16 * (size_t)e[b].c, e[b].c, e[b].nbytes - (tb ? 1 : 0), sft[b]);
                     }
                     /* keystream for data block c (counter inc32(J0) + c), E_K(J0) for the length-block lane */
                     cw[b] = e[b].is_c ? bswap32((uint32_t)e[b].c + 2u) : 0x01000000u;
                     ks[b] = V4{n0, n1, n2, cw[b]};
                     big |= (e[b].is_c && e[b].c >= 65534) ? 1 : 0;
                 }
-                if (wave_max(big) != 0) { /* wave-wide, before any lane branches off */
+                const int bigw = wave_max(big);
+                ks_phase(10);
+                if (bigw != 0) { /* wave-wide, before any lane branches off */
                     aes_encrypt_n<ROUNDS, 2>(lds, lb_aes, rk, ks);
                 } else {
                     const V4 nohash[2] = {V4{0, 0, 0, 0}, V4{0, 0, 0, 0}};
                     V4 ydummy = V4{0, 0, 0, 0};
                     ctr_ghash<ROUNDS, 2, false>(lds, lb_aes, rk, cc, cw, ks, ydummy, nohash, gl);
                 }
+                if (KS_STAMPS)
+                    __builtin_amdgcn_s_waitcnt(0xc07f); /* lgkmcnt(0): the AES lookups are back */
+                ks_phase(11);
+                V4 xs[2];
 #pragma unroll
                 for (int b = 0; b < 2; ++b) {
-                    const V4 x = finish_elem<OPEN, ALIGNED>(e[b], in[b], ks[b], aad_p, A, L, out_p, ek0);
-                    if (e[b].active)
-                        y = gh_mul_main(lds, gl, y, x);
+                    in[b] = tail_shift(in[b], sft[b]);
+                    if (tflag && e[b].is_c && e[b].c == nc - 1)
+                        in[b] = put_byte(in[b], e[b].nbytes - 1, ttype);
+                    xs[b] = finish_elem<OPEN, ALIGNED>(e[b], in[b], ks[b], aad_p, A, L, out_p, ek0);
                 }
+                if (KS_STAMPS)
+                    __builtin_amdgcn_s_waitcnt(0); /* the loads finish_elem used are back */
+                ks_phase(12);
+#pragma unroll
+                for (int b = 0; b < 2; ++b)
+                    if (e[b].active)
+                        y = gh_mul_main(lds, gl, y, xs[b]);
+                if (KS_STAMPS)
+                    __builtin_amdgcn_s_waitcnt(0);
+                ks_phase(13);
             };
 
             auto generic_iter_m = [&](int m) {
                 const Elem e0 = elem_of(i0 + m * G, N, na, nc, L, N);
                 V4 in0 = V4{0, 0, 0, 0};
-                if (e0.is_c) {
-                    const bool tb = tflag && e0.c == nc - 1; /* the block holding the content-type byte */
-                    in0 = load_block<ALIGNED>(in_p + 16 * (size_t)e0.c, e0.nbytes - (tb ? 1 : 0));
-                    if (tb)
-                        in0 = put_byte(in0, e0.nbytes - 1, ttype);
-                }
+                int sft0 = 0;
+                const bool tb0 = tflag && e0.is_c && e0.c == nc - 1; /* the block holding the content-type byte */
+                if (e0.is_c)
+                    in0 = tail_load(in_p + 16 * (size_t)e0.c, e0.c, e0.nbytes - (tb0 ? 1 : 0), sft0);
                 /* keystream for data block c (counter inc32(J0) + c), E_K(J0) for the length-block lane */
                 const uint32_t cw0[1] = {e0.is_c ? bswap32((uint32_t)e0.c + 2u) : 0x01000000u};
                 V4 ks0[1] = {V4{n0, n1, n2, cw0[0]}};
@@ -1282,6 +1359,9 @@ __global__ void __launch_bounds__(WGT)
                 } else {
                     aes_encrypt_n<ROUNDS, 1>(lds, lb_aes, rk, ks0);
                 }
+                in0 = tail_shift(in0, sft0);
+                if (tb0)
+                    in0 = put_byte(in0, e0.nbytes - 1, ttype);
                 const V4 x0 = finish_elem<OPEN, ALIGNED>(e0, in0, ks0[0], aad_p, A, L, out_p, ek0);
                 if (e0.active)
                     y = gh_mul_main(lds, gl, y, x0);
@@ -1306,8 +1386,9 @@ __global__ void __launch_bounds__(WGT)
             const int naad = wave_max(pm0);
             for (int j = 0; j < naad; ++j) {
                 if (j < pm0) {
-                    const Elem e = elem_of(i0 + j * G, N, na, nc, L, N);
-                    const V4 x = load_block<ALIGNED>(aad_p + 16 * e.i, min(16, A - 16 * e.i));
+                    const int ia = i0 + j * G;
+                    const V4 x = ALIGNED ? load_block_nb(aad_p + 16 * ia, min(16, A - 16 * ia), reinterpret_cast<const uint8_t *>(t0))
+                                         : load_block<false>(aad_p + 16 * ia, min(16, A - 16 * ia));
                     y = j == 0 ? x : gh_mul_main(lds, gl, y, x);
                 }
             }
@@ -1480,9 +1561,9 @@ __global__ void __launch_bounds__(WGT)
     }
     if (KS_STAMPS && clk != nullptr) {
         ks_acc[0] = __builtin_amdgcn_s_memtime() - ks_t0;
-        uint64_t *o = clk + 4 * (size_t)gridDim.x + 10 * ((size_t)blockIdx.x * NW + (size_t)wave);
+        uint64_t *o = clk + 4 * (size_t)gridDim.x + 16 * ((size_t)blockIdx.x * NW + (size_t)wave);
 #pragma unroll
-        for (int k = 0; k < 10; ++k)
+        for (int k = 0; k < 16; ++k)
             if (lane == k)
                 o[k] = ks_acc[k];
     }

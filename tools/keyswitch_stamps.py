@@ -43,18 +43,20 @@ d_ct = torch.zeros(out_total + 64, dtype=torch.uint8, device="cuda")
 d_aad = torch.zeros(len(recs) * 16, dtype=torch.uint8, device="cuda")
 NW = b.workgroup // 64
 grid = b.grid
-clk = torch.zeros(4 * grid + 10 * grid * NW, dtype=torch.int64, device="cuda")
+clk = torch.zeros(4 * grid + 16 * grid * NW, dtype=torch.int64, device="cuda")
 for rep in range(3):
     b.set_clock(clk if rep == 2 else None)
     b.seal(ks, d_pt, d_aad, d_ct)
     torch.cuda.synchronize()
-a = clk.cpu().numpy().view(np.uint64)[4 * grid:].reshape(grid, NW, 10).astype(np.float64)
+a = clk.cpu().numpy().view(np.uint64)[4 * grid:].reshape(grid, NW, 16).astype(np.float64)
 tot = a[:, :, 0].sum()
 b1, build, b2, nsw = (a[:, :, k].sum() for k in (1, 2, 3, 4))
 print(f"{args.config} lanes={b.lanes} grid={grid} waves={grid * NW}: switches per wave {nsw / (grid * NW):.1f}; "
       f"share of wave cycles: barrier-1 wait {b1 / tot:.4f}, table build {build / tot:.4f}, barrier-2 wait {b2 / tot:.4f}, "
       f"tasks + dealing {(tot - b1 - build - b2) / tot:.4f}; cycles per switch per wave: barrier-1 {b1 / max(nsw, 1):.0f}, "
       f"build {build / max(nsw, 1):.0f}, barrier-2 {b2 / max(nsw, 1):.0f}")
-ph = {name: a[:, :, k].sum() / tot for k, name in ((5, "draw"), (6, "setup"), (7, "stretch"), (8, "rest"), (9, "combine+tag"))}
+ph = {name: a[:, :, k].sum() / tot for k, name in ((5, "draw"), (6, "setup"), (7, "stretch"), (8, "rest"), (9, "combine+tag"),
+                                                   (10, "  rest: loads issued + wave max"), (11, "  rest: AES"),
+                                                   (12, "  rest: finish (loads back, stores)"), (13, "  rest: GHASH"))}
 print("task phases, share of wave cycles: " + ", ".join(f"{k} {v:.4f}" for k, v in ph.items()) +
       f"")
