@@ -252,7 +252,10 @@ __device__ __forceinline__ void sparse_record(uint8_t *lds, int lane, uint32_t l
     /* batch records: the lane's first AAD block is loaded here, before the counter-mode constants and the H^64 table, so
      * its latency runs under that work (c4s seal 498-504 -> 513-519 GiB/s, profiles/r04_c4s_prefetch_ab.log) */
     V4 aad_pf = V4{0, 0, 0, 0};
-    if (!BYVAL && vl < na)
+    if (!BYVAL && ALIGNED)
+        aad_pf = load_block_nb(vl < na ? aad_p + 16 * vl : reinterpret_cast<const uint8_t *>(slot->rk), vl < na ? min(16, A - 16 * vl) : 0,
+                               reinterpret_cast<const uint8_t *>(slot->rk));
+    else if (!BYVAL && vl < na)
         aad_pf = load_block<ALIGNED>(aad_p + 16 * vl, min(16, A - 16 * vl));
     (void)aad_pf;
     /* a single record builds its lane-combination table (the 16 multiples of H^(q+1)) early, in an LDS area of its own
@@ -297,20 +300,27 @@ __device__ __forceinline__ void sparse_record(uint8_t *lds, int lane, uint32_t l
         Elem e[NE];
         V4 inb[NE], ks[NE];
         uint32_t cw[NE];
+        int sft[NE];
         int big = 0;
 #pragma unroll
         for (int b = 0; b < NE; ++b) {
             e[b] = elem_of(m + b < mend ? vl + (m + b) * S : N, N, na, nc, L, N);
             inb[b] = V4{0, 0, 0, 0};
+            sft[b] = 0;
             /* the lane's first two elements of a single record were read at the start (pre) */
             const bool have_pre = USE_PRE && prefetch && m + b < 2;
             const V4 pv = m + b == 0 ? pre[0] : pre[1];
             if (e[b].is_c) {
                 const bool tb = tflag && e[b].c == nc - 1; /* the block holding the content-type byte */
                 const int nb = e[b].nbytes - (tb ? 1 : 0);
-                inb[b] = have_pre ? mask_block(pv, nb) : load_block<ALIGNED>(in_p + 16 * (size_t)e[b].c, nb);
-                if (tb)
-                    inb[b] = put_byte(inb[b], e[b].nbytes - 1, ttype);
+                /* batch records: one 16-byte load ending at the block's last byte, shifted down after the AES (batch_kernel.h
+                 * tail_load: no load result is combined inside a branch, so the wave does not wait before its AES) */
+                if (have_pre)
+                    inb[b] = mask_block(pv, nb);
+                else if (!BYVAL)
+                    inb[b] = tail_load(in_p + 16 * (size_t)e[b].c, e[b].c, nb, sft[b]);
+                else
+                    inb[b] = load_block<ALIGNED>(in_p + 16 * (size_t)e[b].c, nb);
             } else if (e[b].is_aad) { /* loaded before the AES as well, not after it in finish_elem */
                 const int nb = min(16, A - 16 * e[b].i);
                 inb[b] = have_pre ? mask_block(pv, nb) : load_block<ALIGNED>(aad_p + 16 * e[b].i, nb);
@@ -329,6 +339,11 @@ __device__ __forceinline__ void sparse_record(uint8_t *lds, int lane, uint32_t l
         }
 #pragma unroll
         for (int b = 0; b < NE; ++b) {
+            if (e[b].is_c) {
+                inb[b] = tail_shift(inb[b], sft[b]);
+                if (tflag && e[b].c == nc - 1)
+                    inb[b] = put_byte(inb[b], e[b].nbytes - 1, ttype);
+            }
             const V4 x = finish_elem<OPEN, ALIGNED, true, !BYVAL>(e[b], inb[b], ks[b], aad_p, A, L, out_p, ek0);
             if (m + b == 0)
                 y = x; /* 0 * P ^ x */
