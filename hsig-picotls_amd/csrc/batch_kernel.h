@@ -803,8 +803,9 @@ __device__ __forceinline__ V4 shl8_in(V4 v, uint8_t b)
               __builtin_amdgcn_alignbit(v.w3, v.w2, 24)};
 }
 
-/* exact byte-granular access (n in 0..16), used for unaligned layouts: the n byte loads are independent and all issued
- * before the first use (one memory latency, where a loop carrying the block through its shifts waited n times) */
+/* exact byte-granular access (n in 0..16), used for unaligned layouts and the first block of a record shorter than 16
+ * bytes: n independent byte loads (each still behind a per-lane condition, so the compiler may wait between some of
+ * them; the loop that carried the block through its shifts waited after every byte) */
 __device__ __forceinline__ V4 load_bytes(const uint8_t *p, int n)
 {
     uint32_t b[16];
@@ -832,9 +833,9 @@ __device__ __forceinline__ V4 mask_block(V4 v, int n);
 /* A (possibly partial) block of n bytes: a whole block as one 16-byte load; a partial one at a 16-byte aligned p as its
  * whole dwords, then a 16-bit and / or an 8-bit load for the last 1..3 bytes; unaligned, byte by byte.  Nothing past
  * p + n is read (fusion over-reads within the page, lib/fusion.c:345-388; a caller's allocation may end at the record's
- * last byte, SURVEY.md §5, tests/test_gpu_guard.py).  Every load writes a register of its own inside its (divergent)
- * branch and the pieces are combined after all of them are issued: combining inside a branch made the compiler wait for
- * each load there, up to 4 memory latencies per partial block (one per dword) before the element's AES could start. */
+ * last byte, SURVEY.md §5, tests/test_gpu_guard.py).  Each piece goes to a register of its own and they are combined
+ * at the end (the form that combined each dword inside its branch waited there up to 4 times per block); the loads still
+ * sit behind per-lane conditions, so the hot paths use tail_load / load_block_nb below, which have none. */
 template <bool ALIGNED>
 __device__ __forceinline__ V4 load_block(const uint8_t *p, int n)
 {
