@@ -11,7 +11,7 @@ import sys
 import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB = os.path.join(ROOT, "hsig-picotls_amd", "diag", "libptls_hip_stamps.so")
+LIB = sys.argv[1] if len(sys.argv) > 1 else os.path.join(ROOT, "hsig-picotls_amd", "diag", "libptls_hip_stamps.so")
 os.environ["PTLS_HIP_LIB"] = LIB
 for p in (ROOT, os.path.join(ROOT, "hsig-picotls_amd")):
     sys.path.insert(0, p)
