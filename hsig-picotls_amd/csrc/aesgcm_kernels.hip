@@ -373,6 +373,20 @@ __global__ void __launch_bounds__(256) copy16_kernel(const uint4 *__restrict__ s
         dst[i] = src[i];
 }
 
+/* The copy transport's gap fill (pipeline.cpp pipeline_run_copy): a slice's output span comes back from the device as a
+ * few large copies, so the bytes lying between its records in that span must hold the caller's own bytes first.  The host
+ * gathers them into one packed buffer; workgroup g (grid-stride) copies piece g into the device staging of the output.
+ * Pieces are short (a few to a few thousand bytes): bytes, one per thread. */
+__global__ void __launch_bounds__(256) gap_scatter_kernel(const GapPiece *__restrict__ pieces, uint32_t n, const uint8_t *__restrict__ src,
+                                                          uint8_t *__restrict__ dst)
+{
+    for (uint32_t g = blockIdx.x; g < n; g += gridDim.x) {
+        const GapPiece p = pieces[g];
+        for (uint32_t b = threadIdx.x; b < p.len; b += 256)
+            dst[p.dst + b] = src[p.src + b];
+    }
+}
+
 } // namespace ptls_hip
 
 /* ======================================================================================= *
@@ -432,6 +446,15 @@ int launch_copy16(void *dst, const void *src, size_t n16, void *stream)
     const unsigned grid = (unsigned)((n16 + 255) / 256);
     hipLaunchKernelGGL(copy16_kernel, dim3(grid), dim3(256), 0, static_cast<hipStream_t>(stream), static_cast<const uint4 *>(src),
                        static_cast<uint4 *>(dst), n16);
+    return (int)hipGetLastError();
+}
+
+int launch_gap_scatter(const GapPiece *pieces, uint32_t n, const uint8_t *src, uint8_t *dst, void *stream)
+{
+    if (n == 0)
+        return 0;
+    const unsigned grid = n < 1024 ? n : 1024;
+    hipLaunchKernelGGL(gap_scatter_kernel, dim3(grid), dim3(256), 0, static_cast<hipStream_t>(stream), pieces, n, src, dst);
     return (int)hipGetLastError();
 }
 

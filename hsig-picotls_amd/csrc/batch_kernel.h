@@ -1577,6 +1577,9 @@ __global__ void __launch_bounds__(WGT)
 template <int G, int R, bool O, int W>
 static hipError_t launch_one(unsigned grid, hipStream_t s, const KernelArgs &a, bool aligned)
 {
+    /* KS_STAMPS builds write 16 words per wave after the 4 per workgroup: refuse a smaller stamp buffer */
+    if (KS_STAMPS && a.clk != nullptr && a.clk_bytes < 8 * (4 * (size_t)grid + 16 * (size_t)grid * (W / 64)))
+        return hipErrorInvalidValue;
     if (aligned)
         hipLaunchKernelGGL((aesgcm_batch_kernel<G, R, O, true, W>), dim3(grid), dim3(W), 0, s, a.recs_ord, a.order, a.chunks,
                            a.nchunks, a.in, a.aad, a.out, a.result, a.slots, a.basis, a.t0, a.supp, a.hp_slots, a.hp_nslots, a.mask, a.clk,

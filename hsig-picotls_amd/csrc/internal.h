@@ -48,7 +48,7 @@ struct KeySlot {
 };
 static_assert(sizeof(KeySlot) == 512, "KeySlot must stay 512 bytes");
 
-/* the second compiled workgroup size (the first is 512); tuning builds override it (tools/build_variant.sh) */
+/* the second compiled workgroup size (the first is 512) */
 constexpr int WG_ALT = 768;
 
 struct Chunk {
@@ -87,6 +87,7 @@ struct KernelArgs {
     uint32_t done_seq;
     /* optional diagnostic clock stamps, 4 x uint64 per workgroup (ptls_hip_batch_set_clock); nullptr = none */
     uint64_t *clk;
+    size_t clk_bytes; /* its size (KS_STAMPS diagnostic builds also write 16 words per wave after the workgroups' stamps) */
     /* batch kernel: this launch's chunk-queue words {next chunk - grid, workgroups done}, zero at launch and left zero by
      * the kernel (engine.cpp queue_slot); nullptr = the static grid stride */
     uint32_t *queue;
@@ -144,6 +145,14 @@ static_assert(sizeof(WorkerSlot) == 448 + 2 * WORKER_DATA + 256, "WorkerSlot: se
 constexpr uint32_t WAUX_RESULT = 0, WAUX_SUPP = 32, WAUX_MASK = 64, WAUX_DONE = 128;
 static_assert(__builtin_offsetof(WorkerSlot, quit) == 4, "the worker polls {seq, quit} as one 8-byte word");
 
+/* one run of bytes the copy transport puts back between records (pipeline.cpp): dst = offset in the slice's output
+ * staging, src = offset in the packed gap buffer */
+struct GapPiece {
+    uint64_t dst;
+    uint32_t src;
+    uint32_t len;
+};
+
 /* host-side launchers, defined next to the kernels (aesgcm_kernels.hip, batch_g*.hip) */
 int launch_plugin_worker(WorkerSlot *mb, unsigned nmb, uint32_t epoch, const uint32_t *t0, uint64_t idle_ticks, uint64_t life_ticks,
                          uint64_t *activity, void *stream);
@@ -169,6 +178,7 @@ int launch_derive_traffic_keys(const uint8_t *secrets_in, uint8_t *secrets_out, 
 int launch_fill(const ptls_hip_record_t *recs, uint32_t n, uint8_t *buf, uint64_t seed, uint64_t index_base,
                 const uint64_t *index, unsigned grid, void *stream);
 int launch_copy16(void *dst, const void *src, size_t n16, void *stream);
+int launch_gap_scatter(const GapPiece *pieces, uint32_t n, const uint8_t *src, uint8_t *dst, void *stream);
 
 } // namespace ptls_hip
 

@@ -244,7 +244,7 @@ def test_product_sources_carry_no_experiment_switches():
     (DEAL_MUTANT), the diagnostic stamp builds (KS_STAMPS, STAMP_PHASES, WORKER_STAMPS) and the product guard; the
     rejected variants are measured in EXPERIMENTS.md, not kept in the code"""
     import re
-    allowed = {"PTLS_HIP_BATCH_KERNEL_H", "PTLS_HIP_INTERNAL_H", "PTLS_HIP_GF128_H", "PTLS_HIP_H", "PTLS_HIP_PRODUCT", "DEAL_MUTANT",
+    allowed = {"PTLS_HIP_BATCH_KERNEL_H", "PTLS_HIP_INTERNAL_H", "PTLS_HIP_HOST_H", "PTLS_HIP_PLUGIN_H", "PTLS_HIP_GF128_H", "PTLS_HIP_H", "PTLS_HIP_PRODUCT", "DEAL_MUTANT",
                "KS_STAMPS", "STAMP_PHASES", "WORKER_STAMPS", "__x86_64__", "__i386__", "GF128_FN"}
     csrc = os.path.join(ROOT, "hsig-picotls_amd", "csrc")
     seen = set()

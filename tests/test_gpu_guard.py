@@ -1,9 +1,9 @@
 """The engine reads and writes exactly each record's bytes: proved at an allocation edge.
 
 fusion over-reads partial blocks inside the page by design (lib/fusion.c:51-60, :345-388) and pins that with
-t/fusion.c test_loadn128 (:52-67, every offset of an 8 KiB buffer).  This engine claims more (batch_kernel.h
-load_partial_aligned / load_bytes, SURVEY.md §5: a caller's allocation may end at the record's last byte), so the test
-puts the last byte of every buffer the kernels touch directly in front of an UNMAPPED page:
+t/fusion.c test_loadn128 (:52-67, every offset of an 8 KiB buffer).  This engine claims more (batch_kernel.h tail_load /
+load_block_nb / load_bytes, SURVEY.md §5: a caller's allocation may end at the record's last byte), so the test puts
+the last byte of every buffer the kernels touch directly in front of an UNMAPPED page:
 
 * each buffer (plaintext / ciphertext in, AAD, output) is its own anonymous mmap of whole pages plus one trailing page
   set to PROT_NONE; only the data pages are registered with the GPU (ptls_hip_host_register), so a device access past
@@ -12,9 +12,12 @@ puts the last byte of every buffer the kernels touch directly in front of an UNM
   byte of the last registered page, with that record's length L mod 16 in {0, 1, 15};
 * the kernels read and write those buffers themselves over PCIe (host pipeline, PTLS_HIP_TRANSPORT_MAPPED): short and
   mid-size records (0-200, 300-800 B) go to the batch kernel at 1-2 and 16-32 lanes per record, records of >= 64 GHASH
-  elements (1 100-3 000 B) to the wave-per-record kernel (engine.cpp mapped_lanes), packed at 1 byte (the
+  elements (1 100-3 000 B) to the wave-per-record kernel (pipeline.cpp mapped_lanes), packed at 1 byte (the
   byte-granular path) or 16 bytes (the aligned path: the last record is then a whole number of blocks, the only way an
   aligned record can end on a page boundary);
+* the same buffers through the device-resident batch API at 4 and 8 lanes per record (the planner's choice for
+  device-resident c2 / c3 shapes, which the mapped transport never makes), including the deferred-store seal path of
+  records packed off the 128-byte line (batch_kernel.h, round 5);
 * seal and open are compared with the CPU oracle; a tampered tag must fail.
 """
 import ctypes
@@ -22,7 +25,7 @@ import mmap
 
 import numpy as np
 import pytest
-import torch  # noqa: F401  (the HIP runtime is torch's, loaded before libptls_hip.so: tests/conftest.py)
+import torch  # (the HIP runtime is torch's, loaded before libptls_hip.so: tests/conftest.py)
 
 import ptls_hip
 
@@ -36,6 +39,15 @@ _libc.mmap.restype = ctypes.c_void_p
 _libc.mmap.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_long]
 _libc.mprotect.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
 _libc.munmap.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
+_hip = ctypes.CDLL("libamdhip64.so")
+_hip.hipHostGetDevicePointer.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_void_p, ctypes.c_uint]
+
+
+def _device_ptr(host_addr):
+    """the device address of registered host memory (what the mapped transport hands the kernels)"""
+    d = ctypes.c_void_p()
+    assert _hip.hipHostGetDevicePointer(ctypes.byref(d), ctypes.c_void_p(host_addr), 0) == 0
+    return d.value
 
 
 class GuardedBuffer:
@@ -159,3 +171,56 @@ def test_no_access_past_the_last_record(engine, oracle, kind, last_mod, key_len,
         ks.close()
         for b in bufs:
             b.close()
+
+
+@pytest.mark.parametrize("last_mod,align", [(0, 1), (15, 1), (0, 16)])
+@pytest.mark.parametrize("kind", ["mid", "long"])
+@pytest.mark.parametrize("lanes", [4, 8])
+def test_no_access_past_the_last_record_batch_lanes(engine, oracle, lanes, kind, last_mod, align):
+    """the guarded buffers through ptls_hip_aesgcm_seal_batch / open_batch at a forced 4 or 8 lanes per record (ADVICE
+    r05): the kernels address the registered pages by their device mapping, the last record ends on the last byte"""
+    recs = _records(oracle, kind, last_mod, 16, align)
+    lens = [len(r[4]) for r in recs]
+    ks = ptls_hip.KeySet(engine, 16, 3)
+    keys = [oracle.gen_key(900 + k, 16) for k in range(3)]
+    ks.set(0, b"".join(k for k, _ in keys), b"".join(v for _, v in keys))
+    bufs = []
+    try:
+        d, in_total, out_total, aad_total = _descs(recs, lens, [L + 16 for L in lens], align)
+        g_in, g_aad, g_out = GuardedBuffer(in_total), GuardedBuffer(aad_total), GuardedBuffer(out_total)
+        bufs += [g_in, g_aad, g_out]
+        vin, vaad, vout = g_in.view(), g_aad.view(), g_out.view()
+        for r, e in zip(recs, d):
+            vin[e["in_off"]: e["in_off"] + e["len"]] = np.frombuffer(r[4], np.uint8)
+            vaad[e["aad_off"]: e["aad_off"] + e["aad_len"]] = np.frombuffer(r[3], np.uint8)
+        b = ptls_hip.Batch(engine, d)
+        b.set_lanes(lanes)
+        assert b.lanes == lanes
+        b.seal(ks, _device_ptr(g_in.base), _device_ptr(g_aad.base), _device_ptr(g_out.base))
+        torch.cuda.synchronize()
+        sealed = [vout[e["out_off"]: e["out_off"] + e["len"] + 16].tobytes() for e in d]
+        bad = [i for i, (r, s) in enumerate(zip(recs, sealed)) if s != oracle.seal(*r)]
+        assert not bad, f"seal mismatches at {bad[:8]}"
+        d2, in2, out2, _ = _descs(recs, [L + 16 for L in lens], lens, align)
+        d2["aad_off"] = d["aad_off"]
+        g_in2, g_out2 = GuardedBuffer(in2), GuardedBuffer(out2)
+        bufs += [g_in2, g_out2]
+        vin2, vout2 = g_in2.view(), g_out2.view()
+        for s_, e in zip(sealed, d2):
+            vin2[e["in_off"]: e["in_off"] + len(s_)] = np.frombuffer(s_, np.uint8)
+        tamper = len(recs) // 3
+        vin2[int(d2[tamper]["in_off"]) + lens[tamper] + 1] ^= 0x01
+        b2 = ptls_hip.Batch(engine, d2)
+        b2.set_lanes(lanes)
+        res = torch.zeros(len(recs), dtype=torch.int64, device="cuda")
+        b2.open(ks, _device_ptr(g_in2.base), _device_ptr(g_aad.base), _device_ptr(g_out2.base), res)
+        torch.cuda.synchronize()
+        want = [UINT64_MAX if i == tamper else L for i, L in enumerate(lens)]
+        assert [int(x) & UINT64_MAX for x in res.cpu().numpy()] == want
+        assert [vout2[e["out_off"]: e["out_off"] + e["len"]].tobytes() for e in d2] == [r[4] for r in recs]
+        b.close()
+        b2.close()
+    finally:
+        ks.close()
+        for g in bufs:
+            g.close()
