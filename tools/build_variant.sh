@@ -19,6 +19,11 @@ for src in $ALL; do
   fi
 done
 wait
-g++ -std=c++17 -O2 -fPIC -D__HIP_PLATFORM_AMD__ $EXTRA -I/opt/rocm/include -I../include -Icsrc -c csrc/engine.cpp -o variants/build_${name}/e.o
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $out $objs build/keyschedule.o variants/build_${name}/e.o -L/opt/rocm/lib -lamdhip64 -Wl,-rpath,/opt/rocm/lib
+# the host units (csrc/host.h lists them) with EXTRA as well: some switches are read by both sides
+for u in engine keyset planner batch tls13 pipeline node plugin_worker plugin; do
+  g++ -std=c++17 -O2 -fPIC -D__HIP_PLATFORM_AMD__ $EXTRA -I/opt/rocm/include -I../include -Icsrc -c csrc/$u.cpp -o variants/build_${name}/h_$u.o &
+  objs="$objs variants/build_${name}/h_$u.o"
+done
+wait
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $out $objs build/keyschedule.o -L/opt/rocm/lib -lamdhip64 -Wl,-rpath,/opt/rocm/lib
 echo "built $out"
