@@ -64,38 +64,59 @@ extern "C" int ptls_hip_tls13_seal_batch(ptls_hip_batch_t *b, ptls_hip_keyset_t 
     return run_batch(b, ks, in, out, out, nullptr, stream, false);
 }
 
-/* parse_record_header (lib/picotls.c:5020-5031) over a byte stream of TLS 1.3 application-data records */
+/* parse_record (lib/picotls.c:5033-5062) and parse_record_header (:5020-5031) over a byte stream of TLS 1.3 records,
+ * as far as the record layer of a connection past its handshake takes them (handle_input, :5840-5883):
+ *   - a first byte that is no record type (20-23) is a decode error (parse_record's check, :5040-5048);
+ *   - an application-data record longer than PTLS_MAX_ENCRYPTED_RECORD_SIZE is a decode error as soon as its header is
+ *     in (parse_record_header, before the fragment is complete);
+ *   - a complete application-data record shorter than a tag fails as picotls's aead_decrypt fails it: fusion's
+ *     aead_do_decrypt rejects inlen < 16 (lib/fusion.c:1151-1156) and aead_decrypt turns that into
+ *     PTLS_ALERT_BAD_RECORD_MAC (lib/picotls.c:717-726);
+ *   - an incomplete record (header or fragment) ends the parse without an error: the caller waits for more bytes;
+ *   - a record of another type (change_cipher_spec, alert, handshake) ends it too: picotls's record layer decides those;
+ *     so does an application-data record whose legacy_record_version is not 03 03 (TLS 1.3 senders always write 03 03,
+ *     RFC 8446 §5.1; picotls ignores the field and authenticates 03 03, the device would authenticate the bytes it reads).
+ * Every other application-data record becomes a descriptor; its tag is checked when the batch opens it. */
 extern "C" int ptls_hip_tls13_parse(const void *wire, size_t wire_len, uint64_t wire_off, uint32_t key, uint64_t seq,
                                     uint64_t out_base, ptls_hip_record_t *recs, size_t cap, size_t *nrecs, size_t *consumed)
 {
-    if ((wire == nullptr && wire_len != 0) || nrecs == nullptr || consumed == nullptr)
+    if ((wire == nullptr && wire_len != 0) || nrecs == nullptr || consumed == nullptr || (recs == nullptr && cap != 0))
         return fail(PTLS_HIP_EINVAL, "tls13_parse: bad arguments");
     const uint8_t *src = static_cast<const uint8_t *>(wire);
     size_t pos = 0, k = 0;
     uint64_t out = out_base;
     int rc = 0;
-    while (pos + 5 <= wire_len && k < cap) {
+    while (pos < wire_len && k < cap) {
         const uint8_t type = src[pos];
+        if (type < 20 || type > 23) {
+            rc = fail(PTLS_HIP_TLS13_DECODE_ERROR, "tls13_parse: byte %zu is not a record type (%u)", pos, type);
+            break;
+        }
+        if (type != 0x17 || wire_len - pos < 5)
+            break; /* not application data (left to the caller's record layer), or an incomplete header */
         const size_t length = (size_t)src[pos + 3] << 8 | src[pos + 4];
-        if (type != 0x17)
-            break; /* not application data: left to the caller's record layer */
-        if (length > PTLS_HIP_TLS13_MAX_ENCRYPTED || length < 16) {
+        if (length > PTLS_HIP_TLS13_MAX_ENCRYPTED) {
             rc = fail(PTLS_HIP_TLS13_DECODE_ERROR, "tls13_parse: record at %zu has length %zu", pos, length);
             break;
         }
-        if (pos + 5 + length > wire_len)
+        if (length > wire_len - pos - 5)
             break; /* incomplete */
-        if (recs != nullptr) {
-            ptls_hip_record_t &r = recs[k];
-            r.aad_off = wire_off + pos;
-            r.in_off = wire_off + pos + 5;
-            r.out_off = out;
-            r.seq = seq + k;
-            r.len = (uint32_t)(length - 16);
-            r.aad_len = 5;
-            r.key = key;
-            r.flags = 0;
+        if (length < 16) {
+            rc = fail(PTLS_HIP_TLS13_SHORT_RECORD, "tls13_parse: record at %zu is shorter than a tag (%zu bytes)", pos, length);
+            break;
         }
+        if (src[pos + 1] != 0x03 || src[pos + 2] != 0x03)
+            break; /* picotls authenticates 17 03 03 length (build_aad, :696-703), whatever legacy_record_version the record
+                      carries; the device reads the header as the AAD, so such a record is left to the caller as well */
+        ptls_hip_record_t &r = recs[k];
+        r.aad_off = wire_off + pos;
+        r.in_off = wire_off + pos + 5;
+        r.out_off = out;
+        r.seq = seq + k;
+        r.len = (uint32_t)(length - 16);
+        r.aad_len = 5;
+        r.key = key;
+        r.flags = 0;
         out += length - 16;
         pos += 5 + length;
         ++k;

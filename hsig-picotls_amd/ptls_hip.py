@@ -26,6 +26,7 @@ assert TLS13_MESSAGE_DTYPE.itemsize == 40
 TLS13_BAD_RECORD_MAC = (1 << 64) - 1
 TLS13_NO_CONTENT_TYPE = (1 << 64) - 2
 TLS13_DECODE_ERROR = -50
+TLS13_SHORT_RECORD = -20  # a complete application-data record shorter than a tag (PTLS_ALERT_BAD_RECORD_MAC)
 TRANSPORT_AUTO, TRANSPORT_COPY, TRANSPORT_MAPPED = 0, 1, 2
 
 
@@ -567,12 +568,15 @@ def tls13_frame(msgs):
     return recs
 
 
-def tls13_parse(wire, wire_off=0, key=0, seq=0, out_base=0, cap=1 << 20):
-    """(recs, consumed) for the complete application-data records at the start of `wire` (bytes)"""
-    recs = np.zeros(cap, dtype=RECORD_DTYPE)
+def tls13_parse(wire, wire_off=0, key=0, seq=0, out_base=0, cap=1 << 20, with_rc=False):
+    """(recs, consumed) for the complete application-data records at the start of `wire` (bytes); a non-zero return
+    raises HipError, or with_rc=True gives (rc, recs, consumed) (the records before the error are kept)"""
+    recs = np.zeros(max(cap, 1), dtype=RECORD_DTYPE)
     nrecs, consumed = ctypes.c_size_t(), ctypes.c_size_t()
     rc = lib().ptls_hip_tls13_parse(bytes(wire), len(wire), wire_off, key, seq, out_base, recs.ctypes.data, cap,
                                     ctypes.byref(nrecs), ctypes.byref(consumed))
+    if with_rc:
+        return rc, recs[: nrecs.value].copy(), consumed.value
     if rc != 0:
         raise HipError(f"tls13_parse: {last_error()} (rc={rc})")
     return recs[: nrecs.value].copy(), consumed.value

@@ -265,13 +265,19 @@ size_t ptls_hip_tls13_frame(const ptls_hip_tls13_message_t *msgs, size_t n, ptls
 /* Writes the record headers into `out`, then seals every record (AAD read from the headers). */
 int ptls_hip_tls13_seal_batch(ptls_hip_batch_t *batch, ptls_hip_keyset_t *ks, const void *in, void *out, void *stream);
 
-/* Receive side.  Parses complete TLS records from a received byte stream on the host, like
- * parse_record_header (lib/picotls.c:5020-5031): application-data records (type 23) of at most
+/* Receive side.  Parses complete TLS records from a received byte stream on the host, like picotls's
+ * parse_record / parse_record_header (lib/picotls.c:5020-5062): application-data records (type 23) of 16 to
  * 16384 + 256 bytes become descriptors {aad_off = header, in_off = header + 5, len = length - 16,
- * seq = seq + i, key, out_off = out_base + plaintext position}.  Stops before the first incomplete record
- * or non-application-data record; *consumed = wire bytes parsed, *nrecs = records produced.
- * Returns 0, or PTLS_HIP_TLS13_DECODE_ERROR for an oversized record or one shorter than a tag. */
+ * seq = seq + i, key, out_off = out_base + plaintext position}, at most `cap` of them (recs may be NULL
+ * when cap is 0).  Stops before the first incomplete record, record of another type (change_cipher_spec,
+ * alert, handshake) or record whose legacy_record_version is not 03 03: the caller's picotls record layer
+ * handles those (ptls_receive from *consumed on); *consumed = wire bytes of the records
+ * produced, *nrecs = their number.  Returns 0; or PTLS_HIP_TLS13_DECODE_ERROR for a byte that is no record
+ * type or an oversized application-data record (as parse_record); or PTLS_HIP_TLS13_SHORT_RECORD for a
+ * complete application-data record shorter than a tag (picotls's aead_decrypt fails it with
+ * PTLS_ALERT_BAD_RECORD_MAC, :717-726).  The records before the error are produced either way. */
 #define PTLS_HIP_TLS13_DECODE_ERROR (-50) /* -PTLS_ALERT_DECODE_ERROR */
+#define PTLS_HIP_TLS13_SHORT_RECORD (-20) /* -PTLS_ALERT_BAD_RECORD_MAC */
 int ptls_hip_tls13_parse(const void *wire, size_t wire_len, uint64_t wire_off, uint32_t key, uint64_t seq, uint64_t out_base,
                          ptls_hip_record_t *recs, size_t cap, size_t *nrecs, size_t *consumed);
 /* Opens the records (AAD = their wire headers in `in`), strips the TLSInnerPlaintext padding and reads
