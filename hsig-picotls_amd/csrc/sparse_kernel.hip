@@ -966,6 +966,8 @@ __global__ void __launch_bounds__(WORKER_WG)
                     }
                     if (seq == last && (quit != 0 || now - t_last > idle_ticks || now - t_start > life_ticks))
                         leave = true;
+                    /* no new read once a request is seen: the acquire below waits for every read still in flight, and
+                     * one issued now would add a whole PCIe round trip (round 6) */
                     ring[k] = poll_word(ms);
                     __builtin_amdgcn_s_sleep(2);
                 }
@@ -993,12 +995,13 @@ __global__ void __launch_bounds__(WORKER_WG)
         if (threadIdx.x == 0)
             __hip_atomic_store(&ms->seen, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         const WorkerReq &rq = ms->req;
-        /* an inline record's element 64 w + l for lane l of wave w, and wave 0's element l + 64, loaded with the request
-         * (unused otherwise) */
-        V4 pin[3]; /* elements 64 w + l, + 64, + 128 */
-#pragma unroll
-        for (int m = 0; m < 3; ++m)
-            pin[m] = load_full(ms->data + 16 * (size_t)(lane + 64 * wave + 64 * m));
+        /* an inline record's elements, loaded with the request (unused otherwise): wave 0 elements l, l + 64, l + 128
+         * (a two-wave record: l; a long one: l, l + 128), wave 1 elements l, l + 64, l + 192 (a one-wave record: l, l + 64;
+         * a two-wave record: l + 64; a long one: l + 64, l + 192) */
+        /* (three named values, not an array: a wave-dependent choice between array elements became a dynamic index, i.e.
+         * the array went to scratch) */
+        const V4 pin0 = load_full(ms->data + 16 * (size_t)lane), pin1 = load_full(ms->data + 16 * (size_t)(lane + 64)),
+                 pin2 = load_full(ms->data + 16 * (size_t)(lane + 128 + 64 * wave));
         const ptls_hip_record_t rec = rq.rec;
         const uint32_t flags = __builtin_amdgcn_readfirstlane(rq.flags);
         const uint4 ivo = (flags & WREQ_IV) ? uint4{rq.iv[0], rq.iv[1], rq.iv[2], 1u} : uint4{0, 0, 0, 0};
@@ -1023,7 +1026,7 @@ __global__ void __launch_bounds__(WORKER_WG)
         /* WORKER_STAMPS builds (with STAMP_PHASES): the record's phase stamps (shader cycles) go to the end of the data area,
          * clk[1] = the request loaded, clk[9] = the record done */
         uint64_t *wclk = WORKER_STAMPS ? reinterpret_cast<uint64_t *>(ms->data + WORKER_DATA - 128) : nullptr;
-        if (WORKER_STAMPS && wave == 0) {
+        if (WORKER_STAMPS && wave == 1) {
             const uint64_t t = __builtin_amdgcn_s_memtime();
             if (lane == 0)
                 wclk[1] = t;
@@ -1037,11 +1040,13 @@ __global__ void __launch_bounds__(WORKER_WG)
                 v = load_full(in + rec.in_off + 16 * (size_t)(i - na1));
             return v;
         };
+        /* A record of at most MW_MIN_N - 1 elements and an ECB block run on wave 1: wave 0 polled, and it still waits for its
+         * last poll reads (its acquire drains them, ~1 PCIe round trip); wave 1 has none in flight (round 6). */
         if (ecb) {
-            /* one block with the slot's round keys (the block was read with the request: pin[0], lane 0's element) */
-            if (wave == 0) {
-                const V4 blk = V4{(uint32_t)__builtin_amdgcn_readfirstlane(pin[0].w0), (uint32_t)__builtin_amdgcn_readfirstlane(pin[0].w1),
-                                  (uint32_t)__builtin_amdgcn_readfirstlane(pin[0].w2), (uint32_t)__builtin_amdgcn_readfirstlane(pin[0].w3)};
+            /* one block with the slot's round keys (the block was read with the request: pin0, lane 0's element) */
+            if (wave == 1) {
+                const V4 blk = V4{(uint32_t)__builtin_amdgcn_readfirstlane(pin0.w0), (uint32_t)__builtin_amdgcn_readfirstlane(pin0.w1),
+                                  (uint32_t)__builtin_amdgcn_readfirstlane(pin0.w2), (uint32_t)__builtin_amdgcn_readfirstlane(pin0.w3)};
                 const V4 m = a256 ? aes_encrypt<14>(lds, lb_aes, slots->rk, blk) : aes_encrypt<10>(lds, lb_aes, slots->rk, blk);
                 if (lane == 0)
                     store_full(out, m);
@@ -1049,8 +1054,8 @@ __global__ void __launch_bounds__(WORKER_WG)
         } else if (longrec) {
             V4 p2[2];
             if (flags & WREQ_INLINE) {
-                p2[0] = pin[0];
-                p2[1] = pin[2];
+                p2[0] = wave == 0 ? pin0 : pin1;
+                p2[1] = pin2;
             } else {
                 p2[0] = elem_block(lane + 64 * wave);
                 p2[1] = elem_block(lane + 64 * wave + 128);
@@ -1069,7 +1074,7 @@ __global__ void __launch_bounds__(WORKER_WG)
                 sparse_record<10, false, true, true, 128>(lds, lane, lb_aes, tab_w, rec, 0, in, aad, out, result, slots, basis, supp,
                                                           hp_slots, 1, mask, true, p2, nullptr, false, false, pa, ctab_w, wave, XSLOT, ivo);
         } else if (mw) {
-            const V4 mine = (flags & WREQ_INLINE) ? pin[0] : elem_block(lane + 64 * wave);
+            const V4 mine = (flags & WREQ_INLINE) ? (wave == 0 ? pin0 : pin1) : elem_block(lane + 64 * wave);
             const uint32_t ctab_w = wave == 0 ? CTAB0 : CTAB1;
             if (open && a256)
                 mw_record<14, true, true>(lds, wave, lane, lb_aes, ctab_w, tab, rec, in, aad, out, result, slots, basis, supp, hp_slots, 1, mask, mine, ivo);
@@ -1079,13 +1084,13 @@ __global__ void __launch_bounds__(WORKER_WG)
                 mw_record<14, false, true>(lds, wave, lane, lb_aes, ctab_w, tab, rec, in, aad, out, result, slots, basis, supp, hp_slots, 1, mask, mine, ivo);
             else
                 mw_record<10, false, true>(lds, wave, lane, lb_aes, ctab_w, tab, rec, in, aad, out, result, slots, basis, supp, hp_slots, 1, mask, mine, ivo);
-        } else if (wave == 0) {
+        } else if (wave == 1) {
             {
                 /* the record's first two elements per lane, as the launched single-record kernel reads them */
                 V4 pre[2];
                 if (flags & WREQ_INLINE) {
-                    pre[0] = pin[0];
-                    pre[1] = pin[1];
+                    pre[0] = pin0;
+                    pre[1] = pin1;
                 } else {
                     pre[0] = elem_block(lane);
                     pre[1] = elem_block(lane + 64);
@@ -1107,7 +1112,7 @@ __global__ void __launch_bounds__(WORKER_WG)
         }
         /* the wave holding the tag (wave 1 of a two-wave record; wave 0 otherwise): every store of the call reaches system
          * scope before its completion word (wave 0 of a two-wave record released its own before mw_record's barrier) */
-        if (wave == (mw ? 1 : longrec ? ((n1 - 1) & 127) >> 6 : 0)) {
+        if (wave == (longrec ? ((n1 - 1) & 127) >> 6 : 1)) {
             if (WORKER_STAMPS) {
                 st[3] = worker_stamp();
                 const uint64_t t = __builtin_amdgcn_s_memtime();
