@@ -297,9 +297,13 @@ int ptls_hip_tls13_open_batch(ptls_hip_batch_t *batch, ptls_hip_keyset_t *ks, co
  * cut the record list into slices whose input / output / AAD byte spans fit a slot and overlap, per
  * slice, H2D copy -> kernel -> D2H copy.  Offsets in `recs` are relative to the host buffers.  The
  * call returns when every output byte (and result) is in host memory.  Host buffers should be
- * pinned (hipHostMalloc'd, or ptls_hip_host_register'ed) for the copies to run asynchronously.  Each
- * slice's output (and mask) span is copied back whole: bytes lying between records inside it are not
- * preserved (the device-resident batch calls leave them untouched). */
+ * pinned (hipHostMalloc'd, or ptls_hip_host_register'ed) for the copies to run asynchronously.
+ * Only the records' output bytes change in the caller's output buffer (as fusion's storen128 and tag
+ * store, lib/fusion.c:388-397, :632): a slice's output comes back as the records' runs, several runs
+ * joined by one copy over short gaps that were first filled, on the device, with the caller's own bytes
+ * of those gaps (read when the slice is planned; do not modify them during the call), never over another
+ * slice's record.  The mask span of seal_supp is uploaded before and copied back after the kernel, so its
+ * other bytes come back unchanged as well. */
 typedef struct st_ptls_hip_pipeline_t ptls_hip_pipeline_t;
 ptls_hip_pipeline_t *ptls_hip_pipeline_new(ptls_hip_engine_t *engine, size_t slice_bytes);
 void ptls_hip_pipeline_free(ptls_hip_pipeline_t *p);
@@ -326,7 +330,7 @@ int ptls_hip_pipeline_tls13_open(ptls_hip_pipeline_t *p, ptls_hip_keyset_t *ks, 
  * mask) is pinned or registered, COPY otherwise.  COPY: the staging described above (copy engines).  MAPPED: no
  * staging -- the kernels read the records from and write them to the host buffers over PCIe themselves (their
  * device mappings, hipHostGetDevicePointer), one launch per max-records slice; bytes between records in the
- * output are then left untouched, as by the device-resident batch calls.  A call in MAPPED mode with an unmapped
+ * output are never written, as by the device-resident batch calls.  A call in MAPPED mode with an unmapped
  * buffer fails with PTLS_HIP_EINVAL.  last_transport: what the last seal/open of the pipeline used. */
 #define PTLS_HIP_TRANSPORT_AUTO 0
 #define PTLS_HIP_TRANSPORT_COPY 1
