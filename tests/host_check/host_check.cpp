@@ -12,17 +12,24 @@
  *     permutation in key runs;
  *   - ptls_hip_partition_bytes on random lengths and part counts;
  *   - the argument checks of the C ABI with NULL / out-of-range arguments, and the plugin's setup_crypto without a device
- *     (it must fail cleanly: no CPU fallback).
+ *     (it must fail cleanly: no CPU fallback);
+ *   - with a gfx950 device (argument "device", run on the GPU box): the host pipelines over random layouts -- both
+ *     transports, records in and out of output order, 1-64-byte gaps, exactly-sized heap buffers -- sealed and opened
+ *     back, every record compared with the CPU oracle (oracle/aesgcm_oracle.c, test infrastructure) and every byte
+ *     between records checked unchanged: the slicing, gap-planning and descriptor code of pipeline.cpp under the
+ *     sanitizers (the kernels are the product's).
  * Any sanitizer report aborts the process (-fno-sanitize-recover, halt_on_error); the exit status is 0 only when every
  * check held.  Test infrastructure only: nothing here ships.
  */
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <algorithm>
 #include <random>
 #include <vector>
 
 #include "host.h"
+#include "aesgcm_oracle.h"
 
 static int failures = 0;
 #define CHECK(c)                                                                                                                   \
@@ -276,8 +283,150 @@ static void check_abi_without_device(void)
     CHECK(ptls_hip_aesgcm_new(key, 24, 1500) == nullptr);
 }
 
+/* one pipeline seal + open over a random layout; returns false (and counts failures) on a mismatch */
+static void pipeline_trial(std::mt19937_64 &rng, ptls_hip_pipeline_t *pipe, ptls_hip_keyset_t *ks, size_t key_size,
+                           const std::vector<uint8_t> &keys, const std::vector<uint8_t> &ivs, int transport)
+{
+    const size_t n = 1 + rng() % 160;
+    std::vector<uint32_t> len(n), alen(n), key(n);
+    std::vector<uint64_t> in_off(n), out_off(n), aad_off(n), pt_off(n);
+    size_t in_sz = 0, out_sz = 0, aad_sz = 0, pt_sz = 0;
+    for (size_t i = 0; i < n; ++i) {
+        len[i] = (uint32_t)(rng() % 8 == 0 ? rng() % 16385 : rng() % 3000);
+        alen[i] = (uint32_t)(rng() % 41);
+        key[i] = (uint32_t)((i * 3) / n);
+        in_off[i] = in_sz + rng() % 4;
+        in_sz = in_off[i] + len[i];
+        aad_off[i] = aad_sz + rng() % 4;
+        aad_sz = aad_off[i] + alen[i];
+        out_off[i] = out_sz + 1 + rng() % 64;
+        out_sz = out_off[i] + len[i] + 16;
+        pt_off[i] = pt_sz + 1 + rng() % 64;
+        pt_sz = pt_off[i] + len[i];
+    }
+    out_sz += 1 + rng() % 64;
+    pt_sz += 1 + rng() % 64;
+    const bool pinned = transport == PTLS_HIP_TRANSPORT_MAPPED;
+    /* exactly-sized buffers: heap (ASan-checked) for COPY, pinned for MAPPED */
+    auto alloc = [&](size_t sz) -> uint8_t * {
+        void *p = nullptr;
+        if (pinned) {
+            if (hipHostMalloc(&p, sz ? sz : 1, hipHostMallocDefault) != hipSuccess)
+                return nullptr;
+        } else {
+            p = malloc(sz ? sz : 1);
+        }
+        return static_cast<uint8_t *>(p);
+    };
+    auto release = [&](uint8_t *p) {
+        if (pinned)
+            (void)hipHostFree(p);
+        else
+            free(p);
+    };
+    uint8_t *h_in = alloc(in_sz), *h_aad = alloc(aad_sz), *h_out = alloc(out_sz), *h_pt = alloc(pt_sz);
+    CHECK(h_in && h_aad && h_out && h_pt);
+    if (!(h_in && h_aad && h_out && h_pt))
+        return;
+    for (size_t i = 0; i < in_sz; ++i)
+        h_in[i] = (uint8_t)rng();
+    for (size_t i = 0; i < aad_sz; ++i)
+        h_aad[i] = (uint8_t)rng();
+    memset(h_out, 0xA5, out_sz);
+    memset(h_pt, 0x5A, pt_sz);
+    /* descriptors, in output order or shuffled */
+    std::vector<size_t> perm(n);
+    for (size_t i = 0; i < n; ++i)
+        perm[i] = i;
+    if (rng() % 2)
+        std::shuffle(perm.begin(), perm.end(), rng);
+    std::vector<ptls_hip_record_t> rs(n), ro(n);
+    for (size_t k = 0; k < n; ++k) {
+        const size_t i = perm[k];
+        rs[k] = ptls_hip_record_t{in_off[i], out_off[i], aad_off[i], 1000 + i, len[i], alen[i], key[i], 0};
+        ro[k] = ptls_hip_record_t{out_off[i], pt_off[i], aad_off[i], 1000 + i, len[i], alen[i], key[i], 0};
+    }
+    CHECK(ptls_hip_pipeline_set_transport(pipe, transport) == 0);
+    int rc = ptls_hip_pipeline_seal(pipe, ks, rs.data(), n, h_in, h_aad, h_out);
+    CHECK(rc == 0);
+    std::vector<uint8_t> exp;
+    std::vector<uint8_t> touched(out_sz, 0);
+    for (size_t i = 0; rc == 0 && i < n; ++i) {
+        exp.resize(len[i] + 16);
+        oracle_aesgcm_seal(&keys[key[i] * key_size], key_size, &ivs[key[i] * 12], 1000 + i, h_aad + aad_off[i], alen[i],
+                           h_in + in_off[i], len[i], exp.data());
+        CHECK(memcmp(h_out + out_off[i], exp.data(), len[i] + 16) == 0);
+        memset(&touched[out_off[i]], 1, len[i] + 16);
+    }
+    for (size_t b = 0; b < out_sz; ++b)
+        if (!touched[b] && h_out[b] != 0xA5) {
+            CHECK(!"seal wrote a byte between records");
+            break;
+        }
+    CHECK(ptls_hip_pipeline_last_transport(pipe) == transport);
+    std::vector<uint64_t> res(n, 0);
+    uint64_t *h_res = res.data();
+    void *pres = nullptr;
+    if (pinned && hipHostMalloc(&pres, n * 8, hipHostMallocDefault) == hipSuccess)
+        h_res = static_cast<uint64_t *>(pres);
+    rc = ptls_hip_pipeline_open(pipe, ks, ro.data(), n, h_out, h_aad, h_pt, h_res);
+    CHECK(rc == 0);
+    std::vector<uint8_t> ptouched(pt_sz, 0);
+    for (size_t k = 0; rc == 0 && k < n; ++k) {
+        const size_t i = perm[k];
+        CHECK(h_res[k] == len[i]);
+        CHECK(memcmp(h_pt + pt_off[i], h_in + in_off[i], len[i]) == 0);
+        memset(&ptouched[pt_off[i]], 1, len[i]);
+    }
+    for (size_t b = 0; b < pt_sz; ++b)
+        if (!ptouched[b] && h_pt[b] != 0x5A) {
+            CHECK(!"open wrote a byte between records");
+            break;
+        }
+    if (pres != nullptr)
+        (void)hipHostFree(pres);
+    release(h_in);
+    release(h_aad);
+    release(h_out);
+    release(h_pt);
+}
+
+static void check_pipelines_on_device(std::mt19937_64 &rng, int trials)
+{
+    ptls_hip_engine_t *eng = ptls_hip_engine_new(0);
+    if (eng == nullptr) {
+        printf("host_check: no usable gfx950 device (%s): device paths skipped\n", ptls_hip_last_error());
+        return;
+    }
+    for (size_t key_size : {(size_t)16, (size_t)32}) {
+        std::vector<uint8_t> keys(3 * key_size), ivs(3 * 12);
+        for (auto &b : keys)
+            b = (uint8_t)rng();
+        for (auto &b : ivs)
+            b = (uint8_t)rng();
+        ptls_hip_keyset_t *ks = ptls_hip_keyset_new(eng, key_size, 3);
+        CHECK(ks != nullptr && ptls_hip_keyset_set(ks, 0, 3, keys.data(), ivs.data(), nullptr) == 0);
+        for (size_t slice : {(size_t)64 << 10, (size_t)1 << 20}) {
+            ptls_hip_pipeline_t *pipe = ptls_hip_pipeline_new(eng, slice);
+            CHECK(pipe != nullptr);
+            for (int t = 0; pipe != nullptr && t < trials; ++t)
+                pipeline_trial(rng, pipe, ks, key_size, keys, ivs, t % 2 ? PTLS_HIP_TRANSPORT_COPY : PTLS_HIP_TRANSPORT_MAPPED);
+            ptls_hip_pipeline_free(pipe);
+        }
+        ptls_hip_keyset_free(ks);
+    }
+    ptls_hip_engine_free(eng);
+    printf("host_check: device paths run (%d trials x 2 key sizes x 2 slice sizes)\n", trials);
+}
+
 int main(int argc, char **argv)
 {
+    if (argc > 1 && std::strcmp(argv[1], "device") == 0) { /* the GPU box: the pipelines under the sanitizers */
+        std::mt19937_64 rng(0x70697065ull);
+        check_pipelines_on_device(rng, argc > 2 ? atoi(argv[2]) : 40);
+        printf("host_check: %s (%d failed checks)\n", failures == 0 ? "ok" : "FAILED", failures);
+        return failures == 0 ? 0 : 1;
+    }
     const int scale = argc > 1 ? atoi(argv[1]) : 1;
     std::mt19937_64 rng(0x68737467ull);
     check_parse(rng, 100000 * scale);

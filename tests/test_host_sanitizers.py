@@ -29,3 +29,19 @@ def test_host_code_is_clean_under_asan_ubsan():
     out = r.stdout + r.stderr
     assert r.returncode == 0 and "host_check: ok (0 failed checks)" in out, out[-4000:]
     assert "ERROR: AddressSanitizer" not in out and "runtime error" not in out, out[-4000:]
+
+
+@pytest.mark.gpu
+def test_host_pipelines_clean_under_asan_ubsan_on_device():
+    """the same driver on the GPU box (argument "device"): 80 random pipeline layouts per key size -- both transports,
+    64 KiB and 1 MiB slices, records in and out of output order, 1-64-byte gaps, exactly-sized heap buffers for the copy
+    transport -- sealed and opened back, every record compared with the CPU oracle and every byte between records checked
+    unchanged, with pipeline.cpp's slicing and gap planning instrumented (the kernels are the product's).  Built here by
+    __graft_entry__.build() (make tests-builds); the GPU box runs the shipped binary."""
+    if not os.path.exists(BIN):
+        pytest.skip("asan/host_check not built (make -C hsig-picotls_amd asan)")
+    env = dict(os.environ, ASAN_OPTIONS="protect_shadow_gap=0:detect_leaks=0:halt_on_error=1",
+               UBSAN_OPTIONS="halt_on_error=1:print_stacktrace=1")
+    r = subprocess.run([BIN, "device", "40"], capture_output=True, text=True, timeout=600, env=env)
+    out = r.stdout + r.stderr
+    assert r.returncode == 0 and "host_check: ok (0 failed checks)" in out and "device paths run" in out, out[-4000:]
