@@ -86,7 +86,7 @@ def record_lengths(cfg, idx):
 def partition_bytes(lens, parts):
     """contiguous ranges [b[r], b[r + 1]) of records with about equal payload bytes each (prefix sum
     of L): range r ends at the first record whose prefix sum reaches (r + 1) / parts of the total.  The same rule as
-    ptls_hip_partition_bytes (engine.cpp)."""
+    ptls_hip_partition_bytes (node.cpp)."""
     lens = np.asarray(lens, dtype=np.uint64)
     csum = np.cumsum(lens, dtype=np.uint64)
     total = int(csum[-1]) if len(csum) else 0

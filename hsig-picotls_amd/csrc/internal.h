@@ -1,5 +1,5 @@
 /*
- * internal.h -- layouts shared by the host engine (engine.cpp) and the gfx950 kernels (aesgcm_kernels.hip).
+ * internal.h -- layouts shared by the host units (host.h) and the gfx950 kernels (aesgcm_kernels.hip).
  *
  * HBM layout:
  *   key slots    KeySlot[nslots]             512 B each: round keys, static IV, H powers
@@ -36,7 +36,7 @@ constexpr int SPARSE_LANES = 64; /* "lanes" value of the wave-per-record kernel 
 constexpr int SPARSE_MAX_PER_RUN = 20; /* configs[3]'s lengths, seal GiB/s, sparse kernel / 32 lanes (round 3): 16 records
                                            per key 533 / 498, 24 per key 533 / 680 (tools/calls_r03/r03_call24.sh) */
 /* one workgroup per CU (LDS-limited); 768 threads (3 waves per SIMD, 168 VGPRs) by default, 512 selectable
- * per batch (engine.cpp:plan_wg).  WG_MAX bounds the chunk size the planner cuts key runs into. */
+ * per batch (planner.cpp plan_wg).  WG_MAX bounds the chunk size the planner cuts key runs into. */
 constexpr int WG_MAX = 1024;
 
 struct KeySlot {
@@ -95,7 +95,7 @@ struct KernelArgs {
 /* chunk-queue slots per engine: launches take them round robin, so two launches in flight never share one */
 constexpr uint32_t QUEUE_SLOTS = 4096;
 
-/* The plugin worker (sparse_kernel.hip plugin_worker_kernel, engine.cpp): a resident kernel whose workgroups each serve
+/* The plugin worker (sparse_kernel.hip plugin_worker_kernel, plugin_worker.cpp): a resident kernel whose workgroups each serve
  * the plugin's single-record calls from their own mailbox in fine-grained pinned host memory instead of one kernel launch
  * per call.  The host writes the request, then (release) seq; the workgroup serves it, stores the call's completion word
  * (as a launched call's kernel does), then `served`. */

@@ -878,7 +878,7 @@ __device__ __forceinline__ T *as_global(T *p)
 /* The key slot and basis pointers of a request are constant-address-space pointers (as_const), so the round keys come
  * through the scalar unit (s_load) as in a launched kernel (16 KiB record 28 -> 24 us per call, one ECB block 10.1 ->
  * 9.3 us; tools/calls_r04/r04_call8.sh).  Valid because a slot the resident dispatch may have read never changes while it
- * is resident (engine.cpp slot pool: a freed slot is reused only after that dispatch has left; the IV travels in the
+ * is resident (plugin_worker.cpp slot pool: a freed slot is reused only after that dispatch has left; the IV travels in the
  * request).  The round-3 attempt faulted, and so did this one's first build (r04_call7.sh): both rebuilt the 64-bit
  * pointer from two readfirstlane results, which return int, so an address with bit 31 set sign-extended over the high
  * half (s_bfe_i64 in the disassembly); as_const widens each half through uint32_t (EXPERIMENTS.md E3, "worker requests with key material through the scalar unit"). */
@@ -925,7 +925,7 @@ __global__ void __launch_bounds__(WORKER_WG)
     const uint32_t tab = SP_TAB;
     build_aes_tables<WORKER_WG>(lds, 0, t0);
     __syncthreads();
-    WorkerSlot *ms = mb + blockIdx.x; /* one mailbox per workgroup (engine.cpp PluginWorker: one per calling thread) */
+    WorkerSlot *ms = mb + blockIdx.x; /* one mailbox per workgroup (plugin.h PluginWorker: one per calling thread) */
     const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
     uint64_t t_last = t_start;
     uint32_t last = __builtin_amdgcn_readfirstlane(__hip_atomic_load(&ms->served, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
@@ -984,7 +984,7 @@ __global__ void __launch_bounds__(WORKER_WG)
          * loads is not enough: the vector L1 keeps the previous request's lines at the same addresses (measured: a
          * workgroup-scope acquire served request 2 with request 1's completion pointer), so the acquire is at system
          * scope, which invalidates the L1 and the L2's lines of host memory.  A key slot this dispatch may have read is never
-         * rewritten while it is resident (engine.cpp slot pool: a freed slot is handed out again only after the dispatch
+         * rewritten while it is resident (plugin_worker.cpp slot pool: a freed slot is handed out again only after the dispatch
          * that could hold it has left), so neither the scalar nor the vector caches can hold a stale key slot. */
         uint64_t st[5] = {0, 0, 0, 0, 0};
         if (WORKER_STAMPS)

@@ -1,7 +1,7 @@
 """BASELINE configs[3]'s real execution path under parity (used by tests/test_gpu_c4_keyruns.py).
 
 configs[3] is 4M mixed-length (64 B - 16 KiB) AES-256 records over 64K keys: 64 records per key.  The planner
-(engine.cpp choose_lanes) runs such key runs on the 32-lane batch kernel, each run one chunk of 32 wave tasks (the
+(planner.cpp choose_lanes) runs such key runs on the 32-lane batch kernel, each run one chunk of 32 wave tasks (the
 chunk cap: bench.py's full shape and this one plan the same chunks), so every chunk is a key switch: a workgroup
 rebuilds the key's GHASH tables and resets its task counter between two barriers (batch_kernel.h).  The config samples
 of tests/golden/configs.json hold <= 8 records per key, which the planner sends to the sparse kernel instead, so this

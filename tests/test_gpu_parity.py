@@ -803,7 +803,7 @@ def test_key_setup_for_many_slots(engine, oracle, key_len):
 def test_host_pipeline_plan_keeps_caller_order(engine, oracle, transport, shape):
     """records that already come as the planner orders them (equal lengths, or non-increasing within each key run):
     the pipeline reuses the caller-order descriptors as the plan-order ones (no gather, one upload per slice,
-    engine.cpp identity_order); several slices, two key runs; bit-exact vs the oracle and opened back"""
+    planner.cpp identity_order); several slices, two key runs; bit-exact vs the oracle and opened back"""
     n = 1200
     if shape == "equal":
         lens = [1350] * n

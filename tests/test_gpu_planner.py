@@ -1,4 +1,4 @@
-"""The launch planner's lanes-per-record choice (engine.cpp choose_lanes), pinned on the shapes it was measured on.
+"""The launch planner's lanes-per-record choice (planner.cpp choose_lanes), pinned on the shapes it was measured on.
 
 Descriptors only: no record bytes are touched (a Batch plans on creation), so full-size shapes cost nothing but their
 descriptor upload.  The seal-rate evidence behind each row: round 5 small batches (tools/calls_r05/r05_call11.sh,

@@ -1,4 +1,4 @@
-"""The plugin worker (engine.cpp worker_call, sparse_kernel.hip plugin_worker_kernel): a resident kernel whose workgroups
+"""The plugin worker (plugin_worker.cpp worker_call, sparse_kernel.hip plugin_worker_kernel): a resident kernel whose workgroups
 serve plugin calls from pinned mailboxes (one per calling thread) instead of one launch per call.  Its lifecycle is exercised through the
 reference's own picotls lifecycle code (tests/plugin_driver.py) and every output is compared with lib/fusion.c
 (oracle/_ref): calls separated by gaps longer than the worker's idle timeout (it leaves, the next call relaunches it),
