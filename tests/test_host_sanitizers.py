@@ -23,7 +23,7 @@ def test_host_code_is_clean_under_asan_ubsan():
     r = subprocess.run(["make", "-s", "-j8", "-C", os.path.join(ROOT, "hsig-picotls_amd"), "asan"], capture_output=True,
                        text=True, timeout=900)
     assert r.returncode == 0, r.stderr[-3000:]
-    env = dict(os.environ, ASAN_OPTIONS="halt_on_error=1:detect_leaks=1:abort_on_error=0",
+    env = dict(os.environ, ASAN_OPTIONS="halt_on_error=1:detect_leaks=1:abort_on_error=0:verify_asan_link_order=0",
                UBSAN_OPTIONS="halt_on_error=1:print_stacktrace=1")
     r = subprocess.run([BIN, "1"], capture_output=True, text=True, timeout=900, env=env)
     out = r.stdout + r.stderr
@@ -40,7 +40,7 @@ def test_host_pipelines_clean_under_asan_ubsan_on_device():
     __graft_entry__.build() (make tests-builds); the GPU box runs the shipped binary."""
     if not os.path.exists(BIN):
         pytest.skip("asan/host_check not built (make -C hsig-picotls_amd asan)")
-    env = dict(os.environ, ASAN_OPTIONS="protect_shadow_gap=0:detect_leaks=0:halt_on_error=1",
+    env = dict(os.environ, ASAN_OPTIONS="protect_shadow_gap=0:detect_leaks=0:halt_on_error=1:verify_asan_link_order=0",
                UBSAN_OPTIONS="halt_on_error=1:print_stacktrace=1")
     r = subprocess.run([BIN, "device", "40"], capture_output=True, text=True, timeout=600, env=env)
     out = r.stdout + r.stderr
