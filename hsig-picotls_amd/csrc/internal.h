@@ -25,7 +25,7 @@
 namespace ptls_hip {
 
 constexpr int NPOW = 8; /* H^1 .. H^16 (batch kernel main tables), H^32 (batch kernel main table at G = 32), H^64 (sparse
-                          kernel), H^128 (a single record on two waves, stride 128) */
+                          kernel), H^128 (a single record on two or four waves, stride 128) */
 /* GHASH basis slot: NPOW x 128 vectors P * x^e, then H^1 .. H^128 (the lane combinations' per-lane final powers H^(q+1);
  * a two-wave single record of up to 128 GHASH elements multiplies element i by H^(N - i)) */
 constexpr int LANE_POWS = 128;

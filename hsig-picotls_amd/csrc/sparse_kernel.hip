@@ -199,20 +199,25 @@ __device__ __forceinline__ V4 ghash_combine(uint8_t *lds, uint32_t tab, int lane
  * constants, its per-wave H^64 table, the elements (generic head / branch-free stretch / generic tail), the lane
  * combination, the tag, header protection.  pre / prefetch: a single record's first two elements per lane, read before
  * (BYVAL: the plugin's launch and the worker). */
-template <int ROUNDS, bool OPEN, bool ALIGNED, bool BYVAL, int S = 64>
+template <int ROUNDS, bool OPEN, bool ALIGNED, bool BYVAL, int S = 64, int KPE = SPARSE_PE, bool SPLIT = false>
 __device__ __forceinline__ void sparse_record(uint8_t *lds, int lane, uint32_t lb_aes, uint32_t tab, const ptls_hip_record_t &rec,
                                               uint32_t rec_i, const uint8_t *in, const uint8_t *__restrict__ aad, uint8_t *out,
                                               uint64_t *__restrict__ result, const KeySlot *__restrict__ slots,
                                               const uint32_t *__restrict__ basis, const ptls_hip_supp_t *__restrict__ supp,
                                               const KeySlot *__restrict__ hp_slots, uint32_t hp_nslots, uint8_t *mask, bool prefetch,
                                               const V4 (&pre)[2], uint64_t *__restrict__ clk, bool stamps, bool bstamps, PhaseAcc &pa,
-                                              uint32_t ctab, int vw = 0, uint32_t xslot = 0, uint4 ivo = uint4{0, 0, 0, 0})
+                                              uint32_t ctab, int vw = 0, uint32_t xslot = 0, uint4 ivo = uint4{0, 0, 0, 0},
+                                              int e0 = 0, int hi_split = 0, uint32_t xsplit = 0)
 {
     /* S = 64: one wave per record (lane l: elements l + 64 m, Horner with H^64).  S = 128 (a single long record on two
      * waves, vw = this wave's index 0 / 1): the two waves act as one 128-lane wave, virtual lane vl = 64 vw + l takes
      * elements vl + 128 m with Horner by H^128 (basis plane 7) and multiplies its sum by H^(q+1), q = (N - 1 - vl) mod 128
      * (keysetup's list); wave 0's sum joins wave 1's through LDS (xslot) after a workgroup barrier, and the wave holding
-     * the length block (q = 0) writes the tag.  Every element index below goes through vl and S. */
+     * the length block (q = 0) writes the tag.  Every element index below goes through vl and S.
+     * SPLIT (S = 128, a long record on four waves): two such pairs, each on its own part of the record, elements
+     * [e0, hi_split): pair 0 takes [0, N - 128 k), pair 1 the last 128 k elements, so each lane's sum is weighted from the
+     * end of its own part (q = (hi - 1 - e0 - vl) mod 128).  Pair 0's sum is then multiplied by H^(128 k) (k Horner steps
+     * with the H^128 table) and handed to pair 1's tag wave through LDS (xsplit) after a second workgroup barrier. */
     static_assert(S == 64 || S == 128, "stride: one or two waves");
     constexpr int LOG2S = S == 64 ? 6 : 7;
     constexpr bool by_value = BYVAL;
@@ -224,6 +229,7 @@ __device__ __forceinline__ void sparse_record(uint8_t *lds, int lane, uint32_t l
      * record loop and under the register pressure spilled their value, one scratch reload and wait per record (round 4) */
     asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lane));
     const int vl = 64 * vw + lane; /* the virtual lane (S = 64: the lane) */
+    static_assert(!SPLIT || S == 128, "a split record: two pairs of waves at stride 128");
     const uint32_t key = __builtin_amdgcn_readfirstlane(rec.key);
     const KeySlot *__restrict__ slot = slots + key;
     const uint32_t *__restrict__ rk = slot->rk;
@@ -237,18 +243,21 @@ __device__ __forceinline__ void sparse_record(uint8_t *lds, int lane, uint32_t l
     const uint8_t *in_p = in + rec.in_off;
     uint8_t *out_p = out + rec.out_off;
     const uint8_t *aad_p = aad + rec.aad_off;
+    const int hi = SPLIT ? hi_split : N;      /* the end of this wave's part of the record (exclusive) */
+    const int vle = vl + (SPLIT ? e0 : 0);    /* the lane's first element */
+    const bool last_part = !SPLIT || hi == N; /* holds the length block (the tag) */
     /* ivo.w != 0: the static IV travels in the request (the plugin worker: an IV change never writes device memory) */
     const bool ov = __builtin_amdgcn_readfirstlane(ivo.w) != 0;
     const uint32_t n0 = __builtin_amdgcn_readfirstlane(ov ? ivo.x : slot->iv[0]),
                    n1 = __builtin_amdgcn_readfirstlane((ov ? ivo.y : slot->iv[1]) ^ bswap32((uint32_t)(rec.seq >> 32))),
                    n2 = __builtin_amdgcn_readfirstlane((ov ? ivo.z : slot->iv[2]) ^ bswap32((uint32_t)rec.seq));
-    const int iters = (N + S - 1) >> LOG2S;
-    const bool horner = iters > 1; /* N <= S: one element per lane, no Horner step */
+    const int iters = (hi - (SPLIT ? e0 : 0) + S - 1) >> LOG2S;
+    const bool horner = iters > 1 || SPLIT; /* N <= S: one element per lane, no Horner step (SPLIT: pair 0's H^128 steps) */
     V4 b[4];
     /* a single record (the plugin's launch): the H^64 basis loads go out before the counter-mode constants, so their
      * memory latency overlaps that LDS chain (in batches other waves hide it; there the early loads cost c4s open
      * 2.5 %, measured) */
-    const int q = (N - 1 - vl) & (S - 1);
+    const int q = (hi - 1 - vle) & (S - 1);
     /* batch records: the lane's first AAD block is loaded here, before the counter-mode constants and the H^64 table, so
      * its latency runs under that work (c4s seal 498-504 -> 513-519 GiB/s, profiles/r04_c4s_prefetch_ab.log) */
     V4 aad_pf = V4{0, 0, 0, 0};
@@ -304,7 +313,7 @@ __device__ __forceinline__ void sparse_record(uint8_t *lds, int lane, uint32_t l
         int big = 0;
 #pragma unroll
         for (int b = 0; b < NE; ++b) {
-            e[b] = elem_of(m + b < mend ? vl + (m + b) * S : N, N, na, nc, L, N);
+            e[b] = elem_of(m + b < mend ? vle + (m + b) * S : N, N, na, nc, L, hi);
             inb[b] = V4{0, 0, 0, 0};
             sft[b] = 0;
             /* the lane's first two elements of a single record were read at the start (pre) */
@@ -363,21 +372,21 @@ __device__ __forceinline__ void sparse_record(uint8_t *lds, int lane, uint32_t l
      * 2^16 (lane l, element m = data block 64 m + l - na).  There the body is branch-free, KP blocks per lane per
      * iteration, the counter-mode AES of the blocks skewed against the H^64 multiplies of the previous iteration's
      * ciphertext (seal) or of the input ciphertext (open), the next iteration's plaintext prefetched. */
-    constexpr int KP = SPARSE_PE;
+    constexpr int KP = KPE;
     const int nf = (L - (tflag ? 1 : 0)) >> 4;              /* full blocks that are all input bytes */
-    const int lastc = min(nf, 65534) - 1;                   /* last data block allowed in the stretch */
+    const int lastc = min(min(nf, 65534) - 1, hi - 1 - na); /* last data block allowed in the stretch (of this part) */
     /* Each lane starts the stretch at its own first data element (m = 1 on the lanes holding the AAD block, 0 on the
      * others) and ends where its blocks stop being full: the stretch is the shortest lane's, the AAD elements before
      * it are hashed only, and the record's generic head (one full AES per lane for one AAD block, 17 % of a c4s
      * record, tools/sparse_stamps.py) is gone. */
-    const int ml = vl < na ? (na - vl + S - 1) >> LOG2S : 0;                      /* the lane's first data element */
-    const int mhl = lastc + na - vl >= 0 ? ((lastc + na - vl) >> LOG2S) + 1 : 0;  /* its elements m < mhl: full blocks */
+    const int ml = vle < na ? (na - vle + S - 1) >> LOG2S : 0;                      /* the lane's first data element */
+    const int mhl = lastc + na - vle >= 0 ? ((lastc + na - vle) >> LOG2S) + 1 : 0;  /* its elements m < mhl: full blocks */
     const int fmin = -wave_max_sp(-max(mhl - ml, 0)); /* full-block elements every lane has */
     const int npure = fmin / KP;
     /* an odd full element left over by the KP-block iterations takes one single-block step of the stretch instead of the
      * generic path */
     const int npx = npure > 0 && fmin - npure * KP > 0 ? 1 : 0;
-    const int iters_l = vl < N ? ((N - 1 - vl) >> LOG2S) + 1 : 0;                /* the lane's elements */
+    const int iters_l = vle < hi ? ((hi - 1 - vle) >> LOG2S) + 1 : 0;            /* the lane's elements */
     const int pm1 = ml + npure * KP + npx;                                        /* the lane's first after the stretch */
     if (!npure) { /* head and tail are one range: elements share one round trip to the record's memory (the plugin) */
         generic_range(std::integral_constant<bool, BYVAL>{}, 0, iters);
@@ -385,7 +394,7 @@ __device__ __forceinline__ void sparse_record(uint8_t *lds, int lane, uint32_t l
         const int naad = wave_max_sp(ml);
         for (int j = 0; j < naad; ++j) {
             if (j < ml) {
-                const int i = vl + S * j;
+                const int i = vle + S * j;
                 const int nb = min(16, A - 16 * i);
                 const V4 x = (BYVAL && prefetch && j < 2)       ? mask_block(j == 0 ? pre[0] : pre[1], nb)
                              : (!BYVAL && j == 0)                ? aad_pf
@@ -397,7 +406,7 @@ __device__ __forceinline__ void sparse_record(uint8_t *lds, int lane, uint32_t l
     phase_stamp(clk, stamps, lane, 4);
     phase_acc(pa, bstamps, 4);
     if (npure) {
-        const int c0 = S * ml + vl - na; /* the lane's first data block of the stretch */
+        const int c0 = S * ml + vle - na; /* the lane's first data block of the stretch */
         const uint8_t *src = in_p + 16 * (size_t)c0;
         uint8_t *dst = out_p + 16 * (size_t)c0;
         V4 pend[KP], bufA[KP], bufB[KP];
@@ -500,7 +509,7 @@ __device__ __forceinline__ void sparse_record(uint8_t *lds, int lane, uint32_t l
         y = ghash_combine(lds, tab, lane, bs, q, y);
     /* S = 128: the wave without the length block hands its sum over (and makes its output stores visible at system scope
      * first: the tag wave's caller stores the completion word); both waves pass the barrier */
-    const int tagw = ((N - 1) & (S - 1)) >> 6;
+    const int tagw = ((hi - 1 - (SPLIT ? e0 : 0)) & (S - 1)) >> 6;
     if (S > 64) {
         if (vw != tagw) {
             if (lane == 0)
@@ -511,9 +520,21 @@ __device__ __forceinline__ void sparse_record(uint8_t *lds, int lane, uint32_t l
         if (vw == tagw)
             y = v4xor(y, lds128(lds, xslot));
     }
+    if (SPLIT) { /* pair 0's sum times H^(N - hi) = (H^128)^k, to pair 1's tag wave */
+        if (!last_part && vw == tagw) {
+            for (int j = 0; j < (N - hi) >> LOG2S; ++j)
+                y = gh_mul_nibble(lds, tab, y);
+            if (lane == 0)
+                lds128_store(lds, xsplit, y);
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+        }
+        __syncthreads();
+        if (last_part && vw == tagw)
+            y = v4xor(y, lds128(lds, xsplit));
+    }
     phase_stamp(clk, stamps, lane, 7);
     phase_acc(pa, bstamps, 7);
-    if (q == 0) {
+    if (q == 0 && last_part) {
         const V4 tag = v4xor(y, ek0);
         if (OPEN) {
             const V4 rt = load_block<false>(in_p + L, 16);
@@ -525,7 +546,7 @@ __device__ __forceinline__ void sparse_record(uint8_t *lds, int lane, uint32_t l
     }
     phase_stamp(clk, stamps, lane, 8);
     phase_acc(pa, bstamps, 8);
-    if (!OPEN && supp != nullptr && vw == tagw) {
+    if (!OPEN && supp != nullptr && vw == tagw && last_part) {
         /* QUIC header protection after the record (lib/fusion.c:636-650), as in aesgcm_batch_kernel: the
          * sample may cover the tag written by another lane of this wave */
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
@@ -851,10 +872,12 @@ __global__ void __launch_bounds__(WG)
     }
 }
 
-/* The plugin worker: one wave stays resident and serves the mailbox (internal.h WorkerSlot, fine-grained pinned host
- * memory): it polls seq over PCIe, reads the request, runs the record through sparse_record (the single-record path of a
- * launched call: prefetched first elements, the wave's H^64 table, the early lane-combination table; records of 65..128
- * GHASH elements on both waves, mw_record), stores the call's completion word after all its output (system scope) and then `served`.  The AES tables are built
+/* The plugin worker: one workgroup stays resident per mailbox and serves it (internal.h WorkerSlot, fine-grained pinned
+ * host memory): wave 0 polls seq over PCIe, waves 0 and 1 read the request, and the record runs through sparse_record (the
+ * single-record path of a launched call: prefetched first elements, the wave's H^64 table, the early lane-combination
+ * table; records of 65..128 GHASH elements on waves 0 and 1, mw_record; longer ones on all four waves, two pairs at stride
+ * 128, waves 2 and 3 taking the request from wave 1 through LDS), then the tag's wave stores the call's completion word
+ * after all its output (system scope) and then `served`.  The AES tables are built
  * once for the worker's life instead of once per call, and no launch sits between the caller and the kernel.
  *   - Polling keeps WORKER_POLLS loads of {seq, quit} in flight (a PCIe read takes ~2 us): a new request is seen about one
  *     read latency after it is written, not up to two.
@@ -910,16 +933,21 @@ __device__ __forceinline__ uint64_t poll_word(const WorkerSlot *ms)
     return __hip_atomic_load(reinterpret_cast<const uint64_t *>(&ms->seq), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-constexpr int WORKER_WG = 128; /* two waves: wave 0 polls; both serve a two-wave record (mw_record) */
+/* four waves: wave 0 polls; waves 0 and 1 serve a two-wave record (mw_record), all four a long one (two pairs) */
+constexpr int WORKER_WG = 256;
 
 __global__ void __launch_bounds__(WORKER_WG)
     plugin_worker_kernel(WorkerSlot *mb, uint32_t epoch, const uint32_t *__restrict__ t0, uint64_t idle_ticks, uint64_t life_ticks,
                          uint64_t *activity)
 {
-    /* AES tables | wave 0's Horner table | wave 1's | wave 0's lane-combination table | wave 1's | the poll's verdict | the
-     * long record's hand-over */
-    constexpr uint32_t TAB1 = SP_TAB + 8192, CTAB0 = TAB1 + 8192, CTAB1 = CTAB0 + 16384, CTL = CTAB1 + 16384, XSLOT = CTL + 16;
-    __shared__ __attribute__((aligned(16))) uint8_t lds[XSLOT + 16];
+    /* AES tables | the H^128 Horner table (one key per request: the waves of a long record share it, each writing the same
+     * values before it reads them) | each wave's lane-combination table | the poll's verdict | a long record's hand-overs
+     * (pair 0, pair 1, pair 0 to pair 1) */
+    constexpr uint32_t CTAB0 = SP_TAB + 8192, CTL = CTAB0 + (WORKER_WG / 64) * 16384, XSLOT = CTL + 16, RQ = XSLOT + 48,
+                       RQW = RQ + (uint32_t)sizeof(WorkerReq);
+    __shared__ __attribute__((aligned(16))) uint8_t lds[RQW + 16];
+    /* wave 1 -> waves 2, 3: (request << 2) | (a two-wave record << 1) | a long record */
+    uint32_t *rq_word = reinterpret_cast<uint32_t *>(lds + RQW);
     const int lane = threadIdx.x & 63, wave = (int)(threadIdx.x >> 6);
     const uint32_t lb_aes = (uint32_t)(lane & 31) * 4u;
     const uint32_t tab = SP_TAB;
@@ -931,6 +959,8 @@ __global__ void __launch_bounds__(WORKER_WG)
     uint32_t last = __builtin_amdgcn_readfirstlane(__hip_atomic_load(&ms->served, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
     if (threadIdx.x == 0)
         __hip_atomic_store(&ms->started, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (threadIdx.x == 64) /* a request already served: never the next one's word (seen by waves 2, 3 after the first barrier) */
+        __hip_atomic_store(rq_word, last << 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     PhaseAcc pa{};
     uint64_t ring[WORKER_POLLS];
     if (wave == 0) {
@@ -980,159 +1010,202 @@ __global__ void __launch_bounds__(WORKER_WG)
         const uint32_t seq = __builtin_amdgcn_readfirstlane(verdict.x);
         if (__builtin_amdgcn_readfirstlane(verdict.y) != 0)
             break;
-        /* the request (and the record, inline or in the caller's pinned staging) was written before seq.  Ordering the
-         * loads is not enough: the vector L1 keeps the previous request's lines at the same addresses (measured: a
-         * workgroup-scope acquire served request 2 with request 1's completion pointer), so the acquire is at system
-         * scope, which invalidates the L1 and the L2's lines of host memory.  A key slot this dispatch may have read is never
-         * rewritten while it is resident (plugin_worker.cpp slot pool: a freed slot is handed out again only after the dispatch
-         * that could hold it has left), so neither the scalar nor the vector caches can hold a stale key slot. */
-        uint64_t st[5] = {0, 0, 0, 0, 0};
-        if (WORKER_STAMPS)
-            st[0] = worker_stamp();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
-        if (WORKER_STAMPS)
-            st[1] = worker_stamp();
-        if (threadIdx.x == 0)
-            __hip_atomic_store(&ms->seen, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        const WorkerReq &rq = ms->req;
-        /* an inline record's elements, loaded with the request (unused otherwise): wave 0 elements l, l + 64, l + 128
-         * (a two-wave record: l; a long one: l, l + 128), wave 1 elements l, l + 64, l + 192 (a one-wave record: l, l + 64;
-         * a two-wave record: l + 64; a long one: l + 64, l + 192) */
-        /* (three named values, not an array: a wave-dependent choice between array elements became a dynamic index, i.e.
-         * the array went to scratch) */
-        const V4 pin0 = load_full(ms->data + 16 * (size_t)lane), pin1 = load_full(ms->data + 16 * (size_t)(lane + 64)),
-                 pin2 = load_full(ms->data + 16 * (size_t)(lane + 128 + 64 * wave));
-        const ptls_hip_record_t rec = rq.rec;
-        const uint32_t flags = __builtin_amdgcn_readfirstlane(rq.flags);
-        const uint4 ivo = (flags & WREQ_IV) ? uint4{rq.iv[0], rq.iv[1], rq.iv[2], 1u} : uint4{0, 0, 0, 0};
-        const uint8_t *in = as_global(rq.in), *aad = as_global(rq.aad);
-        uint8_t *out = as_global(rq.out);
-        const KeySlot *slots = as_const(rq.slots);
-        uint32_t *done = as_global(rq.done);
-        const uint32_t done_seq = __builtin_amdgcn_readfirstlane(rq.done_seq);
-        const ptls_hip_supp_t *supp = rq.supp != nullptr ? as_global(rq.supp) : nullptr;
-        const KeySlot *hp_slots = rq.hp_slots != nullptr ? as_global(rq.hp_slots) : nullptr;
-        uint8_t *mask = rq.mask != nullptr ? as_global(rq.mask) : nullptr;
-        uint64_t *result = as_global(rq.result);
-        const uint32_t *basis = as_const(rq.basis);
-        const bool open = (flags & WREQ_OPEN) != 0, a256 = (flags & WREQ_AES256) != 0;
-        const int na1 = ((int)rec.aad_len + 15) >> 4, nc1 = ((int)rec.len + 15) >> 4;
-        const int n1 = na1 + nc1 + 1;
-        const bool ecb = (flags & WREQ_ECB) != 0;
-        const bool mw = !ecb && n1 >= MW_MIN_N && n1 <= MW_MAX_N;
-        const bool longrec = !ecb && n1 > MW_MAX_N; /* both waves at stride 128 (sparse_record S = 128) */
-        if (WORKER_STAMPS)
-            st[2] = worker_stamp();
-        /* WORKER_STAMPS builds (with STAMP_PHASES): the record's phase stamps (shader cycles) go to the end of the data area,
-         * clk[1] = the request loaded, clk[9] = the record done */
-        uint64_t *wclk = WORKER_STAMPS ? reinterpret_cast<uint64_t *>(ms->data + WORKER_DATA - 128) : nullptr;
-        if (WORKER_STAMPS && wave == 1) {
-            const uint64_t t = __builtin_amdgcn_s_memtime();
-            if (lane == 0)
-                wclk[1] = t;
+        /* Waves 0 and 1 read the request from the mailbox.  Waves 2 and 3 serve only a long record's second part: they
+         * wait for wave 1's copy of the request in LDS, since two more waves reading it over PCIe (and two more
+         * system-scope acquires) made every call slower by 0.3-0.9 us (measured, round 6). */
+        bool serve = true;
+        if (wave >= 2) {
+            uint32_t lw;
+            for (;;) {
+                lw = __builtin_amdgcn_readfirstlane(__hip_atomic_load(rq_word, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP));
+                if ((lw >> 2) == (seq & 0x3fffffffu))
+                    break;
+                __builtin_amdgcn_s_sleep(1);
+            }
+            serve = (lw & 1u) != 0;
+            if (lw & 2u)
+                __syncthreads(); /* mw_record's hand-over barrier */
         }
-        /* an element read from the caller's staging (records that do not fit inline) */
-        auto elem_block = [&](int i) __attribute__((always_inline)) {
-            V4 v = V4{0, 0, 0, 0};
-            if (i < na1)
-                v = load_full(aad + rec.aad_off + 16 * (size_t)i);
-            else if (i < na1 + nc1)
-                v = load_full(in + rec.in_off + 16 * (size_t)(i - na1));
-            return v;
-        };
-        /* A record of at most MW_MIN_N - 1 elements and an ECB block run on wave 1: wave 0 polled, and it still waits for its
-         * last poll reads (its acquire drains them, ~1 PCIe round trip); wave 1 has none in flight (round 6). */
-        if (ecb) {
-            /* one block with the slot's round keys (the block was read with the request: pin0, lane 0's element) */
+        if (serve) {
+            /* the request (and the record, inline or in the caller's pinned staging) was written before seq.  Ordering the
+             * loads is not enough: the vector L1 keeps the previous request's lines at the same addresses (measured: a
+             * workgroup-scope acquire served request 2 with request 1's completion pointer), so the acquire is at system
+             * scope, which invalidates the L1 and the L2's lines of host memory.  A key slot this dispatch may have read is never
+             * rewritten while it is resident (plugin_worker.cpp slot pool: a freed slot is handed out again only after the dispatch
+             * that could hold it has left), so neither the scalar nor the vector caches can hold a stale key slot. */
+            uint64_t st[5] = {0, 0, 0, 0, 0};
+            if (WORKER_STAMPS)
+                st[0] = worker_stamp();
+            if (wave < 2) /* (waves 2, 3: wave 1's acquire, then its release of the word above) */
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+            if (WORKER_STAMPS)
+                st[1] = worker_stamp();
+            if (threadIdx.x == 0)
+                __hip_atomic_store(&ms->seen, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            const WorkerReq &rq = wave < 2 ? ms->req : *reinterpret_cast<const WorkerReq *>(lds + RQ);
+            /* an inline record's elements, loaded with the request (unused otherwise): wave 0 elements l, l + 64, l + 128
+             * (a two-wave record: l; a long one: l, l + 128), wave 1 elements l, l + 64, l + 192 (a one-wave record: l, l + 64;
+             * a two-wave record: l + 64; a long one: l + 64, l + 192); waves 2 and 3 none (their part of a long record starts
+             * where the record's length puts it) */
+            /* (three named values, not an array: a wave-dependent choice between array elements became a dynamic index, i.e.
+             * the array went to scratch) */
+            V4 pin0 = V4{0, 0, 0, 0}, pin1 = V4{0, 0, 0, 0}, pin2 = V4{0, 0, 0, 0};
+            if (wave < 2) {
+                pin0 = load_full(ms->data + 16 * (size_t)lane);
+                pin1 = load_full(ms->data + 16 * (size_t)(lane + 64));
+                pin2 = load_full(ms->data + 16 * (size_t)(lane + 128 + 64 * wave));
+            }
+            V4 rqc = V4{0, 0, 0, 0}; /* wave 1: the request's bytes for waves 2, 3 */
+            if (wave == 1 && lane < (int)(sizeof(WorkerReq) / 16))
+                rqc = load_full(reinterpret_cast<const uint8_t *>(&ms->req) + 16 * (size_t)lane);
+            const ptls_hip_record_t rec = rq.rec;
+            const uint32_t flags = __builtin_amdgcn_readfirstlane(rq.flags);
+            const uint4 ivo = (flags & WREQ_IV) ? uint4{rq.iv[0], rq.iv[1], rq.iv[2], 1u} : uint4{0, 0, 0, 0};
+            const uint8_t *in = as_global(rq.in), *aad = as_global(rq.aad);
+            uint8_t *out = as_global(rq.out);
+            const KeySlot *slots = as_const(rq.slots);
+            uint32_t *done = as_global(rq.done);
+            const uint32_t done_seq = __builtin_amdgcn_readfirstlane(rq.done_seq);
+            const ptls_hip_supp_t *supp = rq.supp != nullptr ? as_global(rq.supp) : nullptr;
+            const KeySlot *hp_slots = rq.hp_slots != nullptr ? as_global(rq.hp_slots) : nullptr;
+            uint8_t *mask = rq.mask != nullptr ? as_global(rq.mask) : nullptr;
+            uint64_t *result = as_global(rq.result);
+            const uint32_t *basis = as_const(rq.basis);
+            const bool open = (flags & WREQ_OPEN) != 0, a256 = (flags & WREQ_AES256) != 0;
+            const int na1 = ((int)rec.aad_len + 15) >> 4, nc1 = ((int)rec.len + 15) >> 4;
+            const int n1 = na1 + nc1 + 1;
+            const bool ecb = (flags & WREQ_ECB) != 0;
+            const bool mw = !ecb && n1 >= MW_MIN_N && n1 <= MW_MAX_N;
+            /* a long record on two pairs of waves at stride 128 (sparse_record S = 128, SPLIT): pair 1 takes the last 128 k
+             * elements, about half */
+            const bool longrec = !ecb && n1 > MW_MAX_N;
+            const int n1b = n1 - 128 * max(1, n1 >> 8); /* where pair 1's part starts */
             if (wave == 1) {
-                const V4 blk = V4{(uint32_t)__builtin_amdgcn_readfirstlane(pin0.w0), (uint32_t)__builtin_amdgcn_readfirstlane(pin0.w1),
-                                  (uint32_t)__builtin_amdgcn_readfirstlane(pin0.w2), (uint32_t)__builtin_amdgcn_readfirstlane(pin0.w3)};
-                const V4 m = a256 ? aes_encrypt<14>(lds, lb_aes, slots->rk, blk) : aes_encrypt<10>(lds, lb_aes, slots->rk, blk);
+                if (lane < (int)(sizeof(WorkerReq) / 16))
+                    lds128_store(lds, RQ + 16u * (uint32_t)lane, rqc);
                 if (lane == 0)
-                    store_full(out, m);
+                    __hip_atomic_store(rq_word, (seq << 2) | (mw ? 2u : 0u) | (longrec ? 1u : 0u), __ATOMIC_RELEASE,
+                                       __HIP_MEMORY_SCOPE_WORKGROUP);
             }
-        } else if (longrec) {
-            V4 p2[2];
-            if (flags & WREQ_INLINE) {
-                p2[0] = wave == 0 ? pin0 : pin1;
-                p2[1] = pin2;
-            } else {
-                p2[0] = elem_block(lane + 64 * wave);
-                p2[1] = elem_block(lane + 64 * wave + 128);
-            }
-            const uint32_t tab_w = wave == 0 ? tab : TAB1, ctab_w = wave == 0 ? CTAB0 : CTAB1;
-            if (open && a256)
-                sparse_record<14, true, true, true, 128>(lds, lane, lb_aes, tab_w, rec, 0, in, aad, out, result, slots, basis, supp,
-                                                         hp_slots, 1, mask, true, p2, nullptr, false, false, pa, ctab_w, wave, XSLOT, ivo);
-            else if (open)
-                sparse_record<10, true, true, true, 128>(lds, lane, lb_aes, tab_w, rec, 0, in, aad, out, result, slots, basis, supp,
-                                                         hp_slots, 1, mask, true, p2, nullptr, false, false, pa, ctab_w, wave, XSLOT, ivo);
-            else if (a256)
-                sparse_record<14, false, true, true, 128>(lds, lane, lb_aes, tab_w, rec, 0, in, aad, out, result, slots, basis, supp,
-                                                          hp_slots, 1, mask, true, p2, nullptr, false, false, pa, ctab_w, wave, XSLOT, ivo);
-            else
-                sparse_record<10, false, true, true, 128>(lds, lane, lb_aes, tab_w, rec, 0, in, aad, out, result, slots, basis, supp,
-                                                          hp_slots, 1, mask, true, p2, nullptr, false, false, pa, ctab_w, wave, XSLOT, ivo);
-        } else if (mw) {
-            const V4 mine = (flags & WREQ_INLINE) ? (wave == 0 ? pin0 : pin1) : elem_block(lane + 64 * wave);
-            const uint32_t ctab_w = wave == 0 ? CTAB0 : CTAB1;
-            if (open && a256)
-                mw_record<14, true, true>(lds, wave, lane, lb_aes, ctab_w, tab, rec, in, aad, out, result, slots, basis, supp, hp_slots, 1, mask, mine, ivo);
-            else if (open)
-                mw_record<10, true, true>(lds, wave, lane, lb_aes, ctab_w, tab, rec, in, aad, out, result, slots, basis, supp, hp_slots, 1, mask, mine, ivo);
-            else if (a256)
-                mw_record<14, false, true>(lds, wave, lane, lb_aes, ctab_w, tab, rec, in, aad, out, result, slots, basis, supp, hp_slots, 1, mask, mine, ivo);
-            else
-                mw_record<10, false, true>(lds, wave, lane, lb_aes, ctab_w, tab, rec, in, aad, out, result, slots, basis, supp, hp_slots, 1, mask, mine, ivo);
-        } else if (wave == 1) {
-            {
-                /* the record's first two elements per lane, as the launched single-record kernel reads them */
-                V4 pre[2];
-                if (flags & WREQ_INLINE) {
-                    pre[0] = pin0;
-                    pre[1] = pin1;
-                } else {
-                    pre[0] = elem_block(lane);
-                    pre[1] = elem_block(lane + 64);
-                }
-                const uint32_t ctab = CTAB0;
-                if (open && a256)
-                    sparse_record<14, true, true, true>(lds, lane, lb_aes, tab, rec, 0, in, aad, out, result, slots, basis, supp,
-                                                        hp_slots, 1, mask, true, pre, wclk, WORKER_STAMPS, false, pa, ctab, 0, 0, ivo);
-                else if (open)
-                    sparse_record<10, true, true, true>(lds, lane, lb_aes, tab, rec, 0, in, aad, out, result, slots, basis, supp,
-                                                        hp_slots, 1, mask, true, pre, wclk, WORKER_STAMPS, false, pa, ctab, 0, 0, ivo);
-                else if (a256)
-                    sparse_record<14, false, true, true>(lds, lane, lb_aes, tab, rec, 0, in, aad, out, result, slots, basis, supp,
-                                                         hp_slots, 1, mask, true, pre, wclk, WORKER_STAMPS, false, pa, ctab, 0, 0, ivo);
-                else
-                    sparse_record<10, false, true, true>(lds, lane, lb_aes, tab, rec, 0, in, aad, out, result, slots, basis, supp,
-                                                         hp_slots, 1, mask, true, pre, wclk, WORKER_STAMPS, false, pa, ctab, 0, 0, ivo);
-            }
-        }
-        /* the wave holding the tag (wave 1 of a two-wave record; wave 0 otherwise): every store of the call reaches system
-         * scope before its completion word (wave 0 of a two-wave record released its own before mw_record's barrier) */
-        if (wave == (longrec ? ((n1 - 1) & 127) >> 6 : 1)) {
-            if (WORKER_STAMPS) {
-                st[3] = worker_stamp();
+            if (WORKER_STAMPS)
+                st[2] = worker_stamp();
+            /* WORKER_STAMPS builds (with STAMP_PHASES): the record's phase stamps (shader cycles) go to the end of the data area,
+             * clk[1] = the request loaded, clk[9] = the record done */
+            uint64_t *wclk = WORKER_STAMPS ? reinterpret_cast<uint64_t *>(ms->data + WORKER_DATA - 128) : nullptr;
+            if (WORKER_STAMPS && wave == 1) {
                 const uint64_t t = __builtin_amdgcn_s_memtime();
                 if (lane == 0)
-                    wclk[9] = t;
+                    wclk[1] = t;
             }
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-            if (WORKER_STAMPS) {
-                st[4] = worker_stamp();
-                if (lane < 5)
-                    __hip_atomic_store(&ms->stamps[lane], lane == 0 ? st[0] : lane == 1 ? st[1] : lane == 2 ? st[2] : lane == 3 ? st[3] : st[4],
-                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            /* an element read from the caller's staging (records that do not fit inline) */
+            auto elem_block = [&](int i) __attribute__((always_inline)) {
+                V4 v = V4{0, 0, 0, 0};
+                if (i < na1)
+                    v = load_full(aad + rec.aad_off + 16 * (size_t)i);
+                else if (i < na1 + nc1)
+                    v = load_full(in + rec.in_off + 16 * (size_t)(i - na1));
+                return v;
+            };
+            /* A record of at most MW_MIN_N - 1 elements and an ECB block run on wave 1: wave 0 polled, and it still waits for its
+             * last poll reads (its acquire drains them, ~1 PCIe round trip); wave 1 has none in flight (round 6). */
+            if (ecb) {
+                /* one block with the slot's round keys (the block was read with the request: pin0, lane 0's element) */
+                if (wave == 1) {
+                    const V4 blk = V4{(uint32_t)__builtin_amdgcn_readfirstlane(pin0.w0), (uint32_t)__builtin_amdgcn_readfirstlane(pin0.w1),
+                                      (uint32_t)__builtin_amdgcn_readfirstlane(pin0.w2), (uint32_t)__builtin_amdgcn_readfirstlane(pin0.w3)};
+                    const V4 m = a256 ? aes_encrypt<14>(lds, lb_aes, slots->rk, blk) : aes_encrypt<10>(lds, lb_aes, slots->rk, blk);
+                    if (lane == 0)
+                        store_full(out, m);
+                }
+            } else if (longrec) {
+                const int pair = wave >> 1, vw = wave & 1;
+                V4 p2[2] = {V4{0, 0, 0, 0}, V4{0, 0, 0, 0}};
+                if (pair == 0) { /* the first two elements of each lane of pair 0; pair 1 reads its own in the stretch */
+                    if (flags & WREQ_INLINE) {
+                        p2[0] = vw == 0 ? pin0 : pin1;
+                        p2[1] = pin2;
+                    } else {
+                        p2[0] = elem_block(lane + 64 * vw);
+                        p2[1] = elem_block(lane + 64 * vw + 128);
+                    }
+                }
+                const uint32_t ctab_w = CTAB0 + 16384u * (uint32_t)wave, xs = XSLOT + 16u * (uint32_t)pair;
+                const int e0 = pair == 0 ? 0 : n1b, hi = pair == 0 ? n1b : n1;
+                uint64_t *lwclk = WORKER_STAMPS && wave == 1 ? wclk : nullptr; /* (diagnostic builds: wave 1's phases) */
+                if (open && a256)
+                    sparse_record<14, true, true, true, 128, SPARSE_PE, true>(lds, lane, lb_aes, tab, rec, 0, in, aad, out, result, slots, basis, supp, hp_slots, 1, mask,
+                                                                              pair == 0, p2, lwclk, WORKER_STAMPS && wave == 1, false, pa, ctab_w, vw, xs, ivo, e0, hi, XSLOT + 32);
+                else if (open)
+                    sparse_record<10, true, true, true, 128, SPARSE_PE, true>(lds, lane, lb_aes, tab, rec, 0, in, aad, out, result, slots, basis, supp, hp_slots, 1, mask,
+                                                                              pair == 0, p2, lwclk, WORKER_STAMPS && wave == 1, false, pa, ctab_w, vw, xs, ivo, e0, hi, XSLOT + 32);
+                else if (a256)
+                    sparse_record<14, false, true, true, 128, SPARSE_PE, true>(lds, lane, lb_aes, tab, rec, 0, in, aad, out, result, slots, basis, supp, hp_slots, 1, mask,
+                                                                               pair == 0, p2, lwclk, WORKER_STAMPS && wave == 1, false, pa, ctab_w, vw, xs, ivo, e0, hi, XSLOT + 32);
+                else
+                    sparse_record<10, false, true, true, 128, SPARSE_PE, true>(lds, lane, lb_aes, tab, rec, 0, in, aad, out, result, slots, basis, supp, hp_slots, 1, mask,
+                                                                               pair == 0, p2, lwclk, WORKER_STAMPS && wave == 1, false, pa, ctab_w, vw, xs, ivo, e0, hi, XSLOT + 32);
+            } else if (mw) {
+                const V4 mine = (flags & WREQ_INLINE) ? (wave == 0 ? pin0 : pin1) : elem_block(lane + 64 * wave);
+                const uint32_t ctab_w = CTAB0 + 16384u * (uint32_t)(wave & 1);
+                if (open && a256)
+                    mw_record<14, true, true>(lds, wave, lane, lb_aes, ctab_w, tab, rec, in, aad, out, result, slots, basis, supp, hp_slots, 1, mask, mine, ivo);
+                else if (open)
+                    mw_record<10, true, true>(lds, wave, lane, lb_aes, ctab_w, tab, rec, in, aad, out, result, slots, basis, supp, hp_slots, 1, mask, mine, ivo);
+                else if (a256)
+                    mw_record<14, false, true>(lds, wave, lane, lb_aes, ctab_w, tab, rec, in, aad, out, result, slots, basis, supp, hp_slots, 1, mask, mine, ivo);
+                else
+                    mw_record<10, false, true>(lds, wave, lane, lb_aes, ctab_w, tab, rec, in, aad, out, result, slots, basis, supp, hp_slots, 1, mask, mine, ivo);
+            } else if (wave == 1) {
+                {
+                    /* the record's first two elements per lane, as the launched single-record kernel reads them */
+                    V4 pre[2];
+                    if (flags & WREQ_INLINE) {
+                        pre[0] = pin0;
+                        pre[1] = pin1;
+                    } else {
+                        pre[0] = elem_block(lane);
+                        pre[1] = elem_block(lane + 64);
+                    }
+                    const uint32_t ctab = CTAB0;
+                    if (open && a256)
+                        sparse_record<14, true, true, true>(lds, lane, lb_aes, tab, rec, 0, in, aad, out, result, slots, basis, supp,
+                                                            hp_slots, 1, mask, true, pre, wclk, WORKER_STAMPS, false, pa, ctab, 0, 0, ivo);
+                    else if (open)
+                        sparse_record<10, true, true, true>(lds, lane, lb_aes, tab, rec, 0, in, aad, out, result, slots, basis, supp,
+                                                            hp_slots, 1, mask, true, pre, wclk, WORKER_STAMPS, false, pa, ctab, 0, 0, ivo);
+                    else if (a256)
+                        sparse_record<14, false, true, true>(lds, lane, lb_aes, tab, rec, 0, in, aad, out, result, slots, basis, supp,
+                                                             hp_slots, 1, mask, true, pre, wclk, WORKER_STAMPS, false, pa, ctab, 0, 0, ivo);
+                    else
+                        sparse_record<10, false, true, true>(lds, lane, lb_aes, tab, rec, 0, in, aad, out, result, slots, basis, supp,
+                                                             hp_slots, 1, mask, true, pre, wclk, WORKER_STAMPS, false, pa, ctab, 0, 0, ivo);
+                }
+            }
+            /* the wave holding the tag (wave 1 of a one- or two-wave record, pair 1's tag wave of a long one): every store of
+             * the call reaches system scope before its completion word (the other waves released theirs before the barrier
+             * that handed their sums over) */
+            if (wave == (longrec ? 2 + (((n1 - 1 - n1b) & 127) >> 6) : 1)) {
+                if (WORKER_STAMPS) {
+                    st[3] = worker_stamp();
+                    const uint64_t t = __builtin_amdgcn_s_memtime();
+                    if (lane == 0)
+                        wclk[9] = t;
+                }
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-            }
-            if (lane == 0) {
-                __hip_atomic_store(done, done_seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                __hip_atomic_store(&ms->served, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+                if (WORKER_STAMPS) {
+                    st[4] = worker_stamp();
+                    if (lane < 5)
+                        __hip_atomic_store(&ms->stamps[lane], lane == 0 ? st[0] : lane == 1 ? st[1] : lane == 2 ? st[2] : lane == 3 ? st[3] : st[4],
+                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+                }
+                if (lane == 0) {
+                    __hip_atomic_store(done, done_seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    __hip_atomic_store(&ms->served, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+                }
             }
         }
-        __syncthreads(); /* both waves are done with the request (its LDS tables, the verdict slot) */
+        __syncthreads(); /* every wave is done with the request (its LDS tables, the verdict slot, the request's copy) */
         last = seq;
         t_last = __builtin_amdgcn_s_memrealtime();
         if (threadIdx.x == 0)

@@ -1,8 +1,8 @@
 """Single-record plugin calls at every size around the two-wave record (sparse_kernel.hip mw_record: 65..128 GHASH
-elements go to two waves, one element per lane; fewer stay on one wave; more run on two waves at stride 128,
-sparse_record S = 128), through the reference's own picotls (ptls_aead_new_direct / ptls_aead_encrypt / ptls_aead_decrypt /
+elements go to two waves, one element per lane; fewer stay on one wave; more run on two pairs of waves at stride 128,
+sparse_record S = 128, each pair on its own part of the record), through the reference's own picotls (ptls_aead_new_direct / ptls_aead_encrypt / ptls_aead_decrypt /
 ptls_aead_encrypt_s, tests/plugin_driver.py) and compared with lib/fusion.c (oracle/_ref) in the same process: every GHASH
-length N from 60 to 134 with AADs of 0 to 3 blocks, and long records of 2 000 B to 17 KB with AADs of up to 7 blocks, both
+length N from 60 to 134 with AADs of 0 to 3 blocks, and long records of 2 000 B to 17 KB with AADs of up to 128 blocks, both
 key sizes, seal, open, a tampered tag or ciphertext, and QUIC header protection fused into the call.  Each case runs in its
 own process, with the resident worker (default) and with one launch per call (PTLS_HIP_PLUGIN_WORKER=0)."""
 import os
@@ -53,10 +53,12 @@ for bits in (128, 256):
                     out, supp = drv.encrypt_s(enc, pt, seq, aad, cctx, L % 4)
                     assert (out, supp) == ref.seal_supp(key, iv, seq, aad, pt, hp_key, L % 4), ("supp", bits, A, N, L)
                 calls += 1
-    # long records: two waves at stride 128 (sparse_record S = 128), around the 128-element switch and up to TLS's 16 KiB
-    for A in (0, 5, 13, 100):
-        for L in (2000, 2015, 2016, 2017, 2047, 2048, 2049, 3000, 4095, 4096, 4097, 8191, 8192, 10007, 16383, 16384,
-                  16385, int(rng.integers(2100, 17000))):
+    # long records: two pairs of waves at stride 128 (sparse_record S = 128, SPLIT), around the 128-element switch, where
+    # pair 1's part grows by 128 elements (N = 255 / 256 / 511 / 512), up to TLS's 16 KiB, and an AAD long enough to
+    # reach into pair 1's part
+    for A in (0, 5, 13, 100, 2048):
+        for L in ((2000, 2015, 2016, 2017, 2047, 2048, 2049, 3000, 4064, 4080, 4095, 4096, 4097, 8160, 8176, 8191, 8192, 10007,
+                   16383, 16384, 16385, int(rng.integers(2100, 17000))) if A < 2048 else (0, 1, 100, 2100, 14000)):
             seq = int(rng.integers(0, 2 ** 40))
             pt, aad = rnd(L), rnd(A)
             ct = drv.encrypt(enc, pt, seq, aad)
@@ -65,8 +67,9 @@ for bits in (128, 256):
             bad = bytearray(ct)
             bad[L // 2] ^= 0x01
             assert drv.decrypt(dec, bytes(bad), seq, aad) is None, ("tamper long", bits, A, L)
-            out, supp = drv.encrypt_s(enc, pt, seq, aad, cctx, L - 16)
-            assert (out, supp) == ref.seal_supp(key, iv, seq, aad, pt, hp_key, L - 16), ("supp long", bits, A, L)
+            if L >= 16:
+                out, supp = drv.encrypt_s(enc, pt, seq, aad, cctx, L - 16)
+                assert (out, supp) == ref.seal_supp(key, iv, seq, aad, pt, hp_key, L - 16), ("supp long", bits, A, L)
             calls += 1
     drv.cipher_free(cctx)
     drv.free(enc)
