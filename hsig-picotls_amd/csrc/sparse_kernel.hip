@@ -215,9 +215,11 @@ __device__ __forceinline__ void sparse_record(uint8_t *lds, int lane, uint32_t l
      * (keysetup's list); wave 0's sum joins wave 1's through LDS (xslot) after a workgroup barrier, and the wave holding
      * the length block (q = 0) writes the tag.  Every element index below goes through vl and S.
      * SPLIT (S = 128, a long record on four waves): two such pairs, each on its own part of the record, elements
-     * [e0, hi_split): pair 0 takes [0, N - 128 k), pair 1 the last 128 k elements, so each lane's sum is weighted from the
-     * end of its own part (q = (hi - 1 - e0 - vl) mod 128).  Pair 0's sum is then multiplied by H^(128 k) (k Horner steps
-     * with the H^128 table) and handed to pair 1's tag wave through LDS (xsplit) after a second workgroup barrier. */
+     * [e0, hi_split): pair 0 takes [0, P), pair 1 [P, N).  A lane's last element e is N - e elements from the end:
+     * q_l + 1 + D with q_l = (hi - 1 - e0 - vl) mod 128 its distance from the end of its part and D = N - hi = 128 k + r
+     * (0 in pair 1).  The lane weighs its sum by H^(((q_l + r) mod 128) + 1), times H^128 when q_l + r >= 128 (folded
+     * into its combination table, built once the H^128 table exists); pair 0's combined sum then takes k Horner steps with the H^128 table and goes to pair 1's tag wave
+     * through LDS (xsplit) after a second workgroup barrier. */
     static_assert(S == 64 || S == 128, "stride: one or two waves");
     constexpr int LOG2S = S == 64 ? 6 : 7;
     constexpr bool by_value = BYVAL;
@@ -257,7 +259,10 @@ __device__ __forceinline__ void sparse_record(uint8_t *lds, int lane, uint32_t l
     /* a single record (the plugin's launch): the H^64 basis loads go out before the counter-mode constants, so their
      * memory latency overlaps that LDS chain (in batches other waves hide it; there the early loads cost c4s open
      * 2.5 %, measured) */
-    const int q = (hi - 1 - vle) & (S - 1);
+    const int ql = (hi - 1 - vle) & (S - 1);
+    const int rsp = SPLIT ? (N - hi) & (S - 1) : 0;  /* r above (0 in pair 1 and without SPLIT) */
+    const int q = (ql + rsp) & (S - 1);
+    const bool qwrap = SPLIT && ql + rsp >= S;     /* the lane's extra H^128 step */
     /* batch records: the lane's first AAD block is loaded here, before the counter-mode constants and the H^64 table, so
      * its latency runs under that work (c4s seal 498-504 -> 513-519 GiB/s, profiles/r04_c4s_prefetch_ab.log) */
     V4 aad_pf = V4{0, 0, 0, 0};
@@ -267,6 +272,17 @@ __device__ __forceinline__ void sparse_record(uint8_t *lds, int lane, uint32_t l
     else if (!BYVAL && vl < na)
         aad_pf = load_block<ALIGNED>(aad_p + 16 * vl, min(16, A - 16 * vl));
     (void)aad_pf;
+    /* SPLIT, pair 1 (no AAD block, nothing read with the request): its first two stretch blocks go out before the
+     * counter-mode constants and the tables, as pair 0's came with the request */
+    const bool spre = SPLIT && !prefetch && (SPLIT ? e0 : 0) >= na;
+    V4 pre1[2] = {V4{0, 0, 0, 0}, V4{0, 0, 0, 0}};
+    if (spre) {
+        const int lastc1 = min(min((L - (tflag ? 1 : 0)) >> 4, 65534) - 1, hi - 1 - na);
+#pragma unroll
+        for (int k = 0; k < 2; ++k)
+            if (vle - na + S * k <= lastc1)
+                pre1[k] = load_full(in_p + 16 * (size_t)(vle - na + S * k));
+    }
     /* a single record builds its lane-combination table (the 16 multiples of H^(q+1)) early, in an LDS area of its own
      * (ctab), so that only the lookups remain after its last element */
     constexpr bool early_win = BYVAL;
@@ -285,7 +301,7 @@ __device__ __forceinline__ void sparse_record(uint8_t *lds, int lane, uint32_t l
     cc.k23 = __builtin_amdgcn_readfirstlane(cc.k23);
     cc.r03 = __builtin_amdgcn_readfirstlane(cc.r03);
     Win4<16> w4{};
-    if (early_win)
+    if (early_win && !SPLIT)
         w4 = gf_win4_build<16>(lds, ctab, lane, V4{hpe.x, hpe.y, hpe.z, hpe.w});
     (void)w4, (void)ctab;
     phase_stamp(clk, stamps, lane, 2);
@@ -297,6 +313,11 @@ __device__ __forceinline__ void sparse_record(uint8_t *lds, int lane, uint32_t l
         store_wave_table(lds, tab, b, lane);
     }
     wave_lds_sync();
+    if (early_win && SPLIT) { /* the lane's power times H^128 where q_l + r wrapped (the H^128 table exists now) */
+        const V4 hp = V4{hpe.x, hpe.y, hpe.z, hpe.w}, hs = gh_mul_nibble(lds, tab, hp);
+        w4 = gf_win4_build<16>(lds, ctab, lane, qwrap ? hs : hp);
+        wave_lds_sync();
+    }
     phase_stamp(clk, stamps, lane, 3);
     phase_acc(pa, bstamps, 3);
 
@@ -415,7 +436,7 @@ __device__ __forceinline__ void sparse_record(uint8_t *lds, int lane, uint32_t l
          * iteration into one buffer (8 VGPRs fewer: the seal instantiations stay within 168 without scratch). */
 #pragma unroll
         for (int b = 0; b < KP; ++b)
-            bufA[b] = load_full(src + 16 * S * b);
+            bufA[b] = spre && b < 2 ? pre1[b < 2 ? b : 0] : load_full(src + 16 * S * b);
         auto pure_iter = [&](int it, bool hash_pending, V4(&d)[KP], V4(&dn)[KP]) __attribute__((always_inline)) {
             const size_t o = (size_t)it * KP * 16 * S;
             const size_t on = (size_t)min(it + 1, npure - 1) * KP * 16 * S;
@@ -1079,7 +1100,11 @@ __global__ void __launch_bounds__(WORKER_WG)
             /* a long record on two pairs of waves at stride 128 (sparse_record S = 128, SPLIT): pair 1 takes the last 128 k
              * elements, about half */
             const bool longrec = !ecb && n1 > MW_MAX_N;
-            const int n1b = n1 - 128 * max(1, n1 >> 8); /* where pair 1's part starts */
+            /* where pair 1's part starts: pair 0 takes the AAD blocks and about 5/8 of the data blocks, a multiple of 128 (so
+             * its lanes hold as many); pair 1 starts a request read later (it waits for wave 1's copy) and has no elements
+             * read with the request.  16 KiB, same box: an even split 22.3 / 21.6 us seal / open, 5/8 21.1 / 21.3, 3/4
+             * 21.1-22.3 / 21.2-21.6, 3/8 24.3 / 24.4 (profiles/r06_plugin/plugin_ab_split_point*.log) */
+            const int n1b = na1 + min(nc1, 128 * max(1, (5 * nc1 + 512) >> 10));
             if (wave == 1) {
                 if (lane < (int)(sizeof(WorkerReq) / 16))
                     lds128_store(lds, RQ + 16u * (uint32_t)lane, rqc);

@@ -54,8 +54,8 @@ for bits in (128, 256):
                     assert (out, supp) == ref.seal_supp(key, iv, seq, aad, pt, hp_key, L % 4), ("supp", bits, A, N, L)
                 calls += 1
     # long records: two pairs of waves at stride 128 (sparse_record S = 128, SPLIT), around the 128-element switch, where
-    # pair 1's part grows by 128 elements (N = 255 / 256 / 511 / 512), up to TLS's 16 KiB, and an AAD long enough to
-    # reach into pair 1's part
+    # pair 0's part grows by 128 data blocks (N = 255 / 256 / 511 / 512), up to TLS's 16 KiB, and a 128-block AAD (pair 0's
+    # part all AAD, pair 1's down to the length block)
     for A in (0, 5, 13, 100, 2048):
         for L in ((2000, 2015, 2016, 2017, 2047, 2048, 2049, 3000, 4064, 4080, 4095, 4096, 4097, 8160, 8176, 8191, 8192, 10007,
                    16383, 16384, 16385, int(rng.integers(2100, 17000))) if A < 2048 else (0, 1, 100, 2100, 14000)):
